@@ -1,0 +1,128 @@
+/*
+ * seriation.h -- C ABI of libseriation.so, the MI355X-native drop-in for the reference's
+ * per-chain MCMC sweep (PrayagS/Seriation-in-Paleontological-Data-using-MCMC,
+ * C_Implementation/mcmc.c).  Plain C types only; caller-owned buffers; every function
+ * returns SR_OK (0) or a negative SR_E* code -- the library never calls exit().
+ *
+ * Reference interfaces replaced (file:line in the reference tree):
+ *   sr_parse_dataset / sr_load_dataset   mcmc_readmodel            mcmc.c:339-437, mcmc.h:47
+ *   sr_run_chains / sr_session_*         mcmc_init + mcmc_randomize + mcmc_sample loop
+ *                                         mcmc.c:127-185, 214-258, 477-593, mcmc.h:48,51,55
+ *   sr_chain_summary.exp_*               compute_exp_data / print_exp_data  mcmc.c:53-67
+ *   sr_record / sink                     mcmc_save_chain           mcmc.c:69-92
+ *   sr_run_to_dirs                       main()'s Chains/chain_XX/<name>.csv output  mcmc.c:148-197, 261-293
+ *   sr_chain_summary.consistent          mcmc_consistent           mcmc.c:999-1094, 199-204
+ *   sr_chain_spec.seed                   GSL_RNG_SEED via gsl_rng_env_setup  mcmc.c:591 / script.py:42
+ * A chain's trajectory depends only on (dataset, seed): sharding chains over devices or
+ * sessions never changes any chain's output.
+ */
+#ifndef SERIATION_H
+#define SERIATION_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SR_OK 0
+#define SR_EINVAL (-1)         /* bad argument */
+#define SR_EPARSE (-2)         /* "mcmc_readmodel: read error." (mcmc.c:349, 371) */
+#define SR_EHEADER (-3)        /* "mcmc_readmodel: read error at header." (mcmc.c:355) */
+#define SR_ENOMEM (-4)
+#define SR_EDEVICE (-5)        /* HIP runtime error or no gfx950 device */
+#define SR_EUNSUPPORTED (-6)   /* configuration outside the kernel's limits */
+#define SR_EIO (-7)            /* cannot open/write an output file */
+#define SR_EINCONSISTENT (-8)  /* mcmc_consistent failed after the run (mcmc.c:199-204) */
+
+#define SR_MAXS 2000           /* mcmc.h:25 line limit of the reference parser */
+
+typedef struct {
+  int32_t N, M, nh;   /* sites, taxa, hard sites */
+  uint8_t *X;         /* N*M, row-major (row = site), 0/1 */
+  uint8_t *hard;      /* N, 1 if the row ended with '*' */
+} sr_dataset;
+
+/* maxs = SR_MAXS reproduces the reference's fgets(MAXS) semantics exactly (a longer line
+ * is split and its tail read as the next row); maxs = 0 reads lines of any length. */
+int sr_parse_dataset(const char *text, size_t len, int32_t maxs, sr_dataset *out);
+int sr_load_dataset(const char *path, int32_t maxs, sr_dataset *out);
+void sr_free_dataset(sr_dataset *ds);
+
+typedef struct {
+  int32_t chain_id;   /* names the output directory Chains/chain_NN */
+  uint64_t seed;      /* GSL_RNG_SEED value (0 -> GSL default 4357) */
+} sr_chain_spec;
+
+typedef struct {
+  int32_t burnin_calls;      /* tb: mcmc_sample calls before saving (mcmc.c:107, default 1000) */
+  int32_t sample_calls;      /* ts: saved mcmc_sample calls (default 1000) */
+  int32_t sweeps_per_call;   /* sweeps per mcmc_sample (mcmc.c:225, default 10) */
+  int32_t manycd;            /* 0 only: the reference CLI cannot reach manycd=1 */
+  int32_t device;            /* HIP device ordinal */
+  int32_t block_threads;     /* threads per chain workgroup, 0 = auto */
+  int32_t calls_per_launch;  /* mcmc_sample calls per kernel launch, 0 = auto */
+  int32_t flags;             /* SR_F_* */
+} sr_run_opts;
+#define SR_F_NO_CHECK 1      /* skip the closing mcmc_consistent check */
+
+typedef struct {
+  int32_t chain_id;
+  int32_t consistent;        /* 0 = mcmc_consistent passed (as the reference's exit 0) */
+  double exp_loglik, exp_c, exp_d;   /* exactly print_exp_data's values (sums / 1000) */
+} sr_chain_summary;
+
+typedef struct {
+  int32_t N, M;
+  const int32_t *a, *b, *pi;  /* M, M, N: one mcmc_save_chain line */
+  double c, d, loglik;        /* log P(false 1), log P(false 0) (all taxa share them), loglik */
+} sr_record;
+
+/* Called once per saved sample, per chain in sample order; return nonzero to abort. */
+typedef int (*sr_sample_sink_fn)(void *ctx, int32_t chain_index, int32_t sample_index,
+                                 const sr_record *rec);
+
+void sr_default_opts(sr_run_opts *o);
+
+/* Run n_chains independent chains on one GPU (opts->device), burn-in then sampling;
+ * per-sample records go to sink (may be NULL); out[n_chains] receives the summaries. */
+int sr_run_chains(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n_chains,
+                  const sr_run_opts *opts, sr_sample_sink_fn sink, void *sink_ctx,
+                  sr_chain_summary *out);
+
+/* Same run, writing Chains/chain_NN/{chain_data,exp_data,taxa,sites,hard_sites}.csv
+ * under chains_root byte-for-byte as the reference's main() does. */
+int sr_run_to_dirs(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n_chains,
+                   const sr_run_opts *opts, const char *chains_root, sr_chain_summary *out);
+
+/* ---- sessions: chains resident in HBM on one GPU, asynchronous launches ---- */
+typedef struct sr_session sr_session;
+int sr_session_create(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n_chains,
+                      const sr_run_opts *opts, sr_session **out);
+/* Launch on a caller-owned hipStream_t (e.g. torch.cuda.current_stream().cuda_stream). */
+int sr_session_set_stream(sr_session *s, void *hip_stream);
+/* Enqueue `calls` mcmc_sample calls for every chain; save != 0 appends one record per call. */
+int sr_session_run(sr_session *s, int32_t calls, int32_t save);
+int sr_session_sync(sr_session *s);
+int32_t sr_session_records(const sr_session *s);
+int32_t sr_session_record_capacity(const sr_session *s);
+/* ab_pi: [n_chains][count][2M+N] int16 (a, b, pi); cdl: [n_chains][count][3] (c, d, loglik) */
+int sr_session_fetch_records(sr_session *s, int32_t first, int32_t count, int16_t *ab_pi, double *cdl);
+int sr_session_reset_records(sr_session *s);
+/* Current state of one chain (any pointer may be NULL); counts = t0,f0,t1,f1 (4*M). */
+int sr_session_state(sr_session *s, int32_t chain, int32_t *a, int32_t *b, int32_t *pi,
+                     double *c_d_loglik, int32_t *counts);
+/* Acceptance counters cc, cd, cab, cpi1, cpi20, cpi21, cpi3 (mcmc.c:220). */
+int sr_session_accept_counts(sr_session *s, int32_t chain, int64_t *acc7);
+/* Device time of the last sr_session_run (ms, HIP events on the session stream; syncs). */
+double sr_session_last_kernel_ms(sr_session *s);
+int32_t sr_session_block_threads(const sr_session *s);
+void sr_session_destroy(sr_session *s);
+
+const char *sr_strerror(int code);
+int sr_device_count(void);
+const char *sr_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,180 @@
+/*
+ * oracle/om_gsl.h -- TEST INFRASTRUCTURE ONLY (CPU oracle).  Never linked into the product.
+ *
+ * Restatement of the parts of the GNU Scientific Library 2.6 that the reference
+ * sampler calls (GSL is an external dependency of /root/reference, not vendored:
+ * `readelf -d mcmc` -> libgsl.so.25 = GSL 2.6).  Published algorithms restated:
+ *
+ *   rng/mt.c            mt19937: Knuth seeding (s==0 -> 4357), 624-word twist, tempering
+ *   gsl_rng.h           gsl_rng_uniform      = get()/2^32
+ *                       gsl_rng_uniform_pos  = uniform() until != 0
+ *                       gsl_rng_uniform_int  = get()/(0xffffffff/n), reject >= n
+ *   randist/shuffle.c   gsl_ran_shuffle      (i = n-1..1, swap(i, uniform_int(i+1)))
+ *                       gsl_ran_choose       (take src[i] iff (n-i)*uniform() < k-j)
+ *   randist/gausszig.c  gsl_ran_gaussian_ziggurat (128 strips, R = 3.44428647676)
+ *   randist/gamma.c     gsl_ran_gamma        (Marsaglia-Tsang; a<1 boost branch)
+ *   randist/beta.c      gsl_ran_beta         = X/(X+Y), X~Gamma(a), Y~Gamma(b)
+ *
+ * Reference call sites: mcmc.c:489, 519, 548 (init), 591-592 (setup), 757 (beta),
+ * 909 (randompick), 1140-1141, 1261, 1325-1326, 1340, 1360-1361, 1441, 1505-1506,
+ * 1561-1562, 1636 (proposals).
+ *
+ * Parity status: mt19937 / uniform / uniform_int / shuffle / choose are pinned by
+ * tests against numpy.random.RandomState (same init_genrand recurrence).  The gamma /
+ * ziggurat stream is pinned only through the regenerated tables (tools/gen_tables.py
+ * reproduces the published ytab/ktab/wtab head values); GSL itself is absent here.
+ * libm exp/log are replaced by om_exp/om_log (om_libm.h).
+ */
+#ifndef OM_GSL_H
+#define OM_GSL_H
+#include <stdint.h>
+#include <stddef.h>
+#include <string.h>
+#include "om_libm.h"
+
+#define OM_MT_N 624
+#define OM_MT_M 397
+
+typedef struct {
+  uint32_t mt[OM_MT_N];
+  int mti;
+  uint64_t ndraw; /* words drawn so far (diagnostic) */
+} om_rng;
+
+static inline void om_rng_seed(om_rng *r, unsigned long s)
+{
+  if (s == 0) s = 4357;
+  r->mt[0] = (uint32_t)(s & 0xffffffffUL);
+  for (int i = 1; i < OM_MT_N; i++) {
+    uint32_t p = r->mt[i - 1];
+    r->mt[i] = (uint32_t)(1812433253UL * (p ^ (p >> 30)) + (unsigned long)i);
+  }
+  r->mti = OM_MT_N;
+  r->ndraw = 0;
+}
+
+static inline uint32_t om_rng_get(om_rng *r)
+{
+  uint32_t *mt = r->mt;
+  if (r->mti >= OM_MT_N) {
+    int kk;
+    for (kk = 0; kk < OM_MT_N; kk++) {
+      uint32_t y = (mt[kk] & 0x80000000u) | (mt[(kk + 1) % OM_MT_N] & 0x7fffffffu);
+      uint32_t v = mt[(kk + OM_MT_M) % OM_MT_N] ^ (y >> 1);
+      if (y & 1u) v ^= 0x9908b0dfu;
+      mt[kk] = v;
+    }
+    r->mti = 0;
+  }
+  uint32_t k = mt[r->mti++];
+  k ^= (k >> 11);
+  k ^= (k << 7) & 0x9d2c5680u;
+  k ^= (k << 15) & 0xefc60000u;
+  k ^= (k >> 18);
+  r->ndraw++;
+  return k;
+}
+
+static inline double om_uniform(om_rng *r) { return om_rng_get(r) / 4294967296.0; }
+
+static inline double om_uniform_pos(om_rng *r)
+{
+  double x;
+  do { x = om_uniform(r); } while (x == 0);
+  return x;
+}
+
+static inline unsigned long om_uniform_int(om_rng *r, unsigned long n)
+{
+  unsigned long scale = 0xffffffffUL / n;
+  unsigned long k;
+  do { k = om_rng_get(r) / scale; } while (k >= n);
+  return k;
+}
+
+static inline void om_swap_bytes(void *base, size_t size, size_t i, size_t j)
+{
+  unsigned char *a = (unsigned char *)base + size * i, *b = (unsigned char *)base + size * j;
+  for (size_t s = 0; s < size; s++) { unsigned char t = a[s]; a[s] = b[s]; b[s] = t; }
+}
+
+static inline void om_shuffle(om_rng *r, void *base, size_t n, size_t size)
+{
+  for (size_t i = n - 1; i > 0; i--) {
+    size_t j = om_uniform_int(r, i + 1);
+    om_swap_bytes(base, size, i, j);
+  }
+}
+
+static inline int om_choose(om_rng *r, void *dest, size_t k, const void *src, size_t n, size_t size)
+{
+  size_t i, j = 0;
+  if (k > n) return -1;
+  for (i = 0; i < n && j < k; i++) {
+    if ((double)(n - i) * om_uniform(r) < (double)(k - j)) {
+      memcpy((char *)dest + size * j, (const char *)src + size * i, size);
+      j++;
+    }
+  }
+  return 0;
+}
+
+static inline double om_gaussian_ziggurat(om_rng *r, double sigma)
+{
+  unsigned long i, j;
+  int sign;
+  double x, y;
+  for (;;) {
+    unsigned long k = om_rng_get(r);
+    i = k & 0xFF;
+    j = (k >> 8) & 0xFFFFFF;
+    sign = (i & 0x80) ? +1 : -1;
+    i &= 0x7f;
+    x = j * om_zig_wtab[i];
+    if (j < om_zig_ktab[i]) break;
+    if (i < 127) {
+      double y0 = om_zig_ytab[i], y1 = om_zig_ytab[i + 1];
+      double U1 = om_uniform(r);
+      y = y1 + (y0 - y1) * U1;
+    } else {
+      double U1 = 1.0 - om_uniform(r);
+      double U2 = om_uniform(r);
+      x = OM_ZIG_R - om_log(U1) / OM_ZIG_R;
+      y = om_exp(-OM_ZIG_R * (x - 0.5 * OM_ZIG_R)) * U2;
+    }
+    if (y < om_exp(-0.5 * x * x)) break;
+  }
+  return sign * sigma * x;
+}
+
+static inline double om_gamma(om_rng *r, double a, double b)
+{
+  if (a < 1) {
+    /* GSL boost: gamma(1+a) * pow(u, 1/a).  Unreachable from the sampler (a = 1 + count). */
+    double u = om_uniform_pos(r);
+    return om_gamma(r, 1.0 + a, b) * om_exp(om_log(u) * (1.0 / a));
+  }
+  double x, v, u;
+  double d = a - 1.0 / 3.0;
+  double c = (1.0 / 3.0) / __builtin_sqrt(d);
+  for (;;) {
+    do {
+      x = om_gaussian_ziggurat(r, 1.0);
+      v = 1.0 + c * x;
+    } while (v <= 0);
+    v = v * v * v;
+    u = om_uniform_pos(r);
+    if (u < 1 - 0.0331 * x * x * x * x) break;
+    if (om_log(u) < 0.5 * x * x + d * (1 - v + om_log(v))) break;
+  }
+  return b * d * v;
+}
+
+static inline double om_beta(om_rng *r, double a, double b)
+{
+  double x1 = om_gamma(r, a, 1.0);
+  double x2 = om_gamma(r, b, 1.0);
+  return x1 / (x1 + x2);
+}
+
+#endif

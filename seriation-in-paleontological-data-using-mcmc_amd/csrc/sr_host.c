@@ -1,0 +1,717 @@
+/*
+ * sr_host.c -- C host layer of libseriation.so (implements include/seriation.h).
+ *
+ * Responsibilities (reference file:line in C_Implementation/mcmc.c):
+ *   parsing                 mcmc_readmodel            :339-437  (fgets(MAXS) semantics)
+ *   chain initialisation    mcmc_init/initab/randomize/count01/logl  :440-593, 625-708
+ *   device state build      P columns in position order, hard positions, MT ring
+ *   run loop                main()'s burn-in + sampling loops  :140-185 (on the GPU)
+ *   summaries               compute_exp_data/print_exp_data    :53-67
+ *   consistency             mcmc_consistent                    :999-1094
+ *   output files            mcmc_save_chain / mcmc_save         :69-92, 261-293
+ * The sweep itself runs only in sr_device.hip; there is no CPU fallback: without a
+ * usable gfx950 device every run entry point returns SR_EDEVICE.
+ */
+#define _GNU_SOURCE
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdint.h>
+#include <math.h>
+#include <errno.h>
+#include <sys/stat.h>
+#include <sys/types.h>
+#include "seriation.h"
+#include "sr_internal.h"
+#include "sr_math.h"
+#include "sr_rng.h"
+
+#define SR_API __attribute__((visibility("default")))
+
+static const sr_mtab SR_HOST_TAB = {sr_exp_thi, sr_exp_tlo, sr_log_invc, sr_log_lhi, sr_log_llo};
+static double h_exp(double x) { return sr_exp_m(x, &SR_HOST_TAB); }
+static double h_log(double x) { return sr_log_m(x, &SR_HOST_TAB); }
+
+SR_API const char *sr_version(void) { return "seriation-mi355x 0.1"; }
+
+SR_API const char *sr_strerror(int code)
+{
+  switch (code) {
+  case SR_OK: return "ok";
+  case SR_EINVAL: return "invalid argument";
+  case SR_EPARSE: return "mcmc_readmodel: read error.";
+  case SR_EHEADER: return "mcmc_readmodel: read error at header.";
+  case SR_ENOMEM: return "out of memory";
+  case SR_EDEVICE: return "HIP device error (no usable gfx950 device?)";
+  case SR_EUNSUPPORTED: return "configuration not supported by the kernel";
+  case SR_EIO: return "cannot open or write an output file";
+  case SR_EINCONSISTENT: return "mcmc_consistent: inconsistent chain state";
+  default: return "unknown error";
+  }
+}
+
+SR_API int sr_device_count(void) { return srk_device_count(); }
+
+/* ------------------------------------------------------------------ parsing */
+
+/* one fgets(s, maxs, f) over the buffer; returns line length or -1 at EOF */
+static long next_line(const char *text, size_t len, size_t *off, int maxs, char **buf, size_t *cap)
+{
+  if (*off >= len) return -1;
+  size_t lim = maxs > 0 ? (size_t)maxs - 1 : (size_t)-1, n = 0;
+  while (*off < len && n < lim) {
+    char ch = text[(*off)++];
+    if (n + 2 > *cap) {
+      *cap = *cap * 2 + 256;
+      char *nb = (char *)realloc(*buf, *cap);
+      if (!nb) return -2;
+      *buf = nb;
+    }
+    (*buf)[n++] = ch;
+    if (ch == '\n') break;
+  }
+  (*buf)[n] = '\0';
+  return (long)n;
+}
+
+SR_API void sr_free_dataset(sr_dataset *ds)
+{
+  if (!ds) return;
+  free(ds->X);
+  free(ds->hard);
+  memset(ds, 0, sizeof(*ds));
+}
+
+SR_API int sr_parse_dataset(const char *text, size_t len, int32_t maxs, sr_dataset *out)
+{
+  if (!text || !out) return SR_EINVAL;
+  memset(out, 0, sizeof(*out));
+  size_t off = 0, cap = 256;
+  char *s = (char *)malloc(cap);
+  if (!s) return SR_ENOMEM;
+  long got = next_line(text, len, &off, maxs, &s, &cap);
+  if (got < 0) { free(s); return got == -2 ? SR_ENOMEM : SR_EPARSE; }
+  int n, m;
+  if (sscanf(s, "%d %d", &n, &m) != 2 || n <= 0 || m <= 0) { free(s); return SR_EHEADER; }
+  out->N = n; out->M = m; out->nh = 0;
+  out->X = (uint8_t *)calloc((size_t)n * m, 1);
+  out->hard = (uint8_t *)calloc((size_t)n, 1);
+  if (!out->X || !out->hard) { free(s); sr_free_dataset(out); return SR_ENOMEM; }
+  for (int i = 0; i < n; i++) {
+    got = next_line(text, len, &off, maxs, &s, &cap);
+    if (got < 0) { free(s); sr_free_dataset(out); return got == -2 ? SR_ENOMEM : SR_EPARSE; }
+    int k = 0;
+    for (int j = 0; j < m; j++) {
+      while (s[k] != '0' && s[k] != '1' && s[k] != '\0') k++;
+      if (s[k] == '0') { out->X[(size_t)i * m + j] = 0; k++; }
+      else if (s[k] == '1') { out->X[(size_t)i * m + j] = 1; k++; }
+    }
+    while (s[k] != '*' && s[k] != '\0') k++;
+    if (s[k] == '*') { out->hard[i] = 1; out->nh++; }
+  }
+  free(s);
+  return SR_OK;
+}
+
+SR_API int sr_load_dataset(const char *path, int32_t maxs, sr_dataset *out)
+{
+  FILE *f = fopen(path, "rb");
+  if (!f) return SR_EIO;
+  size_t cap = 1 << 16, len = 0, got;
+  char *t = (char *)malloc(cap);
+  if (!t) { fclose(f); return SR_ENOMEM; }
+  while ((got = fread(t + len, 1, cap - len, f)) > 0) {
+    len += got;
+    if (len == cap) {
+      cap *= 2;
+      char *nt = (char *)realloc(t, cap);
+      if (!nt) { free(t); fclose(f); return SR_ENOMEM; }
+      t = nt;
+    }
+  }
+  fclose(f);
+  int rc = sr_parse_dataset(t, len, maxs, out);
+  free(t);
+  return rc;
+}
+
+SR_API void sr_default_opts(sr_run_opts *o)
+{
+  memset(o, 0, sizeof(*o));
+  o->burnin_calls = 1000;
+  o->sample_calls = 1000;
+  o->sweeps_per_call = 10;
+}
+
+/* ------------------------------------------------------------ chain init */
+typedef struct {
+  int N, M, nh;
+  const uint8_t *X, *hard;
+  int32_t *pi, *rpi, *a, *b, *t0, *f0, *t1, *f1;
+  int t0a, f0a, t1a, f1a;
+  double c, d, loglik;
+} hmodel;
+
+static void h_initab(hmodel *x)                       /* mcmc_initab, mcmc.c:440-474 */
+{
+  for (int m = 0; m < x->M; m++) {
+    int n = 0;
+    while (n < x->N && !x->X[(size_t)x->rpi[n] * x->M + m]) n++;
+    if (n == x->N) { x->a[m] = 0; x->b[m] = x->N; }
+    else {
+      x->a[m] = n;
+      n = x->N - 1;
+      while (n >= 0 && !x->X[(size_t)x->rpi[n] * x->M + m]) n--;
+      x->b[m] = n + 1;
+    }
+  }
+}
+
+static void h_count01(hmodel *x)                      /* mcmc_count01, mcmc.c:651-708 */
+{
+  x->t0a = x->f0a = x->t1a = x->f1a = 0;
+  for (int m = 0; m < x->M; m++) {
+    int t0 = 0, f0 = 0, t1 = 0, f1 = 0;
+    for (int n = 0; n < x->N; n++) {
+      int v = x->X[(size_t)n * x->M + m];
+      if (x->a[m] <= x->pi[n] && x->pi[n] < x->b[m]) { if (v) t1++; else f0++; }
+      else { if (v) f1++; else t0++; }
+    }
+    x->t0a += t0; x->f0a += f0; x->t1a += t1; x->f1a += f1;
+    x->t0[m] = t0; x->f0[m] = f0; x->t1[m] = t1; x->f1[m] = f1;
+  }
+}
+
+static double h_logl(const hmodel *x)                 /* mcmc_logl, mcmc.c:625-648 */
+{
+  double loglik = 0.;
+  for (int m = 0; m < x->M; m++)
+    loglik += x->t0[m] * h_log(1. - h_exp(x->c)) + x->f0[m] * x->d + x->t1[m] * h_log(1. - h_exp(x->d)) + x->f1[m] * x->c;
+  return loglik;
+}
+
+/* mcmc_randomize (mcmc.c:477-578); the read of q[nh] past the end (:530) is guarded */
+static int h_randomize(hmodel *x, sr_hrng *r)
+{
+  const int N = x->N, nh = x->nh;
+  if (nh == 0) {
+    sr_hrng_shuffle(r, x->pi, (size_t)N);
+    for (int i = 0; i < N; i++) x->rpi[x->pi[i]] = i;
+    h_count01(x);
+    x->loglik = h_logl(x);
+    return 0;
+  } else if (nh == N) {
+    return 0;
+  }
+  int32_t *p = (int32_t *)malloc(N * sizeof(int32_t)), *q = (int32_t *)malloc(nh * sizeof(int32_t));
+  if (!p || !q) { free(p); free(q); return SR_ENOMEM; }
+  for (int i = 0; i < N; i++) p[i] = i;
+  sr_hrng_choose(r, q, (size_t)nh, p, (size_t)N);
+  int j = 0, k = 0;
+  for (int i = 0; i < N; i++) {
+    if (j < nh && i == q[j]) j++;
+    else p[k++] = i;
+  }
+  sr_hrng_shuffle(r, p, (size_t)(N - nh));
+  j = k = 0;
+  for (int i = 0; i < N; i++) x->pi[i] = x->hard[i] ? q[j++] : p[k++];
+  for (int i = 0; i < N; i++) x->rpi[x->pi[i]] = i;
+  free(p); free(q);
+  h_initab(x);
+  h_count01(x);
+  x->loglik = h_logl(x);
+  return 0;
+}
+
+static void hmodel_free(hmodel *x)
+{
+  free(x->pi); free(x->rpi); free(x->a); free(x->b);
+  free(x->t0); free(x->f0); free(x->t1); free(x->f1);
+}
+
+static int hmodel_alloc(hmodel *x, const sr_dataset *ds)
+{
+  memset(x, 0, sizeof(*x));
+  x->N = ds->N; x->M = ds->M; x->nh = ds->nh; x->X = ds->X; x->hard = ds->hard;
+  x->pi = (int32_t *)malloc(ds->N * 4); x->rpi = (int32_t *)malloc(ds->N * 4);
+  x->a = (int32_t *)malloc(ds->M * 4); x->b = (int32_t *)malloc(ds->M * 4);
+  x->t0 = (int32_t *)malloc(ds->M * 4); x->f0 = (int32_t *)malloc(ds->M * 4);
+  x->t1 = (int32_t *)malloc(ds->M * 4); x->f1 = (int32_t *)malloc(ds->M * 4);
+  if (!x->pi || !x->rpi || !x->a || !x->b || !x->t0 || !x->f0 || !x->t1 || !x->f1) { hmodel_free(x); return SR_ENOMEM; }
+  return SR_OK;
+}
+
+/* ---------------------------------------------------------------- sessions */
+struct sr_session {
+  sr_dataset ds;            /* private copy */
+  int nchains;
+  sr_chain_spec *specs;
+  sr_run_opts opts;
+  srk_dev *dev;
+  int rec_cap, nrec;
+};
+
+static void state_free(sr_state_host *st)
+{
+  free(st->P); free(st->rpi); free(st->hp); free(st->ab); free(st->cnt);
+  free(st->cdl); free(st->mt); free(st->rng); free(st->acc);
+  memset(st, 0, sizeof(*st));
+}
+
+static int state_alloc(sr_state_host *st, int N, int M, int nh, int C)
+{
+  memset(st, 0, sizeof(*st));
+  st->N = N; st->M = M; st->NW = (N + 31) / 32; st->nh = nh; st->nchains = C;
+  st->P = (uint32_t *)calloc((size_t)C * st->NW * M, 4);
+  st->rpi = (int32_t *)calloc((size_t)C * N, 4);
+  st->hp = (int32_t *)calloc((size_t)C * SR_NHMAX, 4);
+  st->ab = (int32_t *)calloc((size_t)C * 2 * M, 4);
+  st->cnt = (int32_t *)calloc((size_t)C * 4 * M, 4);
+  st->cdl = (double *)calloc((size_t)C * 4, 8);
+  st->mt = (uint32_t *)calloc((size_t)C * SR_RING * SR_MT_N, 4);
+  st->rng = (uint64_t *)calloc((size_t)C * 2, 8);
+  st->acc = (uint64_t *)calloc((size_t)C * 8, 8);
+  if (!st->P || !st->rpi || !st->hp || !st->ab || !st->cnt || !st->cdl || !st->mt || !st->rng || !st->acc) {
+    state_free(st);
+    return SR_ENOMEM;
+  }
+  return SR_OK;
+}
+
+/* initialise one chain exactly as main() does before the burn-in (mcmc.c:127-135) */
+static int init_chain(const sr_dataset *ds, uint64_t seed, sr_state_host *st, int c)
+{
+  hmodel x;
+  int rc = hmodel_alloc(&x, ds);
+  if (rc) return rc;
+  const int N = ds->N, M = ds->M, NW = st->NW;
+  for (int i = 0; i < N; i++) x.pi[i] = x.rpi[i] = i;      /* mcmc.c:405-407 */
+  h_initab(&x);
+  x.c = h_log(.01);                                           /* mcmc.c:417-421 */
+  x.d = h_log(.3);
+  h_count01(&x);
+  x.loglik = h_logl(&x);
+  sr_hrng r;
+  sr_hrng_seed(&r, (unsigned long)seed);
+  rc = h_randomize(&x, &r);
+  if (rc) { hmodel_free(&x); return rc; }
+  /* device state */
+  uint32_t *P = st->P + (size_t)c * NW * M;
+  for (int p = 0; p < N; p++) {
+    const uint8_t *row = ds->X + (size_t)x.rpi[p] * M;
+    for (int m = 0; m < M; m++)
+      if (row[m]) P[(size_t)(p >> 5) * M + m] |= 1u << (p & 31);
+  }
+  memcpy(st->rpi + (size_t)c * N, x.rpi, N * 4);
+  int k = 0;
+  for (int s = 0; s < N; s++)
+    if (ds->hard[s]) st->hp[(size_t)c * SR_NHMAX + k++] = x.pi[s];
+  memcpy(st->ab + (size_t)c * 2 * M, x.a, M * 4);
+  memcpy(st->ab + (size_t)c * 2 * M + M, x.b, M * 4);
+  memcpy(st->cnt + (size_t)c * 4 * M, x.t0, M * 4);
+  memcpy(st->cnt + (size_t)c * 4 * M + M, x.f0, M * 4);
+  memcpy(st->cnt + (size_t)c * 4 * M + 2 * M, x.t1, M * 4);
+  memcpy(st->cnt + (size_t)c * 4 * M + 3 * M, x.f1, M * 4);
+  st->cdl[(size_t)c * 4 + 0] = x.c;
+  st->cdl[(size_t)c * 4 + 1] = x.d;
+  st->cdl[(size_t)c * 4 + 2] = x.loglik;
+  memcpy(st->mt + ((size_t)c * SR_RING + (r.bidx % SR_RING)) * SR_MT_N, r.blk, sizeof(r.blk));
+  st->rng[(size_t)c * 2 + 0] = r.pos;
+  st->rng[(size_t)c * 2 + 1] = r.bidx + 1;
+  hmodel_free(&x);
+  return SR_OK;
+}
+
+static int auto_calls_per_launch(const sr_run_opts *o)
+{
+  return o->calls_per_launch > 0 ? o->calls_per_launch : 100;
+}
+
+SR_API int sr_session_create(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n_chains,
+                             const sr_run_opts *opts, sr_session **out)
+{
+  if (!ds || !specs || n_chains <= 0 || !out || ds->N < 2 || ds->M < 1) return SR_EINVAL;
+  sr_run_opts o;
+  if (opts) o = *opts; else sr_default_opts(&o);
+  if (o.sweeps_per_call <= 0) return SR_EINVAL;
+  if (o.manycd != 0) return SR_EUNSUPPORTED;
+  if (ds->nh > SR_NHMAX || ds->N > 32767 || ds->M > 32767) return SR_EUNSUPPORTED;
+  sr_session *s = (sr_session *)calloc(1, sizeof(*s));
+  if (!s) return SR_ENOMEM;
+  s->ds.N = ds->N; s->ds.M = ds->M; s->ds.nh = ds->nh;
+  s->ds.X = (uint8_t *)malloc((size_t)ds->N * ds->M);
+  s->ds.hard = (uint8_t *)malloc((size_t)ds->N);
+  s->specs = (sr_chain_spec *)malloc(sizeof(sr_chain_spec) * n_chains);
+  if (!s->ds.X || !s->ds.hard || !s->specs) { sr_free_dataset(&s->ds); free(s->specs); free(s); return SR_ENOMEM; }
+  memcpy(s->ds.X, ds->X, (size_t)ds->N * ds->M);
+  memcpy(s->ds.hard, ds->hard, (size_t)ds->N);
+  memcpy(s->specs, specs, sizeof(sr_chain_spec) * n_chains);
+  s->nchains = n_chains;
+  s->opts = o;
+  sr_state_host st;
+  int rc = state_alloc(&st, ds->N, ds->M, ds->nh, n_chains);
+  if (rc) { sr_session_destroy(s); return rc; }
+  for (int c = 0; c < n_chains && rc == SR_OK; c++) rc = init_chain(ds, specs[c].seed, &st, c);
+  if (rc) { state_free(&st); sr_session_destroy(s); return rc; }
+  s->rec_cap = auto_calls_per_launch(&o);
+  rc = srk_create(&st, o.device, o.block_threads, s->rec_cap, &s->dev);
+  state_free(&st);
+  if (rc) { sr_session_destroy(s); return rc == -6 ? SR_EUNSUPPORTED : SR_EDEVICE; }
+  *out = s;
+  return SR_OK;
+}
+
+SR_API int sr_session_set_stream(sr_session *s, void *hip_stream)
+{
+  if (!s) return SR_EINVAL;
+  return srk_set_stream(s->dev, hip_stream) ? SR_EDEVICE : SR_OK;
+}
+
+SR_API int sr_session_run(sr_session *s, int32_t calls, int32_t save)
+{
+  if (!s || calls < 0) return SR_EINVAL;
+  if (save && s->nrec + calls > s->rec_cap) return SR_EINVAL;
+  int rc = srk_run(s->dev, calls, s->opts.sweeps_per_call, save ? 1 : 0, s->nrec);
+  if (rc) return rc == -1 ? SR_EINVAL : SR_EDEVICE;
+  if (save) s->nrec += calls;
+  return SR_OK;
+}
+
+SR_API int sr_session_sync(sr_session *s) { return (!s) ? SR_EINVAL : (srk_sync(s->dev) ? SR_EDEVICE : SR_OK); }
+SR_API int32_t sr_session_records(const sr_session *s) { return s ? s->nrec : 0; }
+SR_API int32_t sr_session_record_capacity(const sr_session *s) { return s ? s->rec_cap : 0; }
+SR_API int32_t sr_session_block_threads(const sr_session *s) { return s ? srk_block_threads(s->dev) : 0; }
+SR_API double sr_session_last_kernel_ms(sr_session *s) { return s ? srk_last_ms(s->dev) : -1.0; }
+
+SR_API int sr_session_fetch_records(sr_session *s, int32_t first, int32_t count, int16_t *ab_pi, double *cdl)
+{
+  if (!s || first < 0 || count < 0 || first + count > s->nrec) return SR_EINVAL;
+  return srk_fetch_records(s->dev, first, count, ab_pi, cdl) ? SR_EDEVICE : SR_OK;
+}
+
+SR_API int sr_session_reset_records(sr_session *s)
+{
+  if (!s) return SR_EINVAL;
+  s->nrec = 0;
+  return SR_OK;
+}
+
+static int download(sr_session *s, sr_state_host *st)
+{
+  int rc = state_alloc(st, s->ds.N, s->ds.M, s->ds.nh, s->nchains);
+  if (rc) return rc;
+  if (srk_download_state(s->dev, st)) { state_free(st); return SR_EDEVICE; }
+  return SR_OK;
+}
+
+SR_API int sr_session_state(sr_session *s, int32_t chain, int32_t *a, int32_t *b, int32_t *pi,
+                            double *cdl3, int32_t *counts)
+{
+  if (!s || chain < 0 || chain >= s->nchains) return SR_EINVAL;
+  sr_state_host st;
+  int rc = download(s, &st);
+  if (rc) return rc;
+  const int N = s->ds.N, M = s->ds.M;
+  if (a) memcpy(a, st.ab + (size_t)chain * 2 * M, M * 4);
+  if (b) memcpy(b, st.ab + (size_t)chain * 2 * M + M, M * 4);
+  if (pi) for (int n = 0; n < N; n++) pi[st.rpi[(size_t)chain * N + n]] = n;
+  if (cdl3) memcpy(cdl3, st.cdl + (size_t)chain * 4, 3 * 8);
+  if (counts) memcpy(counts, st.cnt + (size_t)chain * 4 * M, 4 * M * 4);
+  state_free(&st);
+  return SR_OK;
+}
+
+SR_API int sr_session_accept_counts(sr_session *s, int32_t chain, int64_t *acc7)
+{
+  if (!s || chain < 0 || chain >= s->nchains || !acc7) return SR_EINVAL;
+  sr_state_host st;
+  int rc = download(s, &st);
+  if (rc) return rc;
+  for (int k = 0; k < 7; k++) acc7[k] = (int64_t)st.acc[(size_t)chain * 8 + k];
+  state_free(&st);
+  return SR_OK;
+}
+
+SR_API void sr_session_destroy(sr_session *s)
+{
+  if (!s) return;
+  if (s->dev) srk_destroy(s->dev);
+  sr_free_dataset(&s->ds);
+  free(s->specs);
+  free(s);
+}
+
+/* mcmc_consistent (mcmc.c:999-1094) on a downloaded chain state; 0 = consistent */
+static int check_chain(const sr_dataset *ds, const sr_state_host *st, int c)
+{
+  const int N = ds->N, M = ds->M;
+  hmodel x;
+  if (hmodel_alloc(&x, ds)) return 1;
+  int flag = 0;
+  memcpy(x.rpi, st->rpi + (size_t)c * N, N * 4);
+  memcpy(x.a, st->ab + (size_t)c * 2 * M, M * 4);
+  memcpy(x.b, st->ab + (size_t)c * 2 * M + M, M * 4);
+  for (int m = 0; m < M; m++)
+    if (!(0 <= x.a[m] && x.a[m] <= x.b[m] && x.b[m] <= N)) flag = 1;
+  char *seen = (char *)calloc(N, 1);
+  for (int n = 0; n < N; n++) {
+    int v = x.rpi[n];
+    if (v < 0 || v >= N || seen[v]) { flag = 1; break; }
+    seen[v] = 1;
+  }
+  free(seen);
+  if (flag) { hmodel_free(&x); return 1; }
+  for (int n = 0; n < N; n++) x.pi[x.rpi[n]] = n;
+  int last = -1, nh = 0;
+  for (int n = 0; n < N; n++)
+    if (ds->hard[n]) { nh++; if (last >= 0 && x.pi[n] < last) flag = 1; last = x.pi[n]; }
+  if (nh != ds->nh) flag = 1;
+  x.c = st->cdl[(size_t)c * 4 + 0];
+  x.d = st->cdl[(size_t)c * 4 + 1];
+  h_count01(&x);
+  const int32_t *cnt = st->cnt + (size_t)c * 4 * M;
+  for (int m = 0; m < M; m++)
+    if (x.t0[m] != cnt[m] || x.f0[m] != cnt[M + m] || x.t1[m] != cnt[2 * M + m] || x.f1[m] != cnt[3 * M + m]) flag = 1;
+  double dl = st->cdl[(size_t)c * 4 + 2] - h_logl(&x);
+  if (dl < 0) dl = -dl;
+  if (!(dl <= 1e-8)) flag = 1;
+  /* P must still be X in position order */
+  const uint32_t *P = st->P + (size_t)c * st->NW * M;
+  for (int p = 0; p < N && !flag; p++)
+    for (int m = 0; m < M; m++)
+      if ((int)((P[(size_t)(p >> 5) * M + m] >> (p & 31)) & 1u) != ds->X[(size_t)x.rpi[p] * M + m]) { flag = 1; break; }
+  hmodel_free(&x);
+  return flag;
+}
+
+/* ------------------------------------------------------------- run loops */
+typedef struct {
+  double ls, cs, ds;
+} sr_sums;
+
+static int run_common(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n, const sr_run_opts *opts,
+                      sr_sample_sink_fn sink, void *ctx, sr_chain_summary *out, sr_state_host *final_state)
+{
+  sr_run_opts o;
+  if (opts) o = *opts; else sr_default_opts(&o);
+  if (o.burnin_calls < 0 || o.sample_calls < 0) return SR_EINVAL;
+  sr_session *s = NULL;
+  int rc = sr_session_create(ds, specs, n, &o, &s);
+  if (rc) return rc;
+  const int cpl = s->rec_cap;
+  for (int done = 0; done < o.burnin_calls;) {
+    int k = o.burnin_calls - done < cpl ? o.burnin_calls - done : cpl;
+    if ((rc = sr_session_run(s, k, 0))) goto fail;
+    done += k;
+  }
+  const int N = ds->N, M = ds->M, W = 2 * M + N;
+  sr_sums *sums = (sr_sums *)calloc(n, sizeof(sr_sums));
+  int16_t *rab = (int16_t *)malloc((size_t)n * cpl * W * sizeof(int16_t));
+  double *rcd = (double *)malloc((size_t)n * cpl * 3 * sizeof(double));
+  int32_t *ra = (int32_t *)malloc((size_t)W * 4);
+  if (!sums || !rab || !rcd || !ra) { free(sums); free(rab); free(rcd); free(ra); rc = SR_ENOMEM; goto fail; }
+  for (int done = 0; done < o.sample_calls;) {
+    int k = o.sample_calls - done < cpl ? o.sample_calls - done : cpl;
+    sr_session_reset_records(s);
+    if ((rc = sr_session_run(s, k, 1))) break;
+    if ((rc = sr_session_fetch_records(s, 0, k, rab, rcd))) break;
+    for (int c = 0; c < n && !rc; c++) {
+      for (int t = 0; t < k; t++) {
+        const int16_t *src = rab + ((size_t)c * k + t) * W;
+        const double *cd = rcd + ((size_t)c * k + t) * 3;
+        sums[c].ls += -(cd[2]);                 /* compute_exp_data, mcmc.c:53-58 */
+        sums[c].cs += exp(cd[0]);
+        sums[c].ds += exp(cd[1]);
+        if (sink) {
+          for (int q = 0; q < W; q++) ra[q] = src[q];
+          sr_record rec = {N, M, ra, ra + M, ra + 2 * M, cd[0], cd[1], cd[2]};
+          if (sink(ctx, c, done + t, &rec)) { rc = SR_EINVAL; break; }
+        }
+      }
+    }
+    if (rc) break;
+    done += k;
+  }
+  free(rab); free(rcd); free(ra);
+  if (rc) { free(sums); goto fail; }
+  sr_state_host st;
+  rc = download(s, &st);
+  if (rc) { free(sums); goto fail; }
+  for (int c = 0; c < n; c++) {
+    if (out) {
+      out[c].chain_id = specs[c].chain_id;
+      out[c].exp_loglik = sums[c].ls / 1000;      /* print_exp_data divides by 1000 (mcmc.c:62-64) */
+      out[c].exp_c = sums[c].cs / 1000;
+      out[c].exp_d = sums[c].ds / 1000;
+      out[c].consistent = (o.flags & SR_F_NO_CHECK) ? 0 : check_chain(ds, &st, c);
+    }
+  }
+  free(sums);
+  if (final_state) *final_state = st; else state_free(&st);
+  sr_session_destroy(s);
+  if (out && !(o.flags & SR_F_NO_CHECK))
+    for (int c = 0; c < n; c++) if (out[c].consistent) return SR_EINCONSISTENT;
+  return SR_OK;
+fail:
+  sr_session_destroy(s);
+  return rc;
+}
+
+SR_API int sr_run_chains(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n_chains, const sr_run_opts *opts,
+                         sr_sample_sink_fn sink, void *sink_ctx, sr_chain_summary *out)
+{
+  if (!ds || !specs || n_chains <= 0) return SR_EINVAL;
+  return run_common(ds, specs, n_chains, opts, sink, sink_ctx, out, NULL);
+}
+
+/* ------------------------------------------------------------ file output */
+static char *put_int(char *p, int v)
+{
+  char tmp[16];
+  int n = 0;
+  unsigned u = v < 0 ? (unsigned)(-(long)v) : (unsigned)v;
+  if (v < 0) *p++ = '-';
+  do { tmp[n++] = (char)('0' + u % 10); u /= 10; } while (u);
+  while (n) *p++ = tmp[--n];
+  return p;
+}
+
+typedef struct {
+  FILE **f;
+  char *line;
+  size_t cap;
+  int M;
+} dir_ctx;
+
+/* one mcmc_save_chain line (mcmc.c:69-92); c and d are shared by all taxa (manycd=0),
+ * so their "%.14f " text is formatted once and replicated. */
+static int dir_sink(void *vctx, int32_t ci, int32_t si, const sr_record *r)
+{
+  (void)si;
+  dir_ctx *x = (dir_ctx *)vctx;
+  char cbuf[64], dbuf[64];
+  int cl = snprintf(cbuf, sizeof cbuf, "%.14f ", exp(r->c));
+  int dl = snprintf(dbuf, sizeof dbuf, "%.14f ", exp(r->d));
+  size_t need = (size_t)(2 * r->M + r->N) * 12 + (size_t)r->M * (cl + dl) + 128;
+  if (need > x->cap) {
+    char *nl = (char *)realloc(x->line, need);
+    if (!nl) return 1;
+    x->line = nl; x->cap = need;
+  }
+  char *p = x->line;
+  for (int i = 0; i < r->M; i++) { p = put_int(p, r->a[i]); *p++ = ' '; }
+  *p++ = ',';
+  for (int i = 0; i < r->M; i++) { p = put_int(p, r->b[i]); *p++ = ' '; }
+  *p++ = ',';
+  for (int i = 0; i < r->N; i++) { p = put_int(p, r->pi[i]); *p++ = ' '; }
+  *p++ = ',';
+  for (int i = 0; i < r->M; i++) { memcpy(p, cbuf, cl); p += cl; }
+  *p++ = ',';
+  for (int i = 0; i < r->M; i++) { memcpy(p, dbuf, dl); p += dl; }
+  p += sprintf(p, ",%.14f\n", r->loglik);
+  return fwrite(x->line, 1, (size_t)(p - x->line), x->f[ci]) == (size_t)(p - x->line) ? 0 : 1;
+}
+
+static void chain_dir(char *buf, size_t n, const char *root, int id)
+{
+  if (id >= 0 && id < 100) snprintf(buf, n, "%s/Chains/chain_%02d", root, id);
+  else snprintf(buf, n, "%s/Chains/chain_%d", root, id);
+}
+
+SR_API int sr_run_to_dirs(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n, const sr_run_opts *opts,
+                          const char *root, sr_chain_summary *out)
+{
+  if (!ds || !specs || n <= 0 || !root) return SR_EINVAL;
+  char path[4096], dir[4000];
+  snprintf(path, sizeof path, "%s/mcmc_c.log", root);     /* mcmc.c:104 (never written) */
+  FILE *lf = fopen(path, "a");
+  if (lf) fclose(lf);
+  snprintf(dir, sizeof dir, "%s/Chains", root);
+  mkdir(dir, 0777);
+  dir_ctx x;
+  memset(&x, 0, sizeof x);
+  x.M = ds->M;
+  x.f = (FILE **)calloc(n, sizeof(FILE *));
+  sr_chain_summary *sum = out ? out : (sr_chain_summary *)calloc(n, sizeof(sr_chain_summary));
+  if (!x.f || !sum) { free(x.f); if (!out) free(sum); return SR_ENOMEM; }
+  int rc = SR_OK;
+  for (int c = 0; c < n && !rc; c++) {
+    chain_dir(dir, sizeof dir, root, specs[c].chain_id);
+    mkdir(dir, 0777);
+    snprintf(path, sizeof path, "%s/chain_data.csv", dir);
+    x.f[c] = fopen(path, "w");
+    if (!x.f[c]) rc = SR_EIO;
+  }
+  sr_state_host st;
+  memset(&st, 0, sizeof st);
+  if (!rc) rc = run_common(ds, specs, n, opts, dir_sink, &x, sum, &st);
+  for (int c = 0; c < n; c++) if (x.f[c]) fclose(x.f[c]);
+  free(x.f);
+  free(x.line);
+  if (rc && rc != SR_EINCONSISTENT) { if (!out) free(sum); state_free(&st); return rc; }
+  const int N = ds->N, M = ds->M;
+  for (int c = 0; c < n && st.ab; c++) {
+    chain_dir(dir, sizeof dir, root, specs[c].chain_id);
+    FILE *f1, *f2, *f3, *f4;
+    snprintf(path, sizeof path, "%s/taxa.csv", dir); f1 = fopen(path, "w");
+    snprintf(path, sizeof path, "%s/sites.csv", dir); f2 = fopen(path, "w");
+    snprintf(path, sizeof path, "%s/hard_sites.csv", dir); f3 = fopen(path, "w");
+    snprintf(path, sizeof path, "%s/exp_data.csv", dir); f4 = fopen(path, "w");
+    if (!f1 || !f2 || !f3 || !f4) {
+      if (f1) fclose(f1);
+      if (f2) fclose(f2);
+      if (f3) fclose(f3);
+      if (f4) fclose(f4);
+      rc = SR_EIO;
+      break;
+    }
+    fprintf(f4, "exp_loglik,exp_c,exp_d\n");                   /* print_exp_data, mcmc.c:60-67 */
+    fprintf(f4, "%.14f,%.14f,%.14f", sum[c].exp_loglik, sum[c].exp_c, sum[c].exp_d);
+    const int32_t *a = st.ab + (size_t)c * 2 * M, *b = a + M;
+    const double cc = exp(st.cdl[(size_t)c * 4 + 0]), dd = exp(st.cdl[(size_t)c * 4 + 1]);
+    fprintf(f1, "a,b,c,d\n");                                   /* mcmc_save, mcmc.c:261-293 */
+    for (int i = 0; i < M; i++) fprintf(f1, "%d,%d,%.14f,%.14f\n", a[i], b[i], cc, dd);
+    int *pi = (int *)malloc(N * sizeof(int));
+    for (int p = 0; p < N; p++) pi[st.rpi[(size_t)c * N + p]] = p;
+    fprintf(f2, "sites\n");
+    for (int i = 0; i < N; i++) fprintf(f2, "%d\n", pi[i]);
+    fprintf(f3, "i,pi_i\n");
+    for (int i = 0; i < N; i++) if (ds->hard[i]) fprintf(f3, "%d,%d\n", i, pi[i]);
+    free(pi);
+    fclose(f1); fclose(f2); fclose(f3); fclose(f4);
+  }
+  state_free(&st);
+  if (!out) free(sum);
+  return rc;
+}
+
+/* ------------------------------------------------------ test hooks (host math) */
+SR_API void sr_host_exp_log(const double *in, long n, double *out_exp, double *out_log)
+{
+  for (long k = 0; k < n; k++) {
+    if (out_exp) out_exp[k] = h_exp(in[k]);
+    if (out_log) out_log[k] = h_log(in[k]);
+  }
+}
+
+SR_API double sr_host_run_add(double x, double e, long L) { return sr_run_add(x, e, L); }
+SR_API long sr_host_run_sub(double *r, double p, long L) { return sr_run_sub(r, p, L); }
+
+/* initial chain state as the host builds it (a, b, pi after mcmc_randomize; c, d, loglik) */
+SR_API int sr_host_init_chain(const sr_dataset *ds, uint64_t seed, int32_t *a, int32_t *b, int32_t *pi,
+                              double *cdl3, uint64_t *rng_pos)
+{
+  sr_state_host st;
+  int rc = state_alloc(&st, ds->N, ds->M, ds->nh, 1);
+  if (rc) return rc;
+  rc = init_chain(ds, seed, &st, 0);
+  if (!rc) {
+    if (a) memcpy(a, st.ab, ds->M * 4);
+    if (b) memcpy(b, st.ab + ds->M, ds->M * 4);
+    if (pi) for (int n = 0; n < ds->N; n++) pi[st.rpi[n]] = n;
+    if (cdl3) memcpy(cdl3, st.cdl, 24);
+    if (rng_pos) *rng_pos = st.rng[0];
+  }
+  state_free(&st);
+  return rc;
+}

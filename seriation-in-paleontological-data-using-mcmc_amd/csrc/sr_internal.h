@@ -1,0 +1,53 @@
+/*
+ * sr_internal.h -- interface between the C host layer (sr_host.c) and the HIP device
+ * layer (sr_device.hip).  Plain C.
+ */
+#ifndef SR_INTERNAL_H
+#define SR_INTERNAL_H
+#include <stdint.h>
+#include <stddef.h>
+
+#define SR_NHMAX 32      /* hard sites per dataset the kernel supports */
+#define SR_RING 8        /* MT19937 blocks resident per chain */
+
+/* Per-chain state in HBM, struct-of-arrays over chains.  Layout (per chain c):
+ *   P   [NW][M] u32  position-ordered occurrence columns: bit (p&31) of P[p>>5][m]
+ *                    = X[rpi[p]][m]  (the column of taxon m in current site order)
+ *   rpi [N]     i32  site at each position (gsl_permutation rpi, mcmc.h:37)
+ *   hp  [NHMAX] i32  positions of the hard sites, ascending (hard order is invariant)
+ *   ab  [2][M]  i32  a, b (mcmc.h:36)
+ *   cnt [4][M]  i32  t0, f0, t1, f1 (mcmc.h:42)
+ *   cdl [4]     f64  c, d, loglik, unused
+ *   mt  [RING][624] u32, rng [2] u64 (pos, gen), acc [8] u64                       */
+typedef struct {
+  int N, M, NW, nh, nchains;
+  uint32_t *P;
+  int32_t *rpi, *hp, *ab, *cnt;
+  double *cdl;
+  uint32_t *mt;
+  uint64_t *rng, *acc;
+} sr_state_host;
+
+typedef struct srk_dev srk_dev;
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int srk_device_count(void);
+int srk_create(const sr_state_host *st, int device, int block_threads, int rec_cap_calls, srk_dev **out);
+int srk_set_stream(srk_dev *d, void *stream);
+/* calls*spc sweeps for all chains; save -> records appended at slot rec_base.. */
+int srk_run(srk_dev *d, int calls, int spc, int save, int rec_base);
+int srk_sync(srk_dev *d);
+double srk_last_ms(srk_dev *d);
+int srk_block_threads(const srk_dev *d);
+int srk_fetch_records(srk_dev *d, int first, int count, int16_t *ab_pi, double *cdl);
+int srk_download_state(srk_dev *d, sr_state_host *st);
+void srk_destroy(srk_dev *d);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

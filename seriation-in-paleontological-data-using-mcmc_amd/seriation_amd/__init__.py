@@ -1,0 +1,12 @@
+"""seriation_amd -- MI355X-native drop-in for the reference's per-chain MCMC sweep.
+
+Layers (reference file in parentheses):
+  _lib      ctypes binding of libseriation.so (C ABI: include/seriation.h)
+  core      Dataset / Session / run_chains / run_to_dirs   (mcmc.c main + mcmc.h API)
+  launcher  run_chain / run_all_chains / choose_chains     (script.py:15-99)
+"""
+from ._lib import SrError, LIB_PATH, lib  # noqa: F401
+from .core import Dataset, Session, run_chains, run_to_dirs  # noqa: F401
+from . import launcher  # noqa: F401
+
+__all__ = ["Dataset", "Session", "run_chains", "run_to_dirs", "launcher", "SrError", "lib", "LIB_PATH"]

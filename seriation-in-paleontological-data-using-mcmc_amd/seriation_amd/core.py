@@ -1,0 +1,213 @@
+"""Pythonic wrappers over the C ABI: datasets, sessions, whole-run helpers.
+
+These mirror the reference's C entry points (C_Implementation/mcmc.h:47-72) with numpy
+arrays instead of gsl containers; the computation always happens in libseriation.so on
+the GPU.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import _lib as L
+
+
+def _check(rc, what):
+    if rc != L.SR_OK:
+        raise L.SrError(rc, what)
+
+
+class Dataset:
+    """Occurrence matrix X (N sites x M taxa, uint8 0/1) and hard-site flags.
+
+    Parsed exactly like mcmc_readmodel (mcmc.c:339-437); ``maxs=2000`` keeps the
+    reference's fgets(MAXS) line limit, ``maxs=0`` accepts lines of any length.
+    """
+
+    def __init__(self, X, hard):
+        self.X = np.ascontiguousarray(X, dtype=np.uint8)
+        self.hard = np.ascontiguousarray(hard, dtype=np.uint8)
+        assert self.X.ndim == 2 and self.hard.shape == (self.X.shape[0],)
+        self.N, self.M = self.X.shape
+        self.nh = int(self.hard.sum())
+        self._c = L.sr_dataset(self.N, self.M, self.nh,
+                               self.X.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)),
+                               self.hard.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+
+    @classmethod
+    def parse(cls, text, maxs=L.SR_MAXS):
+        if isinstance(text, str):
+            text = text.encode()
+        ds = L.sr_dataset()
+        _check(L.lib().sr_parse_dataset(text, len(text), maxs, ctypes.byref(ds)), "parse")
+        try:
+            X = np.ctypeslib.as_array(ds.X, shape=(ds.N * ds.M,)).reshape(ds.N, ds.M).copy()
+            hard = np.ctypeslib.as_array(ds.hard, shape=(ds.N,)).copy()
+        finally:
+            L.lib().sr_free_dataset(ctypes.byref(ds))
+        return cls(X, hard)
+
+    @classmethod
+    def load(cls, path, maxs=L.SR_MAXS):
+        with open(path, "rb") as fh:
+            return cls.parse(fh.read(), maxs)
+
+    @property
+    def c(self):
+        return self._c
+
+
+def make_opts(burnin_calls=1000, sample_calls=1000, sweeps_per_call=10, device=0, block_threads=0,
+              calls_per_launch=0, check=True):
+    o = L.sr_run_opts()
+    L.lib().sr_default_opts(ctypes.byref(o))
+    o.burnin_calls = burnin_calls
+    o.sample_calls = sample_calls
+    o.sweeps_per_call = sweeps_per_call
+    o.device = device
+    o.block_threads = block_threads
+    o.calls_per_launch = calls_per_launch
+    o.flags = 0 if check else L.SR_F_NO_CHECK
+    return o
+
+
+def make_specs(seeds, chain_ids=None):
+    n = len(seeds)
+    arr = (L.sr_chain_spec * n)()
+    for k, s in enumerate(seeds):
+        arr[k].chain_id = int(chain_ids[k]) if chain_ids is not None else k
+        arr[k].seed = int(s)
+    return arr
+
+
+class Session:
+    """Chains resident on one GPU (sr_session_*).  ``run(calls, save)`` enqueues
+    ``calls`` mcmc_sample calls (mcmc.c:214-258) for every chain."""
+
+    def __init__(self, dataset, seeds, device=0, sweeps_per_call=10, calls_per_launch=0, block_threads=0,
+                 chain_ids=None):
+        self.ds = dataset
+        self.n = len(seeds)
+        self.specs = make_specs(seeds, chain_ids)
+        self.opts = make_opts(sweeps_per_call=sweeps_per_call, device=device, block_threads=block_threads,
+                              calls_per_launch=calls_per_launch)
+        h = ctypes.c_void_p()
+        _check(L.lib().sr_session_create(ctypes.byref(dataset.c), self.specs, self.n, ctypes.byref(self.opts),
+                                         ctypes.byref(h)), "sr_session_create")
+        self.h = h
+
+    @property
+    def record_capacity(self):
+        return L.lib().sr_session_record_capacity(self.h)
+
+    @property
+    def block_threads(self):
+        return L.lib().sr_session_block_threads(self.h)
+
+    def set_stream(self, stream_handle):
+        _check(L.lib().sr_session_set_stream(self.h, ctypes.c_void_p(stream_handle)), "set_stream")
+
+    def run(self, calls, save=False):
+        _check(L.lib().sr_session_run(self.h, calls, 1 if save else 0), "sr_session_run")
+
+    def sync(self):
+        _check(L.lib().sr_session_sync(self.h), "sr_session_sync")
+
+    def last_kernel_ms(self):
+        return L.lib().sr_session_last_kernel_ms(self.h)
+
+    def reset_records(self):
+        _check(L.lib().sr_session_reset_records(self.h), "reset_records")
+
+    def fetch_records(self):
+        """Returns (ab_pi int16 [n, k, 2M+N], cdl float64 [n, k, 3]) for the k buffered calls."""
+        k = L.lib().sr_session_records(self.h)
+        N, M = self.ds.N, self.ds.M
+        ab = np.zeros((self.n, k, 2 * M + N), np.int16)
+        cdl = np.zeros((self.n, k, 3), np.float64)
+        if k:
+            _check(L.lib().sr_session_fetch_records(self.h, 0, k, ab.ctypes.data_as(ctypes.POINTER(ctypes.c_int16)),
+                                                    cdl.ctypes.data_as(ctypes.POINTER(ctypes.c_double))), "fetch")
+        return ab, cdl
+
+    def state(self, chain):
+        N, M = self.ds.N, self.ds.M
+        a = np.zeros(M, np.int32)
+        b = np.zeros(M, np.int32)
+        pi = np.zeros(N, np.int32)
+        cdl = np.zeros(3, np.float64)
+        cnt = np.zeros(4 * M, np.int32)
+        P = ctypes.POINTER
+        _check(L.lib().sr_session_state(self.h, chain, a.ctypes.data_as(P(ctypes.c_int32)),
+                                        b.ctypes.data_as(P(ctypes.c_int32)), pi.ctypes.data_as(P(ctypes.c_int32)),
+                                        cdl.ctypes.data_as(P(ctypes.c_double)), cnt.ctypes.data_as(P(ctypes.c_int32))),
+               "state")
+        return {"a": a, "b": b, "pi": pi, "c": cdl[0], "d": cdl[1], "loglik": cdl[2], "counts": cnt.reshape(4, M)}
+
+    def accept_counts(self, chain):
+        acc = np.zeros(7, np.int64)
+        _check(L.lib().sr_session_accept_counts(self.h, chain, acc.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))),
+               "accept_counts")
+        return acc
+
+    def close(self):
+        if self.h:
+            L.lib().sr_session_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def run_chains(dataset, seeds, burnin_calls=1000, sample_calls=1000, sweeps_per_call=10, device=0,
+               chain_ids=None, keep_records=False, calls_per_launch=0):
+    """sr_run_chains: returns (summaries list of dicts, records or None).
+    records = (ab_pi int32 [n, ts, 2M+N], cdl [n, ts, 3]) when keep_records."""
+    n = len(seeds)
+    specs = make_specs(seeds, chain_ids)
+    opts = make_opts(burnin_calls, sample_calls, sweeps_per_call, device, calls_per_launch=calls_per_launch)
+    out = (L.sr_chain_summary * n)()
+    N, M = dataset.N, dataset.M
+    recs = None
+    if keep_records:
+        recs = (np.zeros((n, sample_calls, 2 * M + N), np.int32), np.zeros((n, sample_calls, 3)))
+
+    def sink(ctx, ci, si, rp):
+        r = rp.contents
+        ab = recs[0][ci, si]
+        ab[:M] = np.ctypeslib.as_array(r.a, shape=(M,))
+        ab[M:2 * M] = np.ctypeslib.as_array(r.b, shape=(M,))
+        ab[2 * M:] = np.ctypeslib.as_array(r.pi, shape=(N,))
+        recs[1][ci, si] = (r.c, r.d, r.loglik)
+        return 0
+
+    cb = L.SINK_FN(sink) if keep_records else ctypes.cast(None, L.SINK_FN)
+    rc = L.lib().sr_run_chains(ctypes.byref(dataset.c), specs, n, ctypes.byref(opts), cb, None, out)
+    if rc not in (L.SR_OK, L.SR_EINCONSISTENT):
+        raise L.SrError(rc, "sr_run_chains")
+    summ = [dict(chain_id=o.chain_id, consistent=o.consistent, exp_loglik=o.exp_loglik, exp_c=o.exp_c,
+                 exp_d=o.exp_d) for o in out]
+    return summ, recs
+
+
+def run_to_dirs(dataset, seeds, root=".", chain_ids=None, burnin_calls=1000, sample_calls=1000, device=0):
+    """sr_run_to_dirs: writes Chains/chain_NN/*.csv under root like the reference main()."""
+    n = len(seeds)
+    specs = make_specs(seeds, chain_ids)
+    opts = make_opts(burnin_calls, sample_calls, 10, device)
+    out = (L.sr_chain_summary * n)()
+    rc = L.lib().sr_run_to_dirs(ctypes.byref(dataset.c), specs, n, ctypes.byref(opts),
+                                os.fsencode(root), out)
+    if rc not in (L.SR_OK, L.SR_EINCONSISTENT):
+        raise L.SrError(rc, "sr_run_to_dirs")
+    return [dict(chain_id=o.chain_id, consistent=o.consistent, exp_loglik=o.exp_loglik, exp_c=o.exp_c,
+                 exp_d=o.exp_d) for o in out]

@@ -1,0 +1,95 @@
+"""ctypes access to the CPU oracle (oracle/build/liboracle.so) -- TEST INFRASTRUCTURE.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this module.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB = os.path.join(ORACLE_DIR, "build", "liboracle.so")
+_L = None
+P = ctypes.POINTER
+
+
+def lib():
+    global _L
+    if _L is None:
+        if not os.path.exists(LIB):
+            subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
+        L = ctypes.CDLL(LIB)
+        L.oracle_parse.restype = ctypes.c_int
+        L.oracle_parse.argtypes = [ctypes.c_char_p, ctypes.c_long, ctypes.c_int, P(ctypes.c_int), P(ctypes.c_int),
+                                   P(ctypes.c_int), P(ctypes.c_int32), P(ctypes.c_int32)]
+        L.oracle_run_chain.restype = ctypes.c_int
+        L.oracle_run_chain.argtypes = [ctypes.c_char_p, ctypes.c_long, ctypes.c_int, ctypes.c_ulong, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       P(ctypes.c_int32), P(ctypes.c_double), P(ctypes.c_int32), P(ctypes.c_double),
+                                       P(ctypes.c_double), P(ctypes.c_longlong), P(ctypes.c_ulonglong)]
+        L.oracle_rng_stream.restype = None
+        L.oracle_rng_stream.argtypes = [ctypes.c_ulong, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_long,
+                                        P(ctypes.c_double), P(ctypes.c_ulonglong)]
+        L.oracle_shuffle.argtypes = [ctypes.c_ulong, P(ctypes.c_int32), ctypes.c_long]
+        L.oracle_choose.argtypes = [ctypes.c_ulong, P(ctypes.c_int32), ctypes.c_long, P(ctypes.c_int32), ctypes.c_long]
+        L.oracle_exp_log.argtypes = [P(ctypes.c_double), ctypes.c_long, P(ctypes.c_double), P(ctypes.c_double)]
+        _L = L
+    return _L
+
+
+def _p(a, t):
+    return a.ctypes.data_as(P(t)) if a is not None else None
+
+
+def parse(text, maxs=2000):
+    if isinstance(text, str):
+        text = text.encode()
+    N, M, nh = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    rc = lib().oracle_parse(text, len(text), maxs, ctypes.byref(N), ctypes.byref(M), ctypes.byref(nh), None, None)
+    if rc:
+        return rc, None, None
+    X = np.zeros(N.value * M.value, np.int32)
+    h = np.zeros(N.value, np.int32)
+    lib().oracle_parse(text, len(text), maxs, ctypes.byref(N), ctypes.byref(M), ctypes.byref(nh),
+                       _p(X, ctypes.c_int32), _p(h, ctypes.c_int32))
+    return 0, X.reshape(N.value, M.value), h
+
+
+def run_chain(text, seed, tb, ts, sweeps=10, check=0, maxs=2000, want_init=False):
+    """Returns dict(rc, init (a,b,pi), init_cdl, rec_int [ts, 2M+N], rec_dbl [ts, 3], exp, acc, words)."""
+    if isinstance(text, str):
+        text = text.encode()
+    rc, X, h = parse(text, maxs)
+    assert rc == 0, rc
+    N, M = X.shape
+    W = 2 * M + N
+    init = np.zeros(W, np.int32)
+    initd = np.zeros(3)
+    ri = np.zeros(max(ts, 1) * W, np.int32)
+    rd = np.zeros(max(ts, 1) * 3)
+    ex = np.zeros(3)
+    acc = np.zeros(7, np.int64)
+    words = ctypes.c_ulonglong()
+    rc = lib().oracle_run_chain(text, len(text), maxs, seed, 0, tb, ts, sweeps, check,
+                                _p(init, ctypes.c_int32), _p(initd, ctypes.c_double),
+                                _p(ri, ctypes.c_int32), _p(rd, ctypes.c_double), _p(ex, ctypes.c_double),
+                                _p(acc, ctypes.c_longlong), ctypes.byref(words))
+    return dict(rc=rc, N=N, M=M, init=init, init_cdl=initd, rec_int=ri[:ts * W].reshape(ts, W),
+                rec_dbl=rd[:ts * 3].reshape(ts, 3), exp=ex, acc=acc, words=words.value)
+
+
+def rng_stream(seed, kind, count, a=0.0, b=0.0):
+    out = np.zeros(count)
+    w = ctypes.c_ulonglong()
+    lib().oracle_rng_stream(seed, kind, a, b, count, _p(out, ctypes.c_double), ctypes.byref(w))
+    return out, w.value
+
+
+def exp_log(x):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    e = np.zeros_like(x)
+    l = np.zeros_like(x)
+    lib().oracle_exp_log(_p(x, ctypes.c_double), len(x), _p(e, ctypes.c_double), _p(l, ctypes.c_double))
+    return e, l

@@ -1,0 +1,203 @@
+#!/usr/bin/env python3
+"""Benchmark: chain-iterations/s of the MCMC seriation sweep on MI355X.
+
+Workload (BASELINE.json configs[2]/[3]): synthetic 256 sites x 512 taxa
+(tools/gen_synthetic.py, seed 20261015), 100 chains per GPU (weak scaling: 100*N chains on
+N GPUs, 800 on 8 = config 4).  One step = one kernel launch that runs
+`--calls-per-step` reference mcmc_sample calls (10 sweeps each, mcmc.c:225) for every
+chain of the rank and saves one record per call (a, b, pi, c, d, loglik -- the
+mcmc_save_chain payload) to HBM, as the reference's sampling phase does.  Chain state,
+dataset and records stay resident in HBM; host formatting of records is not timed.
+At the end of the timed region ranks all-gather their per-chain loglik over RCCL (the
+one-sigma selection input) -- the only collective.
+
+1 chain-iteration = 1 sweep = body of mcmc.c:225-244.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "seriation-in-paleontological-data-using-mcmc_amd")
+sys.path.insert(0, PKG)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+SYNTH = os.path.join(ROOT, "tests", "golden", "datasets", "synth_256x512.txt")
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes_per_iter(N, M):
+    """B_iter = N*M (one pass over X for the Gibbs a/b update) + 48*M
+    (a, b, t0, f0, t1, f1 read+write) + 16*9*M (16 proposals x (a, b + one row/column slice))."""
+    return N * M + 192 * M
+
+
+def _cpu_worker(args):
+    text, seed, calls = args
+    import oracle_ref
+    t0 = time.perf_counter()
+    o = oracle_ref.run_chain(text, seed, 0, calls, sweeps=10)
+    return time.perf_counter() - t0, o["rc"]
+
+
+def cpu_baseline(path, calls, workers):
+    """The CPU oracle (restatement of mcmc.c, -O2) on `workers` processes, one chain each,
+    `calls` mcmc_sample calls per chain: aggregate chain-iterations/s."""
+    import multiprocessing as mp
+    with open(path, "rb") as fh:
+        text = fh.read()
+    import oracle_ref
+    oracle_ref.lib()  # build/load before forking
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(workers) as pool:
+        res = pool.map(_cpu_worker, [(text, s + 1, calls) for s in range(workers)])
+    wall = time.perf_counter() - t0
+    assert all(rc == 0 for _, rc in res)
+    iters = workers * calls * 10
+    return {"value": iters / wall, "unit": "chain-iterations/s", "cores": workers, "kind": "port",
+            "sample": "%d chains x %d mcmc_sample calls (%d sweeps each) of the bench workload, oracle/ "
+                      "(C restatement of mcmc.c, gcc -O2, recount after accept as the reference) on %d "
+                      "processes, wall %.1f s" % (workers, calls, 10, workers, wall)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--chains-per-gpu", type=int, default=100)
+    ap.add_argument("--calls-per-step", type=int, default=10)
+    ap.add_argument("--dataset", default=SYNTH)
+    ap.add_argument("--cpu-calls", type=int, default=40)
+    ap.add_argument("--cpu-workers", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--block-threads", type=int, default=0)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    if not os.path.exists(args.dataset):
+        import gen_synthetic
+        gen_synthetic.write(256, 512, 20261015, args.dataset)
+
+    # CPU baseline first, before this process touches the GPU (it forks workers).
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        workers = args.cpu_workers or max(1, min(16, os.cpu_count() or 1))
+        cpu = cpu_baseline(args.dataset, args.cpu_calls, workers)
+
+    import torch
+    import seriation_amd as sa
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(local_rank)
+
+    ds = sa.Dataset.load(args.dataset)
+    C = args.chains_per_gpu
+    seeds = [rank * C + k + 1 for k in range(C)]
+    sess = sa.Session(ds, seeds, device=local_rank, calls_per_launch=args.calls_per_step,
+                      block_threads=args.block_threads, chain_ids=[rank * C + k for k in range(C)])
+    stream = torch.cuda.current_stream()
+    sess.set_stream(stream.cuda_stream)
+    cps = args.calls_per_step
+
+    def step():
+        sess.reset_records()
+        sess.run(cps, save=True)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        evs[k][0].record(stream)
+        step()
+        evs[k][1].record(stream)
+    # the one collective: every rank's per-chain loglik of the last saved sample (one-sigma input)
+    _, cdl = sess.fetch_records()
+    ll = torch.tensor(cdl[:, -1, 2], dtype=torch.float64, device="cuda")
+    if dist:
+        parts = [torch.empty_like(ll) for _ in range(world)]
+        dist.all_gather(parts, ll)
+        gathered = torch.cat(parts)
+    else:
+        gathered = ll
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+    assert gathered.numel() == C * world and bool(torch.isfinite(gathered).all())
+
+    total_chains = C * world
+    sweeps_per_step = cps * 10
+    iters = total_chains * sweeps_per_step * args.steps
+    value = iters / elapsed
+    B = algorithmic_bytes_per_iter(ds.N, ds.M)
+    launch_bytes = C * sweeps_per_step * B
+    achieved = launch_bytes / (kernel_ms / 1e3) / 1e9
+    out = {
+        "metric": "chain-iterations/sec (100 chains, 256x512 matrix) at 1/2/4/8 MI355X",
+        "value": value,
+        "unit": "chain-iterations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {
+            "workload": "synthetic %dx%d (tools/gen_synthetic.py seed 20261015), %d chains per GPU, "
+                        "%d mcmc_sample calls (%d sweeps) per chain per step, one saved record per call"
+                        % (ds.N, ds.M, C, cps, sweeps_per_step),
+            "sites": ds.N, "taxa": ds.M, "chains": total_chains, "chains_per_gpu": C,
+            "sweeps_per_step": sweeps_per_step, "block_threads": sess.block_threads,
+            "parallelism": "chains sharded over %d GPU(s), RCCL all-gather at end" % world,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "kernel": "sr_sweep_kernel",
+            "kernel_ms": kernel_ms,
+            "bytes_per_chain_iteration": B,
+            "launch_bytes": launch_bytes,
+        },
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    sess.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

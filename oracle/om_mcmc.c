@@ -50,6 +50,19 @@ typedef struct {                                   /* mcmc.h:32-45 */
 
 #define X_(x, n, m) ((x)->X[(size_t)(n) * (x)->M + (m)])
 
+/* diagnostics: how often |delta| is within the device's certification bound */
+static long long om_stat[8];
+static double om_stat_acc_K, om_stat_A;
+static void om_note(double delta, int K, double A)
+{
+  om_stat[0]++;
+  if (K == 0) { om_stat[1]++; return; }
+  double E = (K + 64.0) * 0x1p-52 * A;
+  if (delta == 0.0) om_stat[2]++;
+  if (-E <= delta && delta <= E) om_stat[3]++;
+  om_stat_acc_K += K; om_stat_A += A;
+}
+
 /* ---------------------------------------------------------------- parsing */
 
 /* fgets(s, maxs, f) over an in-memory buffer; maxs <= 0 means unlimited. */
@@ -431,7 +444,8 @@ static int om_samplepi1(om_model *x)
 {
   int n, m, i, j, ii, jj, a, b, ain, bin, t;
   int dt0, df0, dt1, df1;
-  double delta, c, d;
+  double delta, c, d, aA_ = 0.0;
+  int nK_ = 0;
   const int *v;
   i = (int)om_uniform_int(&x->rng, x->N);
   j = (int)om_uniform_int(&x->rng, x->N - 1);
@@ -467,8 +481,10 @@ static int om_samplepi1(om_model *x)
       }
     }
     c = x->c[m]; d = x->d[m];
-    delta += dt0 * om_log(1. - om_exp(c)) + df0 * d + dt1 * om_log(1. - om_exp(d)) + df1 * c;
+    { double t_ = dt0 * om_log(1. - om_exp(c)) + df0 * d + dt1 * om_log(1. - om_exp(d)) + df1 * c;
+      delta += t_; if (t_ != 0.0) { nK_++; aA_ += t_ < 0 ? -t_ : t_; } }
   }
+  om_note(delta, nK_, aA_);
   if (delta >= 0. || delta > om_log(om_uniform_pos(&x->rng))) {
     if (i < j) {
       for (m = 0; m < x->M; m++) {
@@ -502,7 +518,8 @@ static int om_samplepi2(om_model *x, int swap)
 {
   int i, j, n, m, a, b, inc1, inc2, ain, bin;
   int dt0, df0, dt1, df1;
-  double delta, c, d;
+  double delta, c, d, aA_ = 0.0;
+  int nK_ = 0;
   if (!swap) {
     i = (int)om_uniform_int(&x->rng, x->N);
     j = (int)om_uniform_int(&x->rng, x->N - 1);
@@ -541,8 +558,10 @@ static int om_samplepi2(om_model *x, int swap)
       }
     }
     c = x->c[m]; d = x->d[m];
-    delta += dt0 * om_log(1. - om_exp(c)) + df0 * d + dt1 * om_log(1. - om_exp(d)) + df1 * c;
+    { double t_ = dt0 * om_log(1. - om_exp(c)) + df0 * d + dt1 * om_log(1. - om_exp(d)) + df1 * c;
+      delta += t_; if (t_ != 0.0) { nK_++; aA_ += t_ < 0 ? -t_ : t_; } }
   }
+  om_note(delta, nK_, aA_);
   if (delta >= 0. || delta > om_log(om_uniform_pos(&x->rng))) {
     for (m = 0; m < x->M; m++) {
       a = x->a[m]; b = x->b[m];
@@ -568,7 +587,8 @@ static int om_samplepi3(om_model *x)
 {
   int i, j, n, m, a, b, nn, na, nb, inc1, inc2, ain, bin, wasalive, isalive;
   int dt0, df0, dt1, df1;
-  double delta, c, d;
+  double delta, c, d, aA_ = 0.0;
+  int nK_ = 0;
   int *p = x->p;
   if (x->N - x->nh < 2) return 0;
   n = (int)om_uniform_int(&x->rng, x->N - x->nh);
@@ -606,8 +626,10 @@ static int om_samplepi3(om_model *x)
       }
     }
     c = x->c[m]; d = x->d[m];
-    delta += dt0 * om_log(1. - om_exp(c)) + df0 * d + dt1 * om_log(1. - om_exp(d)) + df1 * c;
+    { double t_ = dt0 * om_log(1. - om_exp(c)) + df0 * d + dt1 * om_log(1. - om_exp(d)) + df1 * c;
+      delta += t_; if (t_ != 0.0) { nK_++; aA_ += t_ < 0 ? -t_ : t_; } }
   }
+  om_note(delta, nK_, aA_);
   if (delta >= 0. || delta > om_log(om_uniform_pos(&x->rng))) {
     for (m = 0; m < x->M; m++) {
       a = x->a[m]; b = x->b[m];
@@ -646,7 +668,16 @@ static int om_sample(om_model *x, int sweeps)
 
 /* ------------------------------------------------------------ library API */
 
+
 #define OM_API __attribute__((visibility("default")))
+
+OM_API void oracle_stats(long long *out8, double *meanK_meanA)
+{
+  for (int k = 0; k < 8; k++) out8[k] = om_stat[k];
+  meanK_meanA[0] = om_stat_acc_K; meanK_meanA[1] = om_stat_A;
+  for (int k = 0; k < 8; k++) om_stat[k] = 0;
+  om_stat_acc_K = om_stat_A = 0;
+}
 
 /* Parse a dataset (reference text format).  X_out may be NULL (dims only). */
 OM_API int oracle_parse(const char *text, long len, int maxs, int *N, int *M, int *nh,

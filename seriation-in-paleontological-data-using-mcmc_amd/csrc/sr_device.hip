@@ -54,25 +54,33 @@ struct KArgs {
   uint64_t *rng, *acc;
   int16_t *rec_abpi;
   double *rec_cdl;
+  unsigned long long *dbg;   /* SR_STAMPS builds: [chain][16] cycles per phase */
 };
 
 /* ---------------------------------------------------------------- LDS carve */
 struct Lay {
-  size_t tab, tbuf, lbuf, mt, P, rpi0, rpi1, nhpos, misc, total;
+  size_t tab, cbuf, lbuf, mt, P, rpi0, rpi1, nhpos, hb, ck, ccnt, sab, scnt, sd, misc, total;
 };
 __host__ __device__ static inline size_t sr_al16(size_t x) { return (x + 15) & ~(size_t)15; }
-__host__ __device__ static inline Lay sr_layout(int N, int M, int NW)
+__host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB)
 {
   Lay L;
   size_t o = 0;
+  const int KT = (M + 63) / 64;
   L.tab = o;   o = sr_al16(o + 640 * sizeof(double));
-  L.tbuf = o;  o = sr_al16(o + (size_t)M * sizeof(double));
+  L.cbuf = o;  o = sr_al16(o + (size_t)KT * 64 * sizeof(double));
   L.lbuf = o;  o = sr_al16(o + (size_t)M * sizeof(double));
   L.mt = o;    o = sr_al16(o + (size_t)SR_RING * SR_MT_N * 4);
   L.P = o;     o = sr_al16(o + (size_t)NW * M * 4);
   L.rpi0 = o;  o = sr_al16(o + (size_t)N * 4);
   L.rpi1 = o;  o = sr_al16(o + (size_t)N * 4);
   L.nhpos = o; o = sr_al16(o + (size_t)N * 4);
+  L.hb = o;    o = sr_al16(o + (size_t)NW * 4);
+  L.ck = o;    o = sr_al16(o + (size_t)((N >> 5) + 1) * TB * sizeof(double));
+  L.ccnt = o;  o = sr_al16(o + (size_t)KT * 4);
+  L.sab = o;   o = sr_al16(o + (size_t)2 * M * 4);
+  L.scnt = o;  o = sr_al16(o + (size_t)4 * M * 4);
+  L.sd = o;    o = sr_al16(o + (size_t)4 * KT * 64 * 4);
   L.misc = o;  o = sr_al16(o + 64 * 8);
   L.total = o;
   return L;
@@ -89,6 +97,10 @@ __host__ __device__ static inline Lay sr_layout(int N, int M, int NW)
 #define MS_GEN 9
 #define MS_LOGL 10
 #define MS_CAB 11
+#define MS_LLS 12
+#define MS_NEXACT 13
+#define MS_FBK 14   /* +1 prev fail, +2 here fail, +3 S==0 (slots 15,16,17) */
+#define MS_RCUR 18
 
 /* ---------------------------------------------------------------- sync */
 template <bool WAVE>
@@ -103,17 +115,31 @@ __device__ __forceinline__ void gsync()
   }
 }
 
+/* ---------------------------------------------------------------- stamps */
+#ifdef SR_STAMPS
+#define STAMP_DECL unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long st_t = __builtin_amdgcn_s_memtime();
+#define STAMP(ph) do { unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[ph] += t_ - st_t; st_t = t_; } while (0)
+#define STAMP_STORE(dst) do { if ((threadIdx.x & 63) == 0 && (dst)) for (int q_ = 0; q_ < 8; ++q_) \
+  (dst)[(blockIdx.x * 17 + 1 + (threadIdx.x >> 6)) * 8 + q_] += st_acc[q_]; } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(ph) do { } while (0)
+#define STAMP_STORE(dst) do { } while (0)
+#endif
+
 /* ---------------------------------------------------------------- RNG */
 struct DRng {
   uint32_t *ring;   /* LDS, SR_RING blocks of 624 raw words */
   uint32_t blk, off, gen;   /* next word = block blk, index off; blocks [.., gen) exist */
 };
 
+/* generate block `gen` from block gen-1 (three dependency phases of the MT recurrence);
+ * by-value arguments so the caller's cursor never escapes to scratch */
 template <bool WAVE>
-__device__ __noinline__ void rng_gen(DRng &r, int t, int nthr)
+__device__ __noinline__ void rng_gen_block(uint32_t *ring, uint32_t gen, int t, int nthr)
 {
-  const uint32_t *prev = r.ring + ((r.gen - 1) & (SR_RING - 1)) * SR_MT_N;
-  uint32_t *nxt = r.ring + (r.gen & (SR_RING - 1)) * SR_MT_N;
+  const uint32_t *prev = ring + ((gen - 1) & (SR_RING - 1)) * SR_MT_N;
+  uint32_t *nxt = ring + (gen & (SR_RING - 1)) * SR_MT_N;
   for (int k = t; k < 227; k += nthr) nxt[k] = sr_mt_mix(prev[k], prev[k + 1], prev[k + 397]);
   gsync<WAVE>();
   for (int k = 227 + t; k < 454; k += nthr) nxt[k] = sr_mt_mix(prev[k], prev[k + 1], nxt[k - 227]);
@@ -121,6 +147,12 @@ __device__ __noinline__ void rng_gen(DRng &r, int t, int nthr)
   for (int k = 454 + t; k < 624; k += nthr)
     nxt[k] = (k < 623) ? sr_mt_mix(prev[k], prev[k + 1], nxt[k - 227]) : sr_mt_mix(prev[623], nxt[0], nxt[396]);
   gsync<WAVE>();
+}
+
+template <bool WAVE>
+__device__ __forceinline__ void rng_gen(DRng &r, int t, int nthr)
+{
+  rng_gen_block<WAVE>(r.ring, r.gen, t, nthr);
   r.gen++;
 }
 
@@ -175,8 +207,34 @@ __device__ __forceinline__ uint32_t rng_uniform_int(DRng &r, uint32_t n, int t, 
   return k;
 }
 
+/* gsl_rng_uniform_int(n) with its divisor scale = 0xffffffff/n precomputed; the quotient
+ * get()/scale is taken from a double reciprocal and corrected to the exact integer. */
+struct UDiv { uint32_t n, scale; double rs; };
+__device__ __forceinline__ UDiv make_udiv(uint32_t n)
+{
+  UDiv u;
+  u.n = n;
+  u.scale = 0xffffffffu / n;
+  u.rs = 1.0 / (double)u.scale;
+  return u;
+}
+template <bool WAVE>
+__device__ __forceinline__ uint32_t rng_uint_fast(DRng &r, const UDiv &u, int t, int nthr)
+{
+  uint32_t k;
+  do {
+    const uint32_t g = rng_get<WAVE>(r, t, nthr);
+    uint32_t q = (uint32_t)((double)g * u.rs);
+    const uint64_t qs = (uint64_t)q * u.scale;
+    if (qs > g) q--;
+    else if (g - (uint32_t)qs >= u.scale) q++;
+    k = q;
+  } while (k >= u.n);
+  return k;
+}
+
 /* ------------------------------------------------ GSL beta/gamma/ziggurat (wave 0) */
-__device__ double d_gauss_zig(DRng &r, int lane, const sr_mtab &tb)
+__device__ __forceinline__ double d_gauss_zig(DRng &r, int lane, const sr_mtab &tb)
 {
   for (;;) {
     uint32_t k = rng_get<true>(r, lane, 64);
@@ -201,7 +259,7 @@ __device__ double d_gauss_zig(DRng &r, int lane, const sr_mtab &tb)
   }
 }
 
-__device__ double d_gamma(DRng &r, double a, int lane, const sr_mtab &tb)
+__device__ __forceinline__ double d_gamma(DRng &r, double a, int lane, const sr_mtab &tb)
 {
   double boost = 1.0;
   if (a < 1) { /* unreachable from the sampler (a = 1 + count); kept for GSL parity */
@@ -227,7 +285,7 @@ __device__ double d_gamma(DRng &r, double a, int lane, const sr_mtab &tb)
 }
 
 /* mcmc_samplebeta: y = beta(1+a, 1+b); keep the old value unless log y in [low, high] */
-__device__ double d_samplebeta(DRng &r, double x, double a, double b, double low, double high, int lane,
+__device__ __forceinline__ double d_samplebeta(DRng &r, double x, double a, double b, double low, double high, int lane,
                                const sr_mtab &tb)
 {
   double x1 = d_gamma(r, 1. + a, lane, tb);
@@ -292,8 +350,8 @@ struct BitWalk {
 /* mcmc_auxa + mcmc_logtop + mcmc_randompick for one limit of one taxon, in walk
  * coordinates (fwd: walk w = position w; rev: walk w = position N-1-w).  o = current limit,
  * entries w = 0..L.  Returns the picked entry and the count deltas dt0,df0,dt1,df1 there. */
-__device__ int draw_limit(const uint32_t *Pm, int M, int N, bool rev, int o, int L, double u, const CD &k,
-                          const sr_mtab &tb, int &dt0, int &df0, int &dt1, int &df1)
+__device__ __forceinline__ int draw_exact(const uint32_t *Pm, int M, int N, bool rev, int o, int L, double u,
+                                      const CD &k, const sr_mtab &tb, int &dt0, int &df0, int &dt1, int &df1)
 {
   const int POo = rev ? ones_range(Pm, M, N - o, N) : ones_range(Pm, M, 0, o);
   auto q_at = [&](int w, int PO) -> double {
@@ -359,7 +417,170 @@ __device__ int draw_limit(const uint32_t *Pm, int M, int N, bool rev, int o, int
   return res;
 }
 
-__device__ __forceinline__ int ininterval(int i, int a, int b, int inc1, int inc2)
+
+/* 32 walk bits [32k, 32k+32): fwd = positions, rev = positions N-1-w (bit i = walk 32k+i) */
+__device__ __forceinline__ uint32_t walk_word(const uint32_t *Pm, int M, int N, int NW, bool rev, int k)
+{
+  if (!rev) return (k < NW) ? Pm[k * M] : 0u;
+  const int s = N - 32 - 32 * k;
+  uint32_t v;
+  if (s >= 0) {
+    const int wi = s >> 5, sh = s & 31;
+    const uint32_t lo = Pm[wi * M];
+    const uint32_t hi = (sh && wi + 1 < NW) ? Pm[(wi + 1) * M] : 0u;
+    v = sh ? ((lo >> sh) | (hi << (32 - sh))) : lo;
+  } else {
+    v = (s > -32) ? (Pm[0] << (-s)) : 0u;
+  }
+  return __brev(v);
+}
+
+/* ones among walk positions [0, w) */
+__device__ __forceinline__ int walk_prefix(const uint32_t *Pm, int M, int N, int NW, bool rev, int w)
+{
+  int s = 0;
+  const int full = w >> 5;
+  for (int k = 0; k < full; ++k) s += __popc(walk_word(Pm, M, N, NW, rev, k));
+  if (w & 31) s += __popc(walk_word(Pm, M, N, NW, rev, full) & ((1u << (w & 31)) - 1u));
+  return s;
+}
+
+#define SR_CERT_REL 0x1p-20  /* relative accuracy of the approximate CDF (2 x the exp error bound) */
+#define SR_CERT_ABS 0x1p-36  /* absolute slack: reference rounding + clamped LOGEPSILON terms */
+
+/* 2^q (q <= ~0) to ~1.6e-7 relative: exact f64 split q = n + f, f in [0,1), v_exp_f32(f) */
+__device__ __forceinline__ double exp2_split(double q)
+{
+  const double n = __builtin_floor(q);
+  if (n < -1070.0) return 0.0;
+  const float y = __builtin_amdgcn_exp2f((float)(q - n));
+  return __builtin_amdgcn_ldexp((double)y, (int)n);
+}
+
+/* mcmc_auxa + mcmc_logtop + mcmc_randompick for one limit of one taxon (exact version:
+ * draw_exact), certified fast path.  The picked index depends only on where u falls in the
+ * cumulative distribution F_k = sum_{i<=k} y_i / x.  We evaluate F_k approximately -- q by
+ * incremental f64 updates (q(w+1) = q(w) - val(bit_w), val(0) = d - cc, val(1) = dd - c, in
+ * log2 units), y = 2^(q - z) via exp2_split -- so that |F^_k - F_k| <= 2^-21 min(F, 1-F) +
+ * 2^-40, and accept index k only if u - F^_{k-1} and F^_k - u both exceed that bound (with 2x
+ * margin, SR_CERT_*): then the reference's exact sequential computation provably returns the
+ * same k.  Otherwise (probability ~1e-5 per draw) the exact path runs.
+ * ck: this lane's checkpoint slots (stride ckstride). */
+__device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int NW, bool rev, int o, int L, double u,
+                                         const CD &K, const sr_mtab &tb, double vA, double vB, double *ck,
+                                         int ckstride, uint64_t *fbk, int &dt0, int &df0, int &dt1, int &df1)
+{
+  const int POo = walk_prefix(Pm, M, N, NW, rev, o);
+  const int nk = (L >> 5) + 1;
+  const double q0 = (double)(o - POo) * vA + (double)POo * vB;   /* q(0), log2 units */
+  /* pass 1: max */
+  double z = q0;
+  {
+    double q = q0;
+    for (int k = 0; k < nk; ++k) {
+      const uint32_t ww = walk_word(Pm, M, N, NW, rev, k);
+      const int bmax = min(32, L + 1 - 32 * k);
+#pragma unroll
+      for (int b = 0; b < 32; ++b) {
+        z = fmax(z, (b < bmax) ? q : -__builtin_inf());
+        q = q - (((ww >> b) & 1u) ? vB : vA);
+      }
+    }
+  }
+  /* pass 2: S_k = sum 2^(q - z), checkpoint after every 32 entries */
+  double S = 0.0;
+  {
+    double q = q0 - z;
+    double S1 = 0.0;
+    for (int k = 0; k < nk; ++k) {
+      const uint32_t ww = walk_word(Pm, M, N, NW, rev, k);
+      const int bmax = min(32, L + 1 - 32 * k);
+#pragma unroll
+      for (int b = 0; b < 32; b += 2) {
+        const double y0 = exp2_split(q);
+        q = q - (((ww >> b) & 1u) ? vB : vA);
+        const double y1 = exp2_split(q);
+        q = q - (((ww >> (b + 1)) & 1u) ? vB : vA);
+        S += (b < bmax) ? y0 : 0.0;
+        S1 += (b + 1 < bmax) ? y1 : 0.0;
+      }
+      ck[k * ckstride] = S + S1;
+    }
+    S = S + S1;
+  }
+  /* pass 3: locate the segment, recompute it, certify */
+  int res = -1;
+  if (S > 0.0) {
+    const double inv = 1.0 / S;
+    int j = 0;
+    while (j < nk - 1 && ck[j * ckstride] * inv < u) ++j;
+    double Sp = (j == 0) ? 0.0 : ck[(j - 1) * ckstride];
+    double tprev = u - Sp * inv;
+    double eprev = SR_CERT_REL * fmin(Sp, S - Sp) * inv + SR_CERT_ABS;
+    const int w0 = 32 * j;
+    const int PO0 = walk_prefix(Pm, M, N, NW, rev, w0);
+    double q = (w0 <= o) ? ((double)((o - w0) - (POo - PO0)) * vA + (double)(POo - PO0) * vB)
+                         : -((double)((w0 - o) - (PO0 - POo)) * vA + (double)(PO0 - POo) * vB);
+    q = q - z;
+    const uint32_t ww = walk_word(Pm, M, N, NW, rev, j);
+    const int bmax = min(32, L + 1 - w0);
+    for (int b = 0; b < bmax; ++b) {
+      const int w = w0 + b;
+      Sp += exp2_split(q);
+      const double t = u - Sp * inv;
+      const double e = SR_CERT_REL * fmin(Sp, S - Sp) * inv + SR_CERT_ABS;
+      if (t < 0.0 || w == L) {
+        const bool prev_ok = (w == 0) || (tprev > eprev);
+        const bool here_ok = (w == L) || (t < -e);
+        if (prev_ok && here_ok) res = w;
+#ifdef SR_STAMPS
+        else atomicAdd((unsigned long long *)fbk + (prev_ok ? 2 : 1), 1ull);
+#endif
+        break;
+      }
+      tprev = t;
+      eprev = e;
+      q = q - (((ww >> b) & 1u) ? vB : vA);
+    }
+  }
+  if (res < 0) {
+#ifdef SR_STAMPS
+    atomicAdd((unsigned long long *)fbk, 1ull);
+    if (!(S > 0.0)) atomicAdd((unsigned long long *)fbk + 3, 1ull);
+#endif
+    return draw_exact(Pm, M, N, rev, o, L, u, K, tb, dt0, df0, dt1, df1);
+  }
+  const int POp = walk_prefix(Pm, M, N, NW, rev, res);
+  if (res == o) { dt0 = df0 = dt1 = df1 = 0; }
+  else if (res < o) { int O = POo - POp; int Z = (o - res) - O; dt0 = -Z; df0 = Z; dt1 = O; df1 = -O; }
+  else { int O = POp - POo; int Z = (res - o) - O; dt0 = Z; df0 = -Z; dt1 = -O; df1 = O; }
+  return res;
+}
+
+/* bits of positions [lo, hi] inside word w */
+__device__ __forceinline__ uint32_t range_mask(int w, int lo, int hi)
+{
+  const int b0 = 32 * w;
+  lo = max(lo, b0);
+  hi = min(hi, b0 + 31);
+  if (hi < lo) return 0u;
+  const int n = hi - lo + 1;
+  return (n == 32) ? 0xffffffffu : (((1u << n) - 1u) << (lo - b0));
+}
+
+/* ones of column m in [lo, mid) and [mid, hi) (one pass over the words) */
+__device__ __forceinline__ void ones_split(const uint32_t *Pm, int M, int lo, int mid, int hi, int &O1, int &O2)
+{
+  O1 = 0; O2 = 0;
+  if (hi <= lo) return;
+  for (int w = lo >> 5; w <= ((hi - 1) >> 5); ++w) {
+    const uint32_t word = Pm[w * M];
+    O1 += __popc(word & range_mask(w, lo, mid - 1));
+    O2 += __popc(word & range_mask(w, mid, hi - 1));
+  }
+}
+
+__device__ __forceinline__ int ininterval(int i, int a, int b, int inc1, int inc2)   /* mcmc.c:1097-1124 */
 {
   int r;
   if (a > b) { r = a; a = b; b = r; }
@@ -368,11 +589,15 @@ __device__ __forceinline__ int ininterval(int i, int a, int b, int inc1, int inc
   return r;
 }
 
+/* hard-site positions hp[0..nh) are ascending (their relative order never changes) */
 __device__ __forceinline__ int hard_count(const int *hp, int nh, int lo, int hi)
 {
   int s = 0;
 #pragma unroll
-  for (int k = 0; k < SR_NHMAX; ++k) s += (k < nh && hp[k] >= lo && hp[k] <= hi) ? 1 : 0;
+  for (int k = 0; k < SR_NHMAX; ++k) {
+    if (k >= nh) break;
+    s += (hp[k] >= lo && hp[k] <= hi) ? 1 : 0;
+  }
   return s;
 }
 
@@ -380,57 +605,77 @@ __device__ __forceinline__ bool is_hard(const int *hp, int nh, int p)
 {
   bool h = false;
 #pragma unroll
-  for (int k = 0; k < SR_NHMAX; ++k) h |= (k < nh && hp[k] == p);
+  for (int k = 0; k < SR_NHMAX; ++k) {
+    if (k >= nh) break;
+    h |= (hp[k] == p);
+  }
   return h;
 }
 
-/* sequential sum of tbuf[0..M) in ascending m, skipping +-0 terms (exact: s never
- * becomes -0.0), on wave 0; result broadcast.  Two barriers. */
-__device__ __forceinline__ double ordered_sum(const double *buf, int M, double *slot, int tid)
+__device__ __forceinline__ void wsync()
 {
-  __syncthreads();
-  if (tid < 64) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+/* Exact delta on wave 0: the reference's sequential `delta += term` over ascending m
+ * (mcmc.c:1214, 1435, 1630).  Zero terms are skipped (adding +-0 is exact; s is never -0.0).
+ * Nonzero terms were compacted per 64-taxon chunk (ascending m) into cbuf with counts ccnt. */
+__device__ __forceinline__ double exact_sum_w0(const double *cbuf, const int *ccnt, int nch, double *slot, int lane)
+{
+  wsync();
+  if (lane == 0) {
     double s = 0.0;
-    for (int base = 0; base < M; base += 64) {
-      int m = base + tid;
-      double t = (m < M) ? buf[m] : 0.0;
-      uint64_t mask = __ballot(t != 0.0);
-      uint64_t tb = __builtin_bit_cast(uint64_t, t);
-      int tlo = (int)(uint32_t)tb, thi = (int)(uint32_t)(tb >> 32);
-      while (mask) {
-        int l = __builtin_ctzll(mask);
-        mask &= mask - 1;
-        uint32_t a = (uint32_t)__builtin_amdgcn_readlane(tlo, l);
-        uint32_t b = (uint32_t)__builtin_amdgcn_readlane(thi, l);
-        s = s + __builtin_bit_cast(double, ((uint64_t)b << 32) | a);
+    for (int ch = 0; ch < nch; ++ch) {
+      const int n = ccnt[ch];
+      const double *p = cbuf + ch * 64;
+      int j = 0;
+      for (; j + 4 <= n; j += 4) {
+        const double a0 = p[j], a1 = p[j + 1], a2 = p[j + 2], a3 = p[j + 3];
+        s = s + a0; s = s + a1; s = s + a2; s = s + a3;
       }
+      for (; j < n; ++j) s = s + p[j];
     }
-    if (tid == 0) *slot = s;
+    *slot = s;
   }
-  __syncthreads();
+  wsync();
   return *slot;
 }
 
 /* ---------------------------------------------------------------- kernel */
-template <int TB, int TPT>
+/* One workgroup per chain.  Phases of one sweep (mcmc.c:225-244):
+ *   A  wave 0:   totals, c and d (GSL beta via gamma/ziggurat)          -> barrier
+ *   B  all:      Gibbs (a_m, b_m) for all taxa (thread per taxon)         -> barrier
+ *   C  wave 0:   logl (last sweep of a call), 16 MH permutation proposals
+ * Per-taxon state (a, b, t0, f0, t1, f1) and the position-ordered columns P live in LDS;
+ * in phase C lane l owns taxa l, l+64, ..., so phase C needs no block barrier at all. */
+template <int TB>
 __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const bool w0 = tid < 64;
   const int chain = blockIdx.x;
   const int N = A.N, M = A.M, NW = A.NW, nh = A.nh;
-  const Lay L = sr_layout(N, M, NW);
+  const int KT = (M + 63) >> 6;
+  const Lay L = sr_layout(N, M, NW, TB);
   double *tabs = (double *)(smem + L.tab);
-  double *tbuf = (double *)(smem + L.tbuf);
+  double *cbuf = (double *)(smem + L.cbuf);
   double *lbuf = (double *)(smem + L.lbuf);
   uint32_t *ring = (uint32_t *)(smem + L.mt);
   uint32_t *P = (uint32_t *)(smem + L.P);
   int32_t *rpiA = (int32_t *)(smem + L.rpi0);
   int32_t *rpiB = (int32_t *)(smem + L.rpi1);
   int32_t *nhpos = (int32_t *)(smem + L.nhpos);
+  uint32_t *Hb = (uint32_t *)(smem + L.hb);
+  double *ckb = (double *)(smem + L.ck);
+  int *ccnt = (int *)(smem + L.ccnt);
+  int32_t *sab = (int32_t *)(smem + L.sab);     /* a[M], b[M] */
+  int32_t *scnt = (int32_t *)(smem + L.scnt);   /* t0[M], f0[M], t1[M], f1[M] */
+  int32_t *sd = (int32_t *)(smem + L.sd);       /* proposal deltas [4][KT*64] */
   uint64_t *misc = (uint64_t *)(smem + L.misc);
-  int *tot = (int *)(misc + MS_TOT);
-  double *dslot = (double *)(misc + MS_DELTA);
+  double *dmisc = (double *)misc;
 
   /* ---- load tables and state */
   for (int i = tid; i < 128; i += TB) {
@@ -442,43 +687,31 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   }
   sr_mtab tb;
   tb.exp_thi = tabs; tb.exp_tlo = tabs + 128; tb.log_invc = tabs + 256; tb.log_lhi = tabs + 384; tb.log_llo = tabs + 512;
-
-  const uint32_t *gP = A.P + (size_t)chain * NW * M;
-  for (int i = tid; i < NW * M; i += TB) P[i] = gP[i];
-  const int32_t *grpi = A.rpi + (size_t)chain * N;
-  for (int i = tid; i < N; i += TB) rpiA[i] = grpi[i];
-  const uint32_t *gmt = A.mt + (size_t)chain * SR_RING * SR_MT_N;
-  for (int i = tid; i < SR_RING * SR_MT_N; i += TB) ring[i] = gmt[i];
-  if (tid < 4) tot[tid] = 0;
-  if (tid == 0) misc[MS_CAB] = 0;
+  {
+    const uint32_t *gP = A.P + (size_t)chain * NW * M;
+    for (int i = tid; i < NW * M; i += TB) P[i] = gP[i];
+    const int32_t *grpi = A.rpi + (size_t)chain * N;
+    for (int i = tid; i < N; i += TB) rpiA[i] = grpi[i];
+    const uint32_t *gmt = A.mt + (size_t)chain * SR_RING * SR_MT_N;
+    for (int i = tid; i < SR_RING * SR_MT_N; i += TB) ring[i] = gmt[i];
+    const int32_t *gab = A.ab + (size_t)chain * 2 * M;
+    for (int i = tid; i < 2 * M; i += TB) sab[i] = gab[i];
+    const int32_t *gcnt = A.cnt + (size_t)chain * 4 * M;
+    for (int i = tid; i < 4 * M; i += TB) scnt[i] = gcnt[i];
+  }
+  if (tid == 0) for (int q = 0; q < 24; ++q) misc[MS_CAB + q] = 0;
 
   int hp[SR_NHMAX];
 #pragma unroll
   for (int k = 0; k < SR_NHMAX; ++k) hp[k] = (k < nh) ? A.hp[(size_t)chain * SR_NHMAX + k] : -1;
-
-  int a_[TPT], b_[TPT], t0_[TPT], f0_[TPT], t1_[TPT], f1_[TPT];
-#pragma unroll
-  for (int k = 0; k < TPT; ++k) {
-    int m = tid + k * TB;
-    if (m < M) {
-      a_[k] = A.ab[(size_t)chain * 2 * M + m];
-      b_[k] = A.ab[(size_t)chain * 2 * M + M + m];
-      t0_[k] = A.cnt[(size_t)chain * 4 * M + m];
-      f0_[k] = A.cnt[(size_t)chain * 4 * M + M + m];
-      t1_[k] = A.cnt[(size_t)chain * 4 * M + 2 * M + m];
-      f1_[k] = A.cnt[(size_t)chain * 4 * M + 3 * M + m];
-    } else {
-      a_[k] = b_[k] = t0_[k] = f0_[k] = t1_[k] = f1_[k] = 0;
-    }
-  }
   double c = A.cdl[(size_t)chain * 4 + 0];
   double d = A.cdl[(size_t)chain * 4 + 1];
-  double loglik = A.cdl[(size_t)chain * 4 + 2];   /* meaningful in wave 0 */
+  double loglik = A.cdl[(size_t)chain * 4 + 2];   /* maintained by wave 0 */
   DRng R;
   R.ring = ring;
   {
-    uint64_t pos = A.rng[(size_t)chain * 2 + 0];
-    uint64_t gen = A.rng[(size_t)chain * 2 + 1];
+    const uint64_t pos = A.rng[(size_t)chain * 2 + 0];
+    const uint64_t gen = A.rng[(size_t)chain * 2 + 1];
     R.blk = (uint32_t)(pos / SR_MT_N);
     R.off = (uint32_t)(pos % SR_MT_N);
     R.gen = (uint32_t)gen;
@@ -486,398 +719,421 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   unsigned long long acc[7];
 #pragma unroll
   for (int k = 0; k < 7; ++k) acc[k] = 0;
-  int rcur = 0;   /* which rpi buffer is current */
+  int rcur = 0;   /* current rpi buffer (wave 0 only writes rpi) */
   __syncthreads();
 
   const double ec = sr_exp_m(SR_LOGEPSILON, &tb);
   const uint32_t nhard = (uint32_t)nh;
+  const UDiv udN = make_udiv((uint32_t)N), udN1 = make_udiv((uint32_t)(N - 1)), ud2 = make_udiv(2u);
+  const UDiv udH = make_udiv((uint32_t)N - nhard > 0 ? (uint32_t)N - nhard : 1u);
+  const UDiv udH1 = make_udiv((uint32_t)N - nhard > 1 ? (uint32_t)N - nhard - 1 : 1u);
+  STAMP_DECL
 
   for (int call = 0; call < A.calls; ++call) {
     for (int sw = 0; sw < A.spc; ++sw) {
       const bool want_logl = (sw == A.spc - 1);
-      /* ---------------- totals for samplec/sampled (mcmc.c:977-984 / count01) */
-      {
+      /* ============ phase A (wave 0): totals and the c, d draws (mcmc.c:768-825) */
+      if (w0) {
         int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-#pragma unroll
-        for (int k = 0; k < TPT; ++k)
-          if (tid + k * TB < M) { s0 += t0_[k]; s1 += f0_[k]; s2 += t1_[k]; s3 += f1_[k]; }
+        for (int m = lane; m < M; m += 64) { s0 += scnt[m]; s1 += scnt[M + m]; s2 += scnt[2 * M + m]; s3 += scnt[3 * M + m]; }
         for (int off = 32; off > 0; off >>= 1) {
           s0 += __shfl_xor(s0, off); s1 += __shfl_xor(s1, off);
           s2 += __shfl_xor(s2, off); s3 += __shfl_xor(s3, off);
         }
-        if ((tid & 63) == 0) {
-          atomicAdd(&tot[0], s0); atomicAdd(&tot[1], s1);
-          atomicAdd(&tot[2], s2); atomicAdd(&tot[3], s3);
+        double ncd[2] = {c, d};
+        for (int which = 0; which < 2; ++which) {   /* mcmc_samplec then mcmc_sampled */
+          const double ba = which ? (double)s1 : (double)s3, bb = which ? (double)s2 : (double)s0;
+          ncd[which] = d_samplebeta(R, ncd[which], ba, bb, which ? SR_MIND : SR_MINC, which ? SR_MAXD : SR_MAXC, lane, tb);
         }
-      }
-      rng_ensure(R, 128, tid, TB);
-      __syncthreads();
-      /* ---------------- c, d (wave 0) */
-      if (tid < 64) {
-        const int t0a = tot[0], f0a = tot[1], t1a = tot[2], f1a = tot[3];
-        double nc = d_samplebeta(R, c, (double)f1a, (double)t0a, SR_MINC, SR_MAXC, tid, tb);
-        double nd = d_samplebeta(R, d, (double)f0a, (double)t1a, SR_MIND, SR_MAXD, tid, tb);
-        if (tid == 0) {
-          ((double *)misc)[MS_C] = nc;
-          ((double *)misc)[MS_D] = nd;
-          ((double *)misc)[MS_CC] = sr_log_m(1. - sr_exp_m(nc, &tb), &tb);
-          ((double *)misc)[MS_DD] = sr_log_m(1. - sr_exp_m(nd, &tb), &tb);
+        c = ncd[0];
+        d = ncd[1];
+        if (lane == 0) {
+          dmisc[MS_C] = c;
+          dmisc[MS_D] = d;
+          dmisc[MS_CC] = sr_log_m(1. - sr_exp_m(c, &tb), &tb);
+          dmisc[MS_DD] = sr_log_m(1. - sr_exp_m(d, &tb), &tb);
           misc[MS_BLK] = R.blk; misc[MS_OFF] = R.off; misc[MS_GEN] = R.gen;
-          tot[0] = tot[1] = tot[2] = tot[3] = 0;
+          acc[0]++; acc[1]++;
         }
       }
+      STAMP(0);
       __syncthreads();
-      c = ((double *)misc)[MS_C];
-      d = ((double *)misc)[MS_D];
+      c = dmisc[MS_C];
+      d = dmisc[MS_D];
       CD K;
-      K.c = c; K.d = d;
-      K.cc = ((double *)misc)[MS_CC];
-      K.dd = ((double *)misc)[MS_DD];
-      K.ec = ec;
+      K.c = c; K.d = d; K.cc = dmisc[MS_CC]; K.dd = dmisc[MS_DD]; K.ec = ec;
       R.blk = (uint32_t)misc[MS_BLK]; R.off = (uint32_t)misc[MS_OFF]; R.gen = (uint32_t)misc[MS_GEN];
-      if (tid == 0) { acc[0]++; acc[1]++; }
+      /* one position's value in q (log2 units): zero -> d - cc, one -> dd - c */
+      const double vA = (K.d - K.cc) * 1.4426950408889634;
+      const double vB = (K.dd - K.c) * 1.4426950408889634;
 
-      /* ---------------- (a, b) Gibbs update (mcmc_sampleab) */
+      /* ============ phase B (all): Gibbs update of every (a_m, b_m) (mcmc_sampleab) */
       rng_ensure(R, 2 * M, tid, TB);
       {
         unsigned long long nchg = 0;
-#pragma unroll
-        for (int k = 0; k < TPT; ++k) {
-          const int m = tid + k * TB;
-          if (m < M) {
-            const uint32_t *Pm = P + m;
-            const double ua = rng_peek(R, 2 * m) / 4294967296.0;
-            const double ub = rng_peek(R, 2 * m + 1) / 4294967296.0;
-            int d0, e0, d1, e1;
-            int na = draw_limit(Pm, M, N, false, a_[k], b_[k], ua, K, tb, d0, e0, d1, e1);
-            t0_[k] += d0; f0_[k] += e0; t1_[k] += d1; f1_[k] += e1;
-            nchg += (na != a_[k]);
-            a_[k] = na;
-            int t = draw_limit(Pm, M, N, true, N - b_[k], N - na, ub, K, tb, d0, e0, d1, e1);
-            t0_[k] += d0; f0_[k] += e0; t1_[k] += d1; f1_[k] += e1;
-            int nb = N - t;
-            nchg += (nb != b_[k]);
-            b_[k] = nb;
-            if (want_logl)
-              lbuf[m] = (double)t0_[k] * K.cc + (double)f0_[k] * K.d + (double)t1_[k] * K.dd + (double)f1_[k] * K.c;
-          }
+        for (int m = tid; m < M; m += TB) {
+          const uint32_t *Pm = P + m;
+          const double ua = rng_peek(R, 2 * m) / 4294967296.0;
+          const double ub = rng_peek(R, 2 * m + 1) / 4294967296.0;
+          const int a0 = sab[m], b0 = sab[M + m];
+          int t0 = scnt[m], f0 = scnt[M + m], t1 = scnt[2 * M + m], f1 = scnt[3 * M + m];
+          int d0, e0, d1, e1;
+          const int na = draw_fast(Pm, M, N, NW, false, a0, b0, ua, K, tb, vA, vB, ckb + tid, TB, &misc[MS_FBK], d0, e0, d1, e1);
+          t0 += d0; f0 += e0; t1 += d1; f1 += e1;
+          const int tt = draw_fast(Pm, M, N, NW, true, N - b0, N - na, ub, K, tb, vA, vB, ckb + tid, TB, &misc[MS_FBK], d0, e0, d1, e1);
+          t0 += d0; f0 += e0; t1 += d1; f1 += e1;
+          const int nb = N - tt;
+          nchg += (na != a0) + (nb != b0);
+          sab[m] = na; sab[M + m] = nb;
+          scnt[m] = t0; scnt[M + m] = f0; scnt[2 * M + m] = t1; scnt[3 * M + m] = f1;
+          if (want_logl)   /* mcmc_logl term (mcmc.c:643-644) */
+            lbuf[m] = (double)t0 * K.cc + (double)f0 * K.d + (double)t1 * K.dd + (double)f1 * K.c;
         }
         for (int off = 32; off > 0; off >>= 1) nchg += __shfl_xor(nchg, off);
-        if ((tid & 63) == 0 && nchg) atomicAdd((unsigned long long *)&misc[MS_CAB], nchg);
+        if (lane == 0 && nchg) atomicAdd((unsigned long long *)&misc[MS_CAB], nchg);
       }
       rng_skip(R, 2 * M);
-      if (want_logl) {
-        __syncthreads();
-        if (tid < 64) {
-          double s = 0.0;
-          for (int base = 0; base < M; base += 64) {
-            int m = base + tid;
-            double t = (m < M) ? lbuf[m] : 0.0;
-            uint64_t tbits = __builtin_bit_cast(uint64_t, t);
-            int tlo = (int)(uint32_t)tbits, thi = (int)(uint32_t)(tbits >> 32);
-            int cnt = min(64, M - base);
-            for (int l = 0; l < cnt; ++l) {
-              uint32_t lo32 = (uint32_t)__builtin_amdgcn_readlane(tlo, l);
-              uint32_t hi32 = (uint32_t)__builtin_amdgcn_readlane(thi, l);
-              s = s + __builtin_bit_cast(double, ((uint64_t)hi32 << 32) | lo32);
-            }
-          }
-          loglik = s;
-        }
-      }
+      STAMP(1);
+      __syncthreads();
+      STAMP(2);
 
-      /* ---------------- permutation proposals */
-      for (int pr = 0; pr < 16; ++pr) {
-        /* order: pi2(swap), then 5 x (pi1, pi2, pi3) (mcmc.c:237-243) */
-        const int kind = (pr == 0) ? 21 : ((pr - 1) % 3 == 0 ? 1 : ((pr - 1) % 3 == 1 ? 20 : 3));
-        int i, j, inc1 = 0, inc2 = 0, ii = 0, jj = 0, Kn = 0;
-        bool veto = false;
-        if (kind == 1) {
-          i = (int)rng_uniform_int<false>(R, (uint32_t)N, tid, TB);
-          j = (int)rng_uniform_int<false>(R, (uint32_t)(N - 1), tid, TB);
-          if (j >= i) j++;
-          ii = min(i, j); jj = max(i, j);
-          if (is_hard(hp, nh, i) && hard_count(hp, nh, ii, jj) > 1) veto = true;
-        } else if (kind == 20 || kind == 21) {
-          if (kind == 20) {
-            i = (int)rng_uniform_int<false>(R, (uint32_t)N, tid, TB);
-            j = (int)rng_uniform_int<false>(R, (uint32_t)(N - 1), tid, TB);
+      /* ============ phase C (wave 0): logl and the permutation proposals */
+      if (w0) {
+        if (want_logl) {
+          if (lane == 0) {   /* mcmc_logl (mcmc.c:639-645), sequential over m */
+            double s = 0.0;
+            int m = 0;
+            for (; m + 4 <= M; m += 4) {
+              const double a0 = lbuf[m], a1 = lbuf[m + 1], a2 = lbuf[m + 2], a3 = lbuf[m + 3];
+              s = s + a0; s = s + a1; s = s + a2; s = s + a3;
+            }
+            for (; m < M; ++m) s = s + lbuf[m];
+            dmisc[MS_LLS] = s;
+          }
+          wsync();
+          loglik = dmisc[MS_LLS];
+        }
+        for (int pr = 0; pr < 16; ++pr) {
+          /* order: pi2(swap), then 5 x (pi1, pi2, pi3) (mcmc.c:237-243) */
+          const int kind = (pr == 0) ? 21 : ((pr - 1) % 3 == 0 ? 1 : ((pr - 1) % 3 == 1 ? 20 : 3));
+          int i, j, inc1 = 0, inc2 = 0, ii = 0, jj = 0, Kn = 0;
+          bool veto = false;
+          if (kind == 1) {
+            i = (int)rng_uint_fast<true>(R, udN, lane, 64);
+            j = (int)rng_uint_fast<true>(R, udN1, lane, 64);
             if (j >= i) j++;
-            else { int t = i; i = j; j = t; }
+            ii = min(i, j); jj = max(i, j);
+            if (is_hard(hp, nh, i) && hard_count(hp, nh, ii, jj) > 1) veto = true;
+          } else if (kind == 20 || kind == 21) {
+            if (kind == 20) {
+              i = (int)rng_uint_fast<true>(R, udN, lane, 64);
+              j = (int)rng_uint_fast<true>(R, udN1, lane, 64);
+              if (j >= i) j++;
+              else { int t = i; i = j; j = t; }
+            } else {
+              i = (int)rng_uint_fast<true>(R, udN1, lane, 64);
+              j = i + 1;
+            }
+            if (hard_count(hp, nh, i, j) > 1) veto = true;
+            if (!veto) {
+              inc1 = (int)rng_uint_fast<true>(R, ud2, lane, 64);
+              inc2 = (int)rng_uint_fast<true>(R, ud2, lane, 64);
+            }
           } else {
-            i = (int)rng_uniform_int<false>(R, (uint32_t)(N - 1), tid, TB);
-            j = i + 1;
-          }
-          if (hard_count(hp, nh, i, j) > 1) veto = true;
-          if (!veto) {
-            inc1 = (int)rng_uniform_int<false>(R, 2u, tid, TB);
-            inc2 = (int)rng_uniform_int<false>(R, 2u, tid, TB);
-          }
-        } else {
-          if ((uint32_t)N - nhard < 2) { veto = true; i = j = 0; }
-          else {
-            int n0 = (int)rng_uniform_int<false>(R, (uint32_t)N - nhard, tid, TB);
-            int m0 = (int)rng_uniform_int<false>(R, (uint32_t)N - nhard - 1, tid, TB);
-            if (n0 <= m0) { i = n0; j = m0 + 1; } else { i = m0; j = n0; }
-            /* rank -> position (mcmc.c:1518-1533), hard positions ascending */
+            if ((uint32_t)N - nhard < 2) { veto = true; i = j = 0; }
+            else {
+              int n0 = (int)rng_uint_fast<true>(R, udH, lane, 64);
+              int m0 = (int)rng_uint_fast<true>(R, udH1, lane, 64);
+              if (n0 <= m0) { i = n0; j = m0 + 1; } else { i = m0; j = n0; }
+              /* rank -> position (mcmc.c:1518-1533), hard positions ascending */
 #pragma unroll
-            for (int k = 0; k < SR_NHMAX; ++k) {
-              if (k < nh) {
+              for (int k = 0; k < SR_NHMAX; ++k) {
+                if (k >= nh) break;
                 if (hp[k] <= i) { i++; j++; }
                 else if (hp[k] <= j) j++;
               }
-            }
-            inc1 = (int)rng_uniform_int<false>(R, 2u, tid, TB);
-            inc2 = (int)rng_uniform_int<false>(R, 2u, tid, TB);
-            Kn = (j - i + 1) - hard_count(hp, nh, i, j);
-            /* non-hard positions of [i, j] in order: nhpos[rank] (barrier: a previous
-               pi3's apply phase may still read nhpos when pi1/pi2 in between were vetoed) */
-            __syncthreads();
-            for (int n = i + tid; n <= j; n += TB) {
-              if (!is_hard(hp, nh, n)) nhpos[(n - i) - hard_count(hp, nh, i, n - 1)] = n;
-            }
-            __syncthreads();
-          }
-        }
-        if (veto) continue;
-
-        /* ---- per-taxon count changes and terms */
-        int dt0v[TPT], df0v[TPT], dt1v[TPT], df1v[TPT];
+              inc1 = (int)rng_uint_fast<true>(R, ud2, lane, 64);
+              inc2 = (int)rng_uint_fast<true>(R, ud2, lane, 64);
+              Kn = (j - i + 1) - hard_count(hp, nh, i, j);
+              /* non-hard positions of [i, j] in order (nhpos[rank]) and the hard bitmap */
+              for (int n = i + lane; n <= j; n += 64)
+                if (!is_hard(hp, nh, n)) nhpos[(n - i) - hard_count(hp, nh, i, n - 1)] = n;
+              for (int w = lane; w < NW; w += 64) {
+                uint32_t hbits = 0;
 #pragma unroll
-        for (int k = 0; k < TPT; ++k) {
-          const int m = tid + k * TB;
-          int dt0 = 0, df0 = 0, dt1 = 0, df1 = 0;
-          if (m < M) {
-            const uint32_t *Pm = P + m;
-            const int a = a_[k], b = b_[k];
-            if (kind == 1) {
-              int ain, bin;
-              const int v = colbit(Pm, M, i);
-              if (i < j) {
-                ain = (ii < a && a <= jj + 1);
-                bin = (ii < b && b <= jj + 1);
-                if (ain && !bin) { if (v) { dt1++; df1--; } else { dt0--; df0++; } }
-                else if (!ain && bin) { if (v) { dt1--; df1++; } else { dt0++; df0--; } }
-              } else {
-                ain = (ii <= a && a <= jj);
-                bin = (ii <= b && b <= jj);
-                if (!ain && bin) { if (v) { dt1++; df1--; } else { dt0--; df0++; } }
-                else if (ain && !bin) { if (v) { dt1--; df1++; } else { dt0++; df0--; } }
-              }
-            } else if (kind != 3) {
-              const int ain = ininterval(a, i, j + 1, inc1, inc2);
-              const int bin = ininterval(b, i, j + 1, inc1, inc2);
-              if (ain && !bin) {
-                int O1 = ones_range(Pm, M, i, a), Z1 = (a - i) - O1;
-                int O2 = ones_range(Pm, M, a, j + 1), Z2 = (j + 1 - a) - O2;
-                dt1 = O1 - O2; df1 = -O1 + O2; dt0 = -Z1 + Z2; df0 = Z1 - Z2;
-              } else if (!ain && bin) {
-                int O1 = ones_range(Pm, M, i, b), Z1 = (b - i) - O1;
-                int O2 = ones_range(Pm, M, b, j + 1), Z2 = (j + 1 - b) - O2;
-                dt1 = -O1 + O2; df1 = O1 - O2; dt0 = Z1 - Z2; df0 = -Z1 + Z2;
-              }
-            } else {
-              const int ain = ininterval(a, i, j + 1, inc1, inc2);
-              const int bin = ininterval(b, i, j + 1, inc1, inc2);
-              int na, nb;
-              if (ain && !bin) { na = i + j + 1 - a; nb = b; }
-              else if (!ain && bin) { na = a; nb = i + j + 1 - b; }
-              else if (ain && bin) { na = i + j + 1 - b; nb = i + j + 1 - a; }
-              else { na = a; nb = b; }
-              for (int r = 0; r < Kn; ++r) {
-                const int n = nhpos[r], nn = nhpos[Kn - 1 - r];
-                const int was = (a <= n && n < b), is = (na <= nn && nn < nb);
-                if (was != is) {
-                  const int v = colbit(Pm, M, n);
-                  if (was) { if (v) { dt1--; df1++; } else { df0--; dt0++; } }
-                  else { if (v) { dt1++; df1--; } else { df0++; dt0--; } }
+                for (int q = 0; q < SR_NHMAX; ++q) {
+                  if (q >= nh) break;
+                  if ((hp[q] >> 5) == w) hbits |= 1u << (hp[q] & 31);
                 }
+                Hb[w] = hbits;
+              }
+              wsync();
+            }
+          }
+          STAMP(3);
+          if (veto) continue;
+
+          /* ---- per-taxon count changes and terms (lane owns m = lane + 64k) */
+          double tsum = 0.0, tabs_ = 0.0;
+          int Kt = 0;
+          for (int k = 0; k < KT; ++k) {
+            const int m = lane + 64 * k;
+            int dt0 = 0, df0 = 0, dt1 = 0, df1 = 0;
+            if (m < M) {
+              const uint32_t *Pm = P + m;
+              const int a = sab[m], b = sab[M + m];
+              if (kind == 1) {                                   /* mcmc.c:1175-1256 */
+                int ain, bin;
+                const int v = (Pm[(i >> 5) * M] >> (i & 31)) & 1;
+                if (i < j) {
+                  ain = (ii < a && a <= jj + 1);
+                  bin = (ii < b && b <= jj + 1);
+                  if (ain && !bin) { if (v) { dt1++; df1--; } else { dt0--; df0++; } }
+                  else if (!ain && bin) { if (v) { dt1--; df1++; } else { dt0++; df0--; } }
+                } else {
+                  ain = (ii <= a && a <= jj);
+                  bin = (ii <= b && b <= jj);
+                  if (!ain && bin) { if (v) { dt1++; df1--; } else { dt0--; df0++; } }
+                  else if (ain && !bin) { if (v) { dt1--; df1++; } else { dt0++; df0--; } }
+                }
+              } else if (kind != 3) {                            /* mcmc.c:1367-1436 */
+                const int ain = ininterval(a, i, j + 1, inc1, inc2);
+                const int bin = ininterval(b, i, j + 1, inc1, inc2);
+                if (ain && !bin) {
+                  int O1, O2;
+                  ones_split(Pm, M, i, a, j + 1, O1, O2);
+                  const int Z1 = (a - i) - O1, Z2 = (j + 1 - a) - O2;
+                  dt1 = O1 - O2; df1 = -O1 + O2; dt0 = -Z1 + Z2; df0 = Z1 - Z2;
+                } else if (!ain && bin) {
+                  int O1, O2;
+                  ones_split(Pm, M, i, b, j + 1, O1, O2);
+                  const int Z1 = (b - i) - O1, Z2 = (j + 1 - b) - O2;
+                  dt1 = -O1 + O2; df1 = O1 - O2; dt0 = Z1 - Z2; df0 = -Z1 + Z2;
+                }
+              } else {                                           /* mcmc.c:1568-1631 */
+                const int ain = ininterval(a, i, j + 1, inc1, inc2);
+                const int bin = ininterval(b, i, j + 1, inc1, inc2);
+                int na, nb;
+                if (ain && !bin) { na = i + j + 1 - a; nb = b; }
+                else if (!ain && bin) { na = a; nb = i + j + 1 - b; }
+                else if (ain && bin) { na = i + j + 1 - b; nb = i + j + 1 - a; }
+                else { na = a; nb = b; }
+                /* by words: was-alive = [a,b) n [i,j]; is-alive after the move (the site at n
+                   goes to p[n]) = hard positions in [na,nb) plus the non-hard positions whose
+                   mirrored rank lands in [na,nb): ranks [Kn-s_hi, Kn-s_lo) */
+                const int xa = min(max(na, i), j + 1), xb = min(max(nb, i), j + 1);
+                const int s_lo = (xa - i) - hard_count(hp, nh, i, xa - 1);
+                const int s_hi = (xb - i) - hard_count(hp, nh, i, xb - 1);
+                int pl = 1, ph = 0;
+                if (s_lo < s_hi) { pl = nhpos[Kn - s_hi]; ph = nhpos[Kn - s_lo - 1]; }
+                for (int w = i >> 5; w <= (j >> 5); ++w) {
+                  const uint32_t rng = range_mask(w, i, j);
+                  const uint32_t H = Hb[w];
+                  const uint32_t Wm = range_mask(w, max(a, i), min(b - 1, j)) & rng;
+                  const uint32_t Im = ((range_mask(w, pl, ph) & ~H) | (range_mask(w, max(na, i), min(nb - 1, j)) & H)) & rng;
+                  const uint32_t dying = Wm & ~Im, born = Im & ~Wm;
+                  const uint32_t col = Pm[w * M];
+                  const int od = __popc(col & dying), zd = __popc(dying) - od;
+                  const int ob = __popc(col & born), zb = __popc(born) - ob;
+                  dt1 += ob - od; df1 += od - ob; dt0 += zd - zb; df0 += zb - zd;
+                }
+              }
+            }
+            const double tv = (m < M) ? qval(dt0, df0, dt1, df1, K) : 0.0;
+            const uint64_t msk = __ballot(tv != 0.0);
+            const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
+            if (tv != 0.0) cbuf[k * 64 + pos] = tv;
+            if (lane == 0) ccnt[k] = __popcll(msk);
+            Kt += __popcll(msk);
+            tsum += tv;
+            tabs_ += __builtin_fabs(tv);
+            sd[k * 64 + lane] = dt0; sd[(KT + k) * 64 + lane] = df0;
+            sd[(2 * KT + k) * 64 + lane] = dt1; sd[(3 * KT + k) * 64 + lane] = df1;
+          }
+          for (int off = 32; off > 0; off >>= 1) {
+            tsum += __shfl_xor(tsum, off);
+            tabs_ += __shfl_xor(tabs_, off);
+          }
+          STAMP(4);
+          /* ---- certified MH decision (mcmc.c:1261 / 1441 / 1636).  S = tree sum of the terms,
+             A = sum |t|, Kt = #nonzero: |sequential delta - S| <= (Kt + 14) 2^-53 A (1+eps), so
+             E = (Kt + 64) 2^-52 A decides "delta >= 0" and "delta > log u" unless the true value
+             is within E; then (and whenever the exact delta feeds a saved loglik) the exact
+             sequential sum runs.  uniform_pos is drawn only once delta < 0 is known. */
+          const double Eb = ((double)Kt + 64.0) * 0x1p-52 * tabs_;
+          double delta = 0.0, lu = 0.0;
+          bool have_exact = false, drew = false;
+          int state;   /* 0 reject, 1 accept, 2 undecided */
+          if (Kt == 0) { have_exact = true; state = 1; }
+          else if (tsum > Eb) state = 1;
+          else if (tsum < -Eb) {
+            lu = sr_log_m(rng_uniform_pos<true>(R, lane, 64), &tb);
+            drew = true;
+            state = (tsum - Eb > lu) ? 1 : ((tsum + Eb < lu) ? 0 : 2);
+          } else state = 2;
+          if (state == 2) {
+            delta = exact_sum_w0(cbuf, ccnt, KT, &dmisc[MS_DELTA], lane);
+            have_exact = true;
+            if (lane == 0) misc[MS_NEXACT]++;
+            if (delta >= 0.) state = 1;
+            else {
+              if (!drew) lu = sr_log_m(rng_uniform_pos<true>(R, lane, 64), &tb);
+              state = (delta > lu) ? 1 : 0;
+            }
+          }
+          STAMP(5);
+          if (state == 0) continue;
+          if (want_logl && !have_exact) delta = exact_sum_w0(cbuf, ccnt, KT, &dmisc[MS_DELTA], lane);
+          if (lane == 0) acc[kind == 1 ? 3 : kind == 20 ? 4 : kind == 21 ? 5 : 6]++;
+          loglik += delta;
+          /* ---- apply: limits, counts, columns (lane-private taxa) */
+          for (int k = 0; k < KT; ++k) {
+            const int m = lane + 64 * k;
+            if (m >= M) continue;
+            uint32_t *Pm = P + m;
+            const int a = sab[m], b = sab[M + m];
+            scnt[m] += sd[k * 64 + lane];
+            scnt[M + m] += sd[(KT + k) * 64 + lane];
+            scnt[2 * M + m] += sd[(2 * KT + k) * 64 + lane];
+            scnt[3 * M + m] += sd[(3 * KT + k) * 64 + lane];
+            if (kind == 1) {                                     /* mcmc.c:1266-1297 */
+              if (i < j) {
+                if (ii < a && a <= jj + 1) sab[m] = a - 1;
+                if (ii < b && b <= jj + 1) sab[M + m] = b - 1;
+                const uint32_t vb = (Pm[(i >> 5) * M] >> (i & 31)) & 1u;
+                for (int w = i >> 5; w <= (j >> 5); ++w) {
+                  const uint32_t old = Pm[w * M];
+                  const uint32_t nxt = (w + 1 < NW) ? Pm[(w + 1) * M] : 0u;
+                  const uint32_t sh = (old >> 1) | (nxt << 31);
+                  const uint32_t m1 = range_mask(w, i, j - 1);
+                  uint32_t nw = (old & ~m1) | (sh & m1);
+                  if ((j >> 5) == w) nw = (nw & ~(1u << (j & 31))) | (vb << (j & 31));
+                  Pm[w * M] = nw;
+                }
+              } else {
+                if (ii <= a && a <= jj) sab[m] = a + 1;
+                if (ii <= b && b <= jj) sab[M + m] = b + 1;
+                const uint32_t vb = (Pm[(i >> 5) * M] >> (i & 31)) & 1u;
+                for (int w = i >> 5; w >= (j >> 5); --w) {
+                  const uint32_t old = Pm[w * M];
+                  const uint32_t prv = (w > 0) ? Pm[(w - 1) * M] : 0u;
+                  const uint32_t sh = (old << 1) | (prv >> 31);
+                  const uint32_t m1 = range_mask(w, j + 1, i);
+                  uint32_t nw = (old & ~m1) | (sh & m1);
+                  if ((j >> 5) == w) nw = (nw & ~(1u << (j & 31))) | (vb << (j & 31));
+                  Pm[w * M] = nw;
+                }
+              }
+            } else {                                             /* mcmc.c:1446-1474, 1641-1670 */
+              const int ain = ininterval(a, i, j + 1, inc1, inc2);
+              const int bin = ininterval(b, i, j + 1, inc1, inc2);
+              if (ain && !bin) sab[m] = i + j + 1 - a;
+              else if (!ain && bin) sab[M + m] = i + j + 1 - b;
+              else if (ain && bin) { sab[M + m] = i + j + 1 - a; sab[m] = i + j + 1 - b; }
+              if (kind != 3) {
+                for (int n = i; n < i + j - n; ++n) {
+                  const int p2 = i + j - n;
+                  const uint32_t b1 = (Pm[(n >> 5) * M] >> (n & 31)) & 1u, b2 = (Pm[(p2 >> 5) * M] >> (p2 & 31)) & 1u;
+                  if (b1 != b2) { Pm[(n >> 5) * M] ^= (1u << (n & 31)); Pm[(p2 >> 5) * M] ^= (1u << (p2 & 31)); }
+                }
+              } else {
+                for (int r = 0; r < Kn - 1 - r; ++r) {
+                  const int n = nhpos[r], p2 = nhpos[Kn - 1 - r];
+                  const uint32_t b1 = (Pm[(n >> 5) * M] >> (n & 31)) & 1u, b2 = (Pm[(p2 >> 5) * M] >> (p2 & 31)) & 1u;
+                  if (b1 != b2) { Pm[(n >> 5) * M] ^= (1u << (n & 31)); Pm[(p2 >> 5) * M] ^= (1u << (p2 & 31)); }
+                }
+              }
+            }
+          }
+          /* ---- rpi (double-buffered full permutation) and hard positions */
+          {
+            const int32_t *ro = rcur ? rpiB : rpiA;
+            int32_t *rn = rcur ? rpiA : rpiB;
+            if (kind == 1) {
+              for (int n = lane; n < N; n += 64) {
+                int src = n;
+                if (i < j) { if (n >= i && n < j) src = n + 1; else if (n == j) src = i; }
+                else { if (n > j && n <= i) src = n - 1; else if (n == j) src = i; }
+                rn[n] = ro[src];
               }
 #pragma unroll
               for (int q = 0; q < SR_NHMAX; ++q) {
-                const int n = hp[q];
-                if (q < nh && n >= i && n <= j) {
-                  const int was = (a <= n && n < b), is = (na <= n && n < nb);
-                  if (was != is) {
-                    const int v = colbit(Pm, M, n);
-                    if (was) { if (v) { dt1--; df1++; } else { df0--; dt0++; } }
-                    else { if (v) { dt1++; df1--; } else { df0++; dt0--; } }
-                  }
-                }
+                if (q >= nh) break;
+                const int h = hp[q];
+                if (h == i) hp[q] = j;
+                else if (i < j && h > i && h <= j) hp[q] = h - 1;
+                else if (i > j && h >= j && h < i) hp[q] = h + 1;
               }
-            }
-            tbuf[m] = qval(dt0, df0, dt1, df1, K);
-          }
-          dt0v[k] = dt0; df0v[k] = df0; dt1v[k] = dt1; df1v[k] = df1;
-        }
-        const double delta = ordered_sum(tbuf, M, dslot, tid);
-        /* ---- MH accept (mcmc.c:1261 / 1441 / 1636): uniform_pos only when delta < 0 */
-        bool accept = (delta >= 0.);
-        if (!accept) accept = delta > sr_log_m(rng_uniform_pos<false>(R, tid, TB), &tb);
-        if (!accept) continue;
-        if (tid == 0) acc[kind == 1 ? 3 : kind == 20 ? 4 : kind == 21 ? 5 : 6]++;
-        if (tid < 64) loglik += delta;
-        /* ---- apply: limits, counts, columns */
-        const int32_t *ro = rcur ? rpiB : rpiA;
-        int32_t *rn = rcur ? rpiA : rpiB;
+            } else if (kind != 3) {
+              for (int n = lane; n < N; n += 64) rn[n] = ro[(n >= i && n <= j) ? (i + j - n) : n];
 #pragma unroll
-        for (int k = 0; k < TPT; ++k) {
-          const int m = tid + k * TB;
-          if (m >= M) continue;
-          uint32_t *Pm = P + m;
-          int a = a_[k], b = b_[k];
-          t0_[k] += dt0v[k]; f0_[k] += df0v[k]; t1_[k] += dt1v[k]; f1_[k] += df1v[k];
-          if (kind == 1) {
-            if (i < j) {
-              if (ii < a && a <= jj + 1) a_[k] = a - 1;
-              if (ii < b && b <= jj + 1) b_[k] = b - 1;
-              const uint32_t vb = (uint32_t)colbit(Pm, M, i);
-              for (int w = i >> 5; w <= (j >> 5); ++w) {
-                const uint32_t old = Pm[w * M];
-                const uint32_t nxt = (w + 1 < NW) ? Pm[(w + 1) * M] : 0u;
-                const uint32_t sh = (old >> 1) | (nxt << 31);
-                const int lo = max(i, 32 * w), hi2 = min(j - 1, 32 * w + 31);
-                uint32_t m1 = 0;
-                if (hi2 >= lo) {
-                  const int nb2 = hi2 - lo + 1;
-                  m1 = (nb2 == 32) ? 0xffffffffu : (((1u << nb2) - 1u) << (lo & 31));
-                }
-                uint32_t nw = (old & ~m1) | (sh & m1);
-                if ((j >> 5) == w) nw = (nw & ~(1u << (j & 31))) | (vb << (j & 31));
-                Pm[w * M] = nw;
+              for (int q = 0; q < SR_NHMAX; ++q) {
+                if (q >= nh) break;
+                if (hp[q] >= i && hp[q] <= j) hp[q] = i + j - hp[q];
               }
             } else {
-              if (ii <= a && a <= jj) a_[k] = a + 1;
-              if (ii <= b && b <= jj) b_[k] = b + 1;
-              const uint32_t vb = (uint32_t)colbit(Pm, M, i);
-              for (int w = i >> 5; w >= (j >> 5); --w) {
-                const uint32_t old = Pm[w * M];
-                const uint32_t prv = (w > 0) ? Pm[(w - 1) * M] : 0u;
-                const uint32_t sh = (old << 1) | (prv >> 31);
-                const int lo = max(j + 1, 32 * w), hi2 = min(i, 32 * w + 31);
-                uint32_t m1 = 0;
-                if (hi2 >= lo) {
-                  const int nb2 = hi2 - lo + 1;
-                  m1 = (nb2 == 32) ? 0xffffffffu : (((1u << nb2) - 1u) << (lo & 31));
-                }
-                uint32_t nw = (old & ~m1) | (sh & m1);
-                if ((j >> 5) == w) nw = (nw & ~(1u << (j & 31))) | (vb << (j & 31));
-                Pm[w * M] = nw;
-              }
+              for (int n = lane; n < N; n += 64)
+                if (n < i || n > j || is_hard(hp, nh, n)) rn[n] = ro[n];
+              for (int r = lane; r < Kn; r += 64) rn[nhpos[r]] = ro[nhpos[Kn - 1 - r]];
             }
-          } else {
-            const int ain = ininterval(a, i, j + 1, inc1, inc2);
-            const int bin = ininterval(b, i, j + 1, inc1, inc2);
-            if (ain && !bin) a_[k] = i + j + 1 - a;
-            else if (!ain && bin) b_[k] = i + j + 1 - b;
-            else if (ain && bin) { b_[k] = i + j + 1 - a; a_[k] = i + j + 1 - b; }
-            if (kind != 3) {
-              for (int n = i; n < i + j - n; ++n) {
-                const int p2 = i + j - n;
-                const uint32_t *w1 = &Pm[(n >> 5) * M];
-                const uint32_t *w2 = &Pm[(p2 >> 5) * M];
-                const uint32_t b1 = (*w1 >> (n & 31)) & 1u, b2 = (*w2 >> (p2 & 31)) & 1u;
-                if (b1 != b2) {
-                  Pm[(n >> 5) * M] ^= (1u << (n & 31));
-                  Pm[(p2 >> 5) * M] ^= (1u << (p2 & 31));
-                }
-              }
-            } else {
-              for (int r = 0; r < Kn - 1 - r; ++r) {
-                const int n = nhpos[r], p2 = nhpos[Kn - 1 - r];
-                const uint32_t b1 = (Pm[(n >> 5) * M] >> (n & 31)) & 1u;
-                const uint32_t b2 = (Pm[(p2 >> 5) * M] >> (p2 & 31)) & 1u;
-                if (b1 != b2) {
-                  Pm[(n >> 5) * M] ^= (1u << (n & 31));
-                  Pm[(p2 >> 5) * M] ^= (1u << (p2 & 31));
-                }
-              }
-            }
+            rcur ^= 1;
+            wsync();
           }
-        }
-        /* ---- rpi (double-buffered full permutation) and hard positions */
-        if (kind == 1) {
-          for (int n = tid; n < N; n += TB) {
-            int src = n;
-            if (i < j) { if (n >= i && n < j) src = n + 1; else if (n == j) src = i; }
-            else { if (n > j && n <= i) src = n - 1; else if (n == j) src = i; }
-            rn[n] = ro[src];
-          }
-#pragma unroll
-          for (int q = 0; q < SR_NHMAX; ++q) {
-            if (q < nh) {
-              const int h = hp[q];
-              if (h == i) hp[q] = j;
-              else if (i < j && h > i && h <= j) hp[q] = h - 1;
-              else if (i > j && h >= j && h < i) hp[q] = h + 1;
-            }
-          }
-        } else if (kind != 3) {
-          for (int n = tid; n < N; n += TB) rn[n] = ro[(n >= i && n <= j) ? (i + j - n) : n];
-#pragma unroll
-          for (int q = 0; q < SR_NHMAX; ++q)
-            if (q < nh && hp[q] >= i && hp[q] <= j) hp[q] = i + j - hp[q];
-        } else {
-          for (int n = tid; n < N; n += TB)
-            if (n < i || n > j || is_hard(hp, nh, n)) rn[n] = ro[n];
-          for (int r = tid; r < Kn; r += TB) rn[nhpos[r]] = ro[nhpos[Kn - 1 - r]];
-        }
-        rcur ^= 1;
-      } /* proposals */
+          STAMP(6);
+        } /* proposals */
+      }   /* wave 0 */
+      STAMP(6);
     } /* sweeps */
 
     /* ---------------- saved sample (mcmc_save_chain, mcmc.c:69-92) */
     if (A.save) {
+      if (w0 && lane == 0) { dmisc[MS_LLS] = loglik; misc[MS_RCUR] = (uint64_t)rcur; }
       __syncthreads();
       const int slot = A.rec_base + call;
       const int W = 2 * M + N;
       int16_t *rec = A.rec_abpi + ((size_t)chain * A.rec_cap + slot) * W;
-#pragma unroll
-      for (int k = 0; k < TPT; ++k) {
-        const int m = tid + k * TB;
-        if (m < M) { rec[m] = (int16_t)a_[k]; rec[M + m] = (int16_t)b_[k]; }
-      }
-      const int32_t *rc = rcur ? rpiB : rpiA;
+      for (int m = tid; m < 2 * M; m += TB) rec[m] = (int16_t)sab[m];
+      const int32_t *rc = misc[MS_RCUR] ? rpiB : rpiA;
       for (int n = tid; n < N; n += TB) rec[2 * M + rc[n]] = (int16_t)n;
       if (tid == 0) {
         double *rd = A.rec_cdl + ((size_t)chain * A.rec_cap + slot) * 3;
-        rd[0] = c; rd[1] = d; rd[2] = loglik;
+        rd[0] = c; rd[1] = d; rd[2] = dmisc[MS_LLS];
       }
+      __syncthreads();
     }
   } /* calls */
 
   /* ---------------- store state */
+  STAMP(7);
+  STAMP_STORE(A.dbg);
+#ifdef SR_STAMPS
+  if (tid == 0) { A.dbg[blockIdx.x * 17 * 8 + 0] += misc[MS_NEXACT]; for (int q_ = 0; q_ < 4; ++q_) A.dbg[blockIdx.x * 17 * 8 + 1 + q_] += misc[MS_FBK + q_]; }
+#endif
+  if (w0 && lane == 0) { misc[MS_RCUR] = (uint64_t)rcur; dmisc[MS_LLS] = loglik; }
   __syncthreads();
   uint32_t *oP = A.P + (size_t)chain * NW * M;
   for (int i = tid; i < NW * M; i += TB) oP[i] = P[i];
-  const int32_t *rc = rcur ? rpiB : rpiA;
+  const int32_t *rc = misc[MS_RCUR] ? rpiB : rpiA;
   int32_t *orpi = A.rpi + (size_t)chain * N;
   for (int i = tid; i < N; i += TB) orpi[i] = rc[i];
   uint32_t *omt = A.mt + (size_t)chain * SR_RING * SR_MT_N;
   for (int i = tid; i < SR_RING * SR_MT_N; i += TB) omt[i] = ring[i];
-#pragma unroll
-  for (int k = 0; k < TPT; ++k) {
-    const int m = tid + k * TB;
-    if (m < M) {
-      A.ab[(size_t)chain * 2 * M + m] = a_[k];
-      A.ab[(size_t)chain * 2 * M + M + m] = b_[k];
-      A.cnt[(size_t)chain * 4 * M + m] = t0_[k];
-      A.cnt[(size_t)chain * 4 * M + M + m] = f0_[k];
-      A.cnt[(size_t)chain * 4 * M + 2 * M + m] = t1_[k];
-      A.cnt[(size_t)chain * 4 * M + 3 * M + m] = f1_[k];
-    }
-  }
+  int32_t *oab = A.ab + (size_t)chain * 2 * M;
+  for (int i = tid; i < 2 * M; i += TB) oab[i] = sab[i];
+  int32_t *ocnt = A.cnt + (size_t)chain * 4 * M;
+  for (int i = tid; i < 4 * M; i += TB) ocnt[i] = scnt[i];
   if (tid == 0) {
 #pragma unroll
     for (int k = 0; k < SR_NHMAX; ++k)
       if (k < nh) A.hp[(size_t)chain * SR_NHMAX + k] = hp[k];
     A.cdl[(size_t)chain * 4 + 0] = c;
     A.cdl[(size_t)chain * 4 + 1] = d;
-    A.cdl[(size_t)chain * 4 + 2] = loglik;
+    A.cdl[(size_t)chain * 4 + 2] = dmisc[MS_LLS];
     A.rng[(size_t)chain * 2 + 0] = (uint64_t)R.blk * SR_MT_N + R.off;
     A.rng[(size_t)chain * 2 + 1] = R.gen;
     for (int k = 0; k < 7; ++k) A.acc[(size_t)chain * 8 + k] += acc[k];
     A.acc[(size_t)chain * 8 + 2] += misc[MS_CAB];
+    A.acc[(size_t)chain * 8 + 7] += misc[MS_NEXACT];
   }
 }
 
@@ -899,11 +1155,11 @@ struct srk_dev {
 
 typedef void (*sr_kfn)(KArgs);
 
-static sr_kfn sr_pick_kernel(int TB, int TPT)
+static sr_kfn sr_pick_kernel(int TB)
 {
-#define SR_K(tb, tpt) if (TB == tb && TPT == tpt) return (sr_kfn)sr_sweep_kernel<tb, tpt>;
-  SR_K(64, 1) SR_K(128, 1) SR_K(256, 1) SR_K(512, 1) SR_K(1024, 1) SR_K(1024, 2) SR_K(1024, 4)
-#undef SR_K
+  if (TB == 256) return (sr_kfn)sr_sweep_kernel<256>;
+  if (TB == 512) return (sr_kfn)sr_sweep_kernel<512>;
+  if (TB == 1024) return (sr_kfn)sr_sweep_kernel<1024>;
   return nullptr;
 }
 
@@ -935,12 +1191,10 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
   srk_dev *d = new srk_dev();
   d->device = device; d->N = st->N; d->M = st->M; d->NW = st->NW; d->nh = st->nh; d->nchains = st->nchains;
   int TB = block_threads;
-  if (TB <= 0) { TB = 64; while (TB < st->M && TB < 1024) TB *= 2; }
-  int TPT = (st->M + TB - 1) / TB;
-  if (TPT == 3) TPT = 4;
-  if (!sr_pick_kernel(TB, TPT)) { delete d; return -6; }
-  d->TB = TB; d->TPT = TPT;
-  Lay L = sr_layout(st->N, st->M, st->NW);
+  if (TB <= 0) { TB = 256; while (TB < st->M && TB < 1024) TB *= 2; }
+  if (!sr_pick_kernel(TB)) { delete d; return -6; }
+  d->TB = TB; d->TPT = 1;
+  Lay L = sr_layout(st->N, st->M, st->NW, TB);
   d->lds = L.total;
   if (d->lds > 160 * 1024) { delete d; return -6; }
   d->rec_cap = rec_cap_calls > 0 ? rec_cap_calls : 1;
@@ -960,8 +1214,9 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
   rc |= dev_alloc_copy(d, &A.acc, st->acc, C * 8);
   rc |= dev_alloc_copy(d, &A.rec_abpi, (const int16_t *)nullptr, C * d->rec_cap * (2 * st->M + st->N));
   rc |= dev_alloc_copy(d, &A.rec_cdl, (const double *)nullptr, C * d->rec_cap * 3);
+  rc |= dev_alloc_copy(d, &A.dbg, (const unsigned long long *)nullptr, C * 17 * 8);
   if (rc) { srk_destroy(d); return -5; }
-  sr_kfn k = sr_pick_kernel(TB, TPT);
+  sr_kfn k = sr_pick_kernel(TB);
   if (hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d->lds) != hipSuccess) {
     srk_destroy(d);
     return -5;
@@ -988,7 +1243,7 @@ extern "C" int srk_run(srk_dev *d, int calls, int spc, int save, int rec_base)
   HIPCHK(hipSetDevice(d->device));
   KArgs A = d->args;
   A.calls = calls; A.spc = spc; A.save = save; A.rec_base = rec_base;
-  sr_kfn k = sr_pick_kernel(d->TB, d->TPT);
+  sr_kfn k = sr_pick_kernel(d->TB);
   if (d->have_events) HIPCHK(hipEventRecord(d->ev0, d->stream));
   hipLaunchKernelGGL(k, dim3(d->nchains), dim3(d->TB), d->lds, d->stream, A);
   HIPCHK(hipGetLastError());
@@ -1013,6 +1268,14 @@ extern "C" double srk_last_ms(srk_dev *d)
 }
 
 extern "C" int srk_block_threads(const srk_dev *d) { return d->TB; }
+
+extern "C" int srk_fetch_dbg(srk_dev *d, unsigned long long *out)
+{
+  HIPCHK(hipSetDevice(d->device));
+  HIPCHK(hipStreamSynchronize(d->stream));
+  HIPCHK(hipMemcpy(out, d->args.dbg, (size_t)d->nchains * 17 * 8 * 8, hipMemcpyDeviceToHost));
+  return 0;
+}
 
 extern "C" int srk_fetch_records(srk_dev *d, int first, int count, int16_t *ab_pi, double *cdl)
 {

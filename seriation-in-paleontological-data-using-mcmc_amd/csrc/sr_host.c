@@ -685,7 +685,14 @@ SR_API int sr_run_to_dirs(const sr_dataset *ds, const sr_chain_spec *specs, int3
   return rc;
 }
 
-/* ------------------------------------------------------ test hooks (host math) */
+/* ------------------------------------------------------ test / diagnostic hooks */
+/* per-chain phase cycle counters of an SR_STAMPS build ([n_chains][16]); zeros otherwise */
+SR_API int sr_session_debug_counters(sr_session *s, unsigned long long *out)
+{
+  if (!s || !out) return SR_EINVAL;
+  return srk_fetch_dbg(s->dev, out) ? SR_EDEVICE : SR_OK;
+}
+
 SR_API void sr_host_exp_log(const double *in, long n, double *out_exp, double *out_log)
 {
   for (long k = 0; k < n; k++) {

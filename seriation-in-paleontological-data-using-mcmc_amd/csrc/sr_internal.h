@@ -42,6 +42,7 @@ int srk_run(srk_dev *d, int calls, int spc, int save, int rec_base);
 int srk_sync(srk_dev *d);
 double srk_last_ms(srk_dev *d);
 int srk_block_threads(const srk_dev *d);
+int srk_fetch_dbg(srk_dev *d, unsigned long long *out);
 int srk_fetch_records(srk_dev *d, int first, int count, int16_t *ab_pi, double *cdl);
 int srk_download_state(srk_dev *d, sr_state_host *st);
 void srk_destroy(srk_dev *d);

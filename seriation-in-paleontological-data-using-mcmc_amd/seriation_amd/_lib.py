@@ -8,7 +8,7 @@ import ctypes
 import os
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "build", "libseriation.so")
+LIB_PATH = os.environ.get("SERIATION_LIB") or os.path.join(PKG_DIR, "build", "libseriation.so")
 
 SR_OK = 0
 SR_EINVAL = -1
@@ -114,6 +114,7 @@ def _lib():
         "sr_host_run_sub": (ctypes.c_long, [P(c_double), c_double, ctypes.c_long]),
         "sr_host_init_chain": (c_int, [P(sr_dataset), ctypes.c_uint64, P(c_i32), P(c_i32), P(c_i32),
                                        P(c_double), P(ctypes.c_uint64)]),
+        "sr_session_debug_counters": (c_int, [c_void_p, P(ctypes.c_ulonglong)]),
         "sr_device_selftest_math": (c_int, [c_int, P(c_double), ctypes.c_long, P(c_double), P(c_double)]),
     }
     for name, (res, args) in sig.items():

@@ -75,7 +75,7 @@ def main():
     ap.add_argument("--chains-per-gpu", type=int, default=100)
     ap.add_argument("--calls-per-step", type=int, default=10)
     ap.add_argument("--dataset", default=SYNTH)
-    ap.add_argument("--cpu-calls", type=int, default=40)
+    ap.add_argument("--cpu-calls", type=int, default=300)
     ap.add_argument("--cpu-workers", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--block-threads", type=int, default=0)
@@ -95,8 +95,10 @@ def main():
         workers = args.cpu_workers or max(1, min(16, os.cpu_count() or 1))
         cpu = cpu_baseline(args.dataset, args.cpu_calls, workers)
 
+    import numpy as np
     import torch
     import seriation_amd as sa
+    from seriation_amd import dist as sd
 
     dist = None
     if world > 1:
@@ -108,9 +110,11 @@ def main():
 
     ds = sa.Dataset.load(args.dataset)
     C = args.chains_per_gpu
-    seeds = [rank * C + k + 1 for k in range(C)]
+    # weak scaling: C chains per rank, rank r owns chains [r*C, (r+1)*C) (sd.shard), seed = id + 1
+    chain_ids = list(sd.shard(C * world, world, rank))
+    seeds = [i + 1 for i in chain_ids]
     sess = sa.Session(ds, seeds, device=local_rank, calls_per_launch=args.calls_per_step,
-                      block_threads=args.block_threads, chain_ids=[rank * C + k for k in range(C)])
+                      block_threads=args.block_threads, chain_ids=chain_ids)
     stream = torch.cuda.current_stream()
     sess.set_stream(stream.cuda_stream)
     cps = args.calls_per_step
@@ -130,15 +134,15 @@ def main():
         evs[k][0].record(stream)
         step()
         evs[k][1].record(stream)
-    # the one collective: every rank's per-chain loglik of the last saved sample (one-sigma input)
+    # the one collective: every rank's per-chain summary record (exp_data payload of the
+    # last step's saved samples) all-gathered, then the one-sigma selection on every rank
     _, cdl = sess.fetch_records()
-    ll = torch.tensor(cdl[:, -1, 2], dtype=torch.float64, device="cuda")
+    rows = sd.summaries_from_records(chain_ids, cdl)
     if dist:
-        parts = [torch.empty_like(ll) for _ in range(world)]
-        dist.all_gather(parts, ll)
-        gathered = torch.cat(parts)
+        gathered = sd.gather_summaries(rows, C * world, device="cuda")
     else:
-        gathered = ll
+        gathered = rows
+    selected = sd.select_chains(gathered, 8)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -148,7 +152,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
-    assert gathered.numel() == C * world and bool(torch.isfinite(gathered).all())
+    assert len(gathered) == C * world and np.isfinite(gathered).all() and selected
 
     total_chains = C * world
     sweeps_per_step = cps * 10

@@ -40,6 +40,10 @@ class Dataset:
             text = text.encode()
         ds = L.sr_dataset()
         _check(L.lib().sr_parse_dataset(text, len(text), maxs, ctypes.byref(ds)), "parse")
+        return cls._adopt(ds)
+
+    @classmethod
+    def _adopt(cls, ds):
         try:
             X = np.ctypeslib.as_array(ds.X, shape=(ds.N * ds.M,)).reshape(ds.N, ds.M).copy()
             hard = np.ctypeslib.as_array(ds.hard, shape=(ds.N,)).copy()
@@ -49,8 +53,9 @@ class Dataset:
 
     @classmethod
     def load(cls, path, maxs=L.SR_MAXS):
-        with open(path, "rb") as fh:
-            return cls.parse(fh.read(), maxs)
+        ds = L.sr_dataset()
+        _check(L.lib().sr_load_dataset(os.fsencode(path), maxs, ctypes.byref(ds)), "load %s" % path)
+        return cls._adopt(ds)
 
     @property
     def c(self):

@@ -55,6 +55,7 @@ def run_all_chains(dataset, n_chains=100, seeds=None, devices=None, burnin_calls
     seeds = list(seeds)[:n_chains]
     devices = devices or [0]
     ds = core.Dataset.load(str(dataset))
+    os.makedirs(os.path.join(root, "Chains"), exist_ok=True)
     start = time.perf_counter()
     shards = np.array_split(np.arange(len(seeds)), len(devices))
     results = [None] * len(devices)

@@ -1,0 +1,56 @@
+"""Posterior summaries (script.py:102-189) on oracle-written chain files: file form equals
+the literal restatement, record form equals file form up to the %.14f text rounding."""
+import os
+import subprocess
+
+import numpy as np
+
+import oracle_ref
+from seriation_amd import analysis
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DS = os.path.join(ROOT, "tests", "golden", "datasets", "g10s10.txt")
+ORACLE_CLI = os.path.join(ROOT, "oracle", "build", "mcmc_oracle")
+
+
+def _write_chains(tmp, seeds, tb, ts):
+    oracle_ref.lib()
+    if not os.path.exists(ORACLE_CLI):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    recs = {}
+    text = open(DS, "rb").read()
+    for k, s in enumerate(seeds):
+        d = os.path.join(tmp, "run%d" % k)
+        os.makedirs(os.path.join(d, "Chains", "chain_00"))
+        with open(DS, "rb") as fin:
+            subprocess.check_call([ORACLE_CLI, "0", str(tb), str(ts)], cwd=d, stdin=fin,
+                                  env=dict(os.environ, GSL_RNG_SEED=str(s)), stderr=subprocess.DEVNULL)
+        os.makedirs(os.path.join(tmp, "Chains"), exist_ok=True)
+        os.rename(os.path.join(d, "Chains", "chain_00"), os.path.join(tmp, "Chains", "chain_%02d" % k))
+        recs[k] = oracle_ref.run_chain(text, s, tb, ts)
+    return recs
+
+
+def test_file_and_record_forms_agree(tmp_path):
+    recs = _write_chains(str(tmp_path), [3, 8, 11], 3, 6)
+    chains = [0, 1, 2]
+    N, M = 124, 139
+    c, d = analysis.compute_exp_cd(chains, 3, root=str(tmp_path))
+    c2, d2 = analysis.exp_cd_from_records([recs[k]["rec_dbl"] for k in chains])
+    assert abs(c - c2) < 1e-13 and abs(d - d2) < 1e-13
+    r = analysis.compute_exp_ages(chains, 3, N, root=str(tmp_path))
+    r2 = analysis.corr_mn_from_records([recs[k]["rec_int"][:, 2 * M:] for k in chains])
+    assert abs(r - r2) < 1e-12
+    # literal pair-order restatement (script.py:155-189 with generate_po_matrix's loops)
+    po_ref = np.zeros((N, N))
+    po_chain = np.zeros((N, N))
+    for k in chains:
+        for p in recs[k]["rec_int"][:, 2 * M:]:
+            for i in range(N):
+                for j in range(N):
+                    po_chain[i][j] += -1 if i == j else int(p[i] < p[j])
+        po_chain /= 1000
+        po_ref += po_chain
+    po_ref /= 3
+    np.testing.assert_allclose(analysis.compute_pair_order_matrix(chains, 3, N, root=str(tmp_path)), po_ref,
+                               rtol=0, atol=1e-15)

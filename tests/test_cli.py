@@ -1,0 +1,106 @@
+"""The `mcmc` CLI contract (mcmc.c:102-210).
+
+CPU: the oracle CLI's five output files have the reference's exact layout; the product
+CLI fails loudly (exit 1) when no GPU is present -- there is no CPU fallback.
+GPU: the product CLI's files are byte-identical to the oracle CLI's for the same seed.
+"""
+import os
+import subprocess
+
+import pytest
+
+import oracle_ref
+from seriation_amd import _lib as L
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DS = os.path.join(ROOT, "tests", "golden", "datasets")
+ORACLE_CLI = os.path.join(ROOT, "oracle", "build", "mcmc_oracle")
+PRODUCT_CLI = os.path.join(os.path.dirname(L.LIB_PATH), "mcmc")
+FILES = ["chain_data.csv", "exp_data.csv", "taxa.csv", "sites.csv", "hard_sites.csv"]
+
+
+def run_cli(exe, cwd, dataset, args, seed, chain_dir):
+    os.makedirs(os.path.join(cwd, "Chains", chain_dir), exist_ok=True)
+    env = dict(os.environ, GSL_RNG_SEED=str(seed))
+    with open(os.path.join(DS, dataset), "rb") as fin:
+        p = subprocess.run([exe] + list(args), cwd=cwd, stdin=fin, env=env, capture_output=True, timeout=900)
+    return p
+
+
+def read_dir(cwd, chain_dir):
+    out = {}
+    for f in FILES:
+        with open(os.path.join(cwd, "Chains", chain_dir, f), "rb") as fh:
+            out[f] = fh.read()
+    return out
+
+
+def test_oracle_cli_format(tmp_path):
+    oracle_ref.lib()
+    if not os.path.exists(ORACLE_CLI):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    p = run_cli(ORACLE_CLI, str(tmp_path), "g10s10.txt", ["0", "2", "3"], 7, "chain_00")
+    assert p.returncode == 0, p.stderr
+    assert b"GSL_RNG_SEED=7" in p.stderr
+    files = read_dir(str(tmp_path), "chain_00")
+    N, M = 124, 139
+    lines = files["chain_data.csv"].decode().splitlines()
+    assert len(lines) == 3
+    for ln in lines:
+        f = ln.split(",")
+        assert len(f) == 6
+        assert len(f[0].split()) == M and len(f[1].split()) == M and len(f[2].split()) == N
+        assert len(f[3].split()) == M and f[3].endswith(" ")
+        assert sorted(map(int, f[2].split())) == list(range(N))
+    ex = files["exp_data.csv"].decode()
+    assert ex.startswith("exp_loglik,exp_c,exp_d\n") and not ex.endswith("\n")
+    o = oracle_ref.run_chain(open(os.path.join(DS, "g10s10.txt"), "rb").read(), 7, 2, 3)
+    assert ex.split("\n")[1] == "%.14f,%.14f,%.14f" % tuple(o["exp"])
+    assert files["taxa.csv"].decode().splitlines()[0] == "a,b,c,d"
+    assert len(files["taxa.csv"].decode().splitlines()) == M + 1
+    assert files["sites.csv"].decode().splitlines()[1:] == [str(v) for v in o["rec_int"][-1][2 * M:]]
+    hs = files["hard_sites.csv"].decode().splitlines()
+    assert hs[0] == "i,pi_i" and len(hs) == 1 + 11
+
+
+def test_product_cli_fails_loudly_without_gpu(tmp_path):
+    if os.path.exists("/dev/kfd"):
+        pytest.skip("GPU node: covered by the gpu tests")
+    p = run_cli(PRODUCT_CLI, str(tmp_path), "g2s2.txt", ["3"], 1, "chain_03")
+    assert p.returncode == 1
+    assert p.stderr.strip()
+
+
+def test_cli_usage_error(tmp_path):
+    p = subprocess.run([PRODUCT_CLI, "1", "2"], cwd=str(tmp_path), capture_output=True, stdin=subprocess.DEVNULL)
+    assert p.returncode == 1 and b"usage" in p.stderr
+
+
+def _compare(tmp_path, dataset, args, seed, chain_dir):
+    a, b = str(tmp_path / "oracle"), str(tmp_path / "product")
+    pa = run_cli(ORACLE_CLI, a, dataset, args, seed, chain_dir)
+    pb = run_cli(PRODUCT_CLI, b, dataset, args, seed, chain_dir)
+    assert pa.returncode == 0, pa.stderr
+    assert pb.returncode == 0, pb.stderr
+    fa, fb = read_dir(a, chain_dir), read_dir(b, chain_dir)
+    for f in FILES:
+        assert fa[f] == fb[f], f
+    assert os.path.exists(os.path.join(b, "mcmc_c.log"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("index,chain_dir", [("5", "chain_05"), ("42", "chain_42")])
+def test_product_cli_byte_identical_g10s10(tmp_path, index, chain_dir):
+    """chain-index form: defaults 1000 + 1000 calls, output dir named as mcmc.c:153-178."""
+    _compare(tmp_path, "g10s10.txt", [index], int(index) + 100, chain_dir)
+
+
+@pytest.mark.gpu
+def test_product_cli_four_argument_form(tmp_path):
+    _compare(tmp_path, "g10s10.txt", ["0", "20", "30"], 3, "chain_00")
+
+
+@pytest.mark.gpu
+def test_product_cli_g2s2_reference_defaults(tmp_path):
+    """BASELINE config 1: g2s2, 1 chain, CLI defaults (1000 burn-in + 1000 saved calls)."""
+    _compare(tmp_path, "g2s2.txt", ["7"], 1, "chain_07")

@@ -1,0 +1,135 @@
+"""Host-side pieces of the product against the oracle (CPU only, no device calls).
+
+* deterministic exp/log (csrc/sr_math.h, same algorithm as the device): bitwise equal to
+  the oracle's om_libm.h and within 1 ulp of glibc (which the reference links);
+* sr_run_add / sr_run_sub (closed-form runs of equal sequential roundings used by the
+  device for the clamped tails of mcmc_logtop / mcmc_randompick, mcmc.c:731-737,
+  909-913) against the naive loops they replace;
+* chain initialisation (mcmc_readmodel + mcmc_randomize + mcmc_init, mcmc.c:339-593,
+  including its ran_choose / ran_shuffle RNG consumption) against the oracle.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import oracle_ref
+import seriation_amd as sa
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+DS = os.path.join(HERE, "golden", "datasets")
+PD = ctypes.POINTER(ctypes.c_double)
+PI = ctypes.POINTER(ctypes.c_int32)
+
+
+def host_exp_log(x):
+    x = np.ascontiguousarray(x, np.float64)
+    e, l = np.zeros_like(x), np.zeros_like(x)
+    sa.lib().sr_host_exp_log(x.ctypes.data_as(PD), len(x), e.ctypes.data_as(PD), l.ctypes.data_as(PD))
+    return e, l
+
+
+def _inputs():
+    rng = np.random.default_rng(5)
+    return np.concatenate([
+        rng.uniform(-745.5, 710.0, 100000), rng.uniform(-33.0, 0.0, 100000),
+        rng.uniform(-7.0, 0.0, 50000), -0.5 * rng.normal(0, 3, 50000) ** 2,
+        rng.uniform(0.0, 1.0, 100000), rng.uniform(0.9, 1.0, 100000),
+        np.ldexp(rng.uniform(0.5, 1.0, 50000), rng.integers(-1070, 1000, 50000)),
+        [0.0, -0.0, 1.0, np.inf, -np.inf, np.nan, 5e-324, 709.78, -745.13, 1e-300],
+    ])
+
+
+def _bits_equal(a, b):
+    return (a.view(np.uint64) == b.view(np.uint64)) | (np.isnan(a) & np.isnan(b))
+
+
+def test_exp_log_bitwise_equal_to_oracle():
+    x = _inputs()
+    e, l = host_exp_log(x)
+    e0, l0 = oracle_ref.exp_log(x)
+    assert _bits_equal(e, e0).all()
+    assert _bits_equal(l, l0).all()
+
+
+def _ulps(a, b):
+    return np.abs(a.view(np.int64) - b.view(np.int64))
+
+
+def test_exp_log_within_one_ulp_of_glibc():
+    x = _inputs()
+    with np.errstate(all="ignore"):
+        e, l = host_exp_log(x)
+        ge, gl = np.exp(x), np.log(x)
+    fe = np.isfinite(ge) & (ge > 2.3e-308)
+    fl = np.isfinite(gl) & (x > 0)
+    assert _ulps(e[fe], ge[fe]).max() <= 1
+    assert _ulps(l[fl], gl[fl]).max() <= 1
+    # against glibc itself (numpy's exp may use its own SIMD code): agreement rate
+    libm = ctypes.CDLL("libm.so.6")
+    libm.exp.restype = libm.log.restype = ctypes.c_double
+    libm.exp.argtypes = libm.log.argtypes = [ctypes.c_double]
+    sel = np.random.default_rng(1).choice(len(x), 20000, replace=False)
+    xs = x[sel]
+    ge2 = np.array([libm.exp(v) for v in xs])
+    gl2 = np.array([libm.log(v) if v > 0 else np.nan for v in xs])
+    fe2, fl2 = fe[sel], fl[sel]
+    assert _ulps(e[sel][fe2], ge2[fe2]).max() <= 1 and _ulps(l[sel][fl2], gl2[fl2]).max() <= 1
+    assert np.mean(e[sel][fe2] == ge2[fe2]) > 0.99 and np.mean(l[sel][fl2] == gl2[fl2]) > 0.99
+
+
+def test_run_add_matches_loop():
+    rng = np.random.default_rng(9)
+    lib = sa.lib()
+    for _ in range(300):
+        x = float(rng.uniform(0, 2) * 2.0 ** rng.integers(-40, 3))
+        e = float(np.exp(-32.236191301916641) * rng.choice([1.0, rng.uniform(0.5, 3)]))
+        L = int(rng.integers(1, 3000))
+        ref = x
+        for _k in range(L):
+            ref = ref + e
+        assert lib.sr_host_run_add(x, e, L) == ref
+
+
+def test_run_sub_matches_loop():
+    rng = np.random.default_rng(10)
+    lib = sa.lib()
+    for _ in range(300):
+        r0 = float(rng.uniform(0, 1) * 2.0 ** rng.integers(-30, 1))
+        p = float(rng.uniform(0.2, 4) * 2.0 ** rng.integers(-50, -20))
+        L = int(rng.integers(1, 5000))
+        ref, steps = r0, 0
+        while steps < L:
+            ref = ref - p
+            steps += 1
+            if ref <= 0.0:
+                break
+        r = ctypes.c_double(r0)
+        got = lib.sr_host_run_sub(ctypes.byref(r), p, L)
+        assert (got, r.value) == (steps, ref)
+
+
+@pytest.mark.parametrize("name", ["g2s2.txt", "g10s10.txt", "g5s5.txt", "g10s2.txt", "synth_256x512.txt"])
+def test_init_chain_matches_oracle(name):
+    with open(os.path.join(DS, name), "rb") as fh:
+        text = fh.read()
+    ds = sa.Dataset.parse(text)
+    for seed in (0, 1, 2, 77, 4357):
+        a = np.zeros(ds.M, np.int32)
+        b = np.zeros(ds.M, np.int32)
+        pi = np.zeros(ds.N, np.int32)
+        cdl = np.zeros(3)
+        pos = ctypes.c_uint64()
+        rc = sa.lib().sr_host_init_chain(ctypes.byref(ds.c), seed, a.ctypes.data_as(PI), b.ctypes.data_as(PI),
+                                         pi.ctypes.data_as(PI), cdl.ctypes.data_as(PD), ctypes.byref(pos))
+        assert rc == 0
+        o = oracle_ref.run_chain(text, seed, 0, 0)
+        M = ds.M
+        np.testing.assert_array_equal(a, o["init"][:M])
+        np.testing.assert_array_equal(b, o["init"][M:2 * M])
+        np.testing.assert_array_equal(pi, o["init"][2 * M:])
+        assert cdl.view(np.uint64).tolist() == o["init_cdl"].view(np.uint64).tolist()
+        # hard sites keep their relative order under mcmc_randomize (mcmc.c:496-593)
+        hp = pi[ds.hard.astype(bool)]
+        assert (np.diff(hp) > 0).all()

@@ -1,0 +1,57 @@
+"""script.py-compatible launcher pieces that need no GPU (script.py:15-99)."""
+import os
+
+import numpy as np
+
+from seriation_amd import launcher
+
+
+def reference_choose(vals_by_dir, k):
+    """script.py:70-99 restated literally (list walk, np.std ddof=0, strict window)."""
+    neg = list(vals_by_dir.values())
+    lo = min(neg)
+    sd = np.std(neg)
+    y = sorted(x for x in neg if lo - sd < x < lo + sd)
+    out = []
+    for z in y[:k]:
+        for d, x in vals_by_dir.items():
+            if x == z:
+                out.append(int(d.split("_")[1]))
+    return sorted(out)
+
+
+def test_choose_matches_reference_rule():
+    rng = np.random.default_rng(4)
+    for trial in range(50):
+        n = int(rng.integers(2, 100))
+        vals = {"chain_%02d" % i: float(np.round(rng.normal(1500, 30), int(rng.integers(0, 3))))
+                for i in rng.permutation(n)}
+        for k in (1, 2, 8):
+            assert launcher.choose_from_values(vals, k) == reference_choose(vals, k)
+
+
+def test_choose_quirks():
+    # equal values map back to every chain holding them (may return more than k)
+    vals = {"chain_00": 10.0, "chain_01": 10.0, "chain_02": 30.0, "chain_03": 11.0}
+    assert launcher.choose_from_values(vals, 1) == [0, 1]
+    assert launcher.choose_from_values(vals, 2) == [0, 0, 1, 1]
+    # strict window: a value exactly one sigma away is excluded
+    vals = {"chain_00": 0.0, "chain_01": 2.0}   # sigma = 1 -> window (-1, 1)
+    assert launcher.choose_from_values(vals, 2) == [0]
+
+
+def test_choose_chains_reads_exp_data(tmp_path):
+    for i, v in enumerate([1500.5, 1490.25, 1600.0]):
+        d = tmp_path / "Chains" / ("chain_%02d" % i)
+        d.mkdir(parents=True)
+        (d / "exp_data.csv").write_text("exp_loglik,exp_c,exp_d\n%.14f,0.01,0.5" % v)
+    assert launcher.choose_chains(2, root=str(tmp_path)) == [0, 1]
+
+
+def test_seed_generation_like_script_py():
+    s = launcher.generate_random_seed()
+    assert 0 <= int(s.strip()) <= 255
+    old = []
+    seeds = [launcher._unique_seed(old) for _ in range(20)]
+    assert len(set(seeds)) == 20 and len(old) == 20
+    assert all(0 <= x <= 255 for x in seeds)

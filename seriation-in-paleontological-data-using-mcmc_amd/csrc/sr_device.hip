@@ -59,28 +59,31 @@ struct KArgs {
 
 /* ---------------------------------------------------------------- LDS carve */
 struct Lay {
-  size_t tab, cbuf, lbuf, mt, P, rpi0, rpi1, nhpos, hb, ck, ccnt, sab, scnt, sd, misc, total;
+  size_t tab, cbuf, lbuf, mt, P, rpi0, rpi1, nhpos, hb, ck, ccnt, sab, scnt, sd, part, tot, xs, misc, total;
 };
 __host__ __device__ static inline size_t sr_al16(size_t x) { return (x + 15) & ~(size_t)15; }
 __host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB)
 {
   Lay L;
   size_t o = 0;
-  const int KT = (M + 63) / 64;
+  const int KT = (M + 63) / 64, NWV = TB / 64;
   L.tab = o;   o = sr_al16(o + 640 * sizeof(double));
-  L.cbuf = o;  o = sr_al16(o + (size_t)KT * 64 * sizeof(double));
+  L.cbuf = o;  o = sr_al16(o + (size_t)2 * KT * 64 * sizeof(double));   /* [2][KT*64] by proposal parity */
   L.lbuf = o;  o = sr_al16(o + (size_t)M * sizeof(double));
   L.mt = o;    o = sr_al16(o + (size_t)SR_RING * SR_MT_N * 4);
   L.P = o;     o = sr_al16(o + (size_t)NW * M * 4);
   L.rpi0 = o;  o = sr_al16(o + (size_t)N * 4);
   L.rpi1 = o;  o = sr_al16(o + (size_t)N * 4);
-  L.nhpos = o; o = sr_al16(o + (size_t)N * 4);
-  L.hb = o;    o = sr_al16(o + (size_t)NW * 4);
+  L.nhpos = o; o = sr_al16(o + (size_t)NWV * N * 4);                     /* per wave */
+  L.hb = o;    o = sr_al16(o + (size_t)NWV * NW * 4);                    /* per wave */
   L.ck = o;    o = sr_al16(o + (size_t)((N >> 5) + 1) * TB * sizeof(double));
-  L.ccnt = o;  o = sr_al16(o + (size_t)KT * 4);
+  L.ccnt = o;  o = sr_al16(o + (size_t)2 * KT * 4);
   L.sab = o;   o = sr_al16(o + (size_t)2 * M * 4);
   L.scnt = o;  o = sr_al16(o + (size_t)4 * M * 4);
   L.sd = o;    o = sr_al16(o + (size_t)4 * KT * 64 * 4);
+  L.part = o;  o = sr_al16(o + (size_t)2 * NWV * 4 * sizeof(double));  /* [2][wave] tsum, tabs, Kt */
+  L.tot = o;   o = sr_al16(o + (size_t)2 * NWV * 4 * 4);               /* [2][wave] t0, f0, t1, f1 */
+  L.xs = o;    o = sr_al16(o + (size_t)NWV * sizeof(double));          /* per-wave broadcast slot */
   L.misc = o;  o = sr_al16(o + 64 * 8);
   L.total = o;
   return L;
@@ -233,11 +236,12 @@ __device__ __forceinline__ uint32_t rng_uint_fast(DRng &r, const UDiv &u, int t,
   return k;
 }
 
-/* ------------------------------------------------ GSL beta/gamma/ziggurat (wave 0) */
-__device__ __forceinline__ double d_gauss_zig(DRng &r, int lane, const sr_mtab &tb)
+/* ------------------------------------------------ GSL beta/gamma/ziggurat */
+template <bool WAVE>
+__device__ __forceinline__ double d_gauss_zig(DRng &r, int lane, int nthr, const sr_mtab &tb)
 {
   for (;;) {
-    uint32_t k = rng_get<true>(r, lane, 64);
+    uint32_t k = rng_get<WAVE>(r, lane, nthr);
     uint32_t i = k & 0xFF;
     uint32_t j = (k >> 8) & 0xFFFFFF;
     int sign = (i & 0x80) ? +1 : -1;
@@ -247,11 +251,11 @@ __device__ __forceinline__ double d_gauss_zig(DRng &r, int lane, const sr_mtab &
     double y;
     if (i < 127) {
       double y0 = c_zig_y[i], y1 = c_zig_y[i + 1];
-      double U1 = rng_uniform<true>(r, lane, 64);
+      double U1 = rng_uniform<WAVE>(r, lane, nthr);
       y = y1 + (y0 - y1) * U1;
     } else {
-      double U1 = 1.0 - rng_uniform<true>(r, lane, 64);
-      double U2 = rng_uniform<true>(r, lane, 64);
+      double U1 = 1.0 - rng_uniform<WAVE>(r, lane, nthr);
+      double U2 = rng_uniform<WAVE>(r, lane, nthr);
       x = SR_ZIGR - sr_log_m(U1, &tb) / SR_ZIGR;
       y = sr_exp_m(-SR_ZIGR * (x - 0.5 * SR_ZIGR), &tb) * U2;
     }
@@ -259,11 +263,12 @@ __device__ __forceinline__ double d_gauss_zig(DRng &r, int lane, const sr_mtab &
   }
 }
 
-__device__ __forceinline__ double d_gamma(DRng &r, double a, int lane, const sr_mtab &tb)
+template <bool WAVE>
+__device__ __forceinline__ double d_gamma(DRng &r, double a, int lane, int nthr, const sr_mtab &tb)
 {
   double boost = 1.0;
   if (a < 1) { /* unreachable from the sampler (a = 1 + count); kept for GSL parity */
-    double u = rng_uniform_pos<true>(r, lane, 64);
+    double u = rng_uniform_pos<WAVE>(r, lane, nthr);
     boost = sr_exp_m(sr_log_m(u, &tb) * (1.0 / a), &tb);
     a = 1.0 + a;
   }
@@ -272,11 +277,11 @@ __device__ __forceinline__ double d_gamma(DRng &r, double a, int lane, const sr_
   double c = (1.0 / 3.0) / __builtin_sqrt(d);
   for (;;) {
     do {
-      x = d_gauss_zig(r, lane, tb);
+      x = d_gauss_zig<WAVE>(r, lane, nthr, tb);
       v = 1.0 + c * x;
     } while (v <= 0);
     v = v * v * v;
-    u = rng_uniform_pos<true>(r, lane, 64);
+    u = rng_uniform_pos<WAVE>(r, lane, nthr);
     if (u < 1 - 0.0331 * x * x * x * x) break;
     if (sr_log_m(u, &tb) < 0.5 * x * x + d * (1 - v + sr_log_m(v, &tb))) break;
   }
@@ -285,11 +290,12 @@ __device__ __forceinline__ double d_gamma(DRng &r, double a, int lane, const sr_
 }
 
 /* mcmc_samplebeta: y = beta(1+a, 1+b); keep the old value unless log y in [low, high] */
+template <bool WAVE>
 __device__ __forceinline__ double d_samplebeta(DRng &r, double x, double a, double b, double low, double high, int lane,
-                               const sr_mtab &tb)
+                                               int nthr, const sr_mtab &tb)
 {
-  double x1 = d_gamma(r, 1. + a, lane, tb);
-  double x2 = d_gamma(r, 1. + b, lane, tb);
+  double x1 = d_gamma<WAVE>(r, 1. + a, lane, nthr, tb);
+  double x2 = d_gamma<WAVE>(r, 1. + b, lane, nthr, tb);
   double y = x1 / (x1 + x2);
   if (y > 0.) {
     y = sr_log_m(y, &tb);
@@ -445,9 +451,6 @@ __device__ __forceinline__ int walk_prefix(const uint32_t *Pm, int M, int N, int
   return s;
 }
 
-#define SR_CERT_REL 0x1p-20  /* relative accuracy of the approximate CDF (2 x the exp error bound) */
-#define SR_CERT_ABS 0x1p-36  /* absolute slack: reference rounding + clamped LOGEPSILON terms */
-
 /* 2^q (q <= ~0) to ~1.6e-7 relative: exact f64 split q = n + f, f in [0,1), v_exp_f32(f) */
 __device__ __forceinline__ double exp2_split(double q)
 {
@@ -457,79 +460,97 @@ __device__ __forceinline__ double exp2_split(double q)
   return __builtin_amdgcn_ldexp((double)y, (int)n);
 }
 
+#define SR_WIN_T 40.0        /* words whose q stays 40 bits below q(o) are skipped (mass <= 2^-40 each entry) */
+
 /* mcmc_auxa + mcmc_logtop + mcmc_randompick for one limit of one taxon (exact version:
  * draw_exact), certified fast path.  The picked index depends only on where u falls in the
- * cumulative distribution F_k = sum_{i<=k} y_i / x.  We evaluate F_k approximately -- q by
- * incremental f64 updates (q(w+1) = q(w) - val(bit_w), val(0) = d - cc, val(1) = dd - c, in
- * log2 units), y = 2^(q - z) via exp2_split -- so that |F^_k - F_k| <= 2^-21 min(F, 1-F) +
- * 2^-40, and accept index k only if u - F^_{k-1} and F^_k - u both exceed that bound (with 2x
- * margin, SR_CERT_*): then the reference's exact sequential computation provably returns the
- * same k.  Otherwise (probability ~1e-5 per draw) the exact path runs.
- * ck: this lane's checkpoint slots (stride ckstride). */
+ * cumulative distribution F_k = sum_{i<=k} y_i / x, y_i = exp(max(LOGEPS, q_i - z)).
+ *
+ * Walk coordinates w = 0..L; q(w) relative to the current limit o (q(o) = 0) in log2 units:
+ * q(w+1) = q(w) - v(bit_w), v(0) = vA = (d - cc) log2e < 0 (zeros raise q), v(1) = vB =
+ * (dd - c) log2e > 0 (ones lower it).  Approximation F^:
+ *   - pass 0 (per 32-entry word, exact integer counts): an upper bound of q inside the word;
+ *     words whose bound is <= -40 are outside the window [klo, khi] and contribute 0;
+ *   - pass 1 over the window: y_{w+1} = y_w * r(bit_w), r = 2^-v computed to f64 accuracy
+ *     (rA = e^(cc-d), rB = e^(c-dd)), S accumulated in order, checkpoint ck[k] after word k.
+ *     The common factor of the first y (exp2_split) cancels in F; the chain contributes
+ *     <= 3(N+1) 2^-52 relative error;
+ *   - the reference's clamped terms (<= (N+1) e^LOGEPS), skipped words (<= (N+1) 2^-40) and
+ *     its own sequential rounding are absorbed by the absolute slack.
+ * Index k is accepted only if u - F^_{k-1} and F^_k - u both exceed the error bound; then the
+ * reference's exact sequential computation provably returns the same k.  Otherwise (or on
+ * overflow) the exact path runs.  ck: this lane's checkpoint slots (stride ckstride). */
 __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int NW, bool rev, int o, int L, double u,
-                                         const CD &K, const sr_mtab &tb, double vA, double vB, double *ck,
-                                         int ckstride, uint64_t *fbk, int &dt0, int &df0, int &dt1, int &df1)
+                                         const CD &K, const sr_mtab &tb, double vA, double vB, double rA, double rB,
+                                         double *ck, int ckstride, uint64_t *fbk, int &dt0, int &df0, int &dt1, int &df1)
 {
   const int POo = walk_prefix(Pm, M, N, NW, rev, o);
   const int nk = (L >> 5) + 1;
-  const double q0 = (double)(o - POo) * vA + (double)POo * vB;   /* q(0), log2 units */
-  /* pass 1: max */
-  double z = q0;
+  /* pass 0: window of words that can hold mass above 2^-40 relative to entry o */
+  int klo = nk, khi = -1;
+  double qlo = 0.0;
   {
-    double q = q0;
+    int O = 0;   /* ones among walk entries [0, 32k) */
     for (int k = 0; k < nk; ++k) {
       const uint32_t ww = walk_word(Pm, M, N, NW, rev, k);
-      const int bmax = min(32, L + 1 - 32 * k);
-#pragma unroll
-      for (int b = 0; b < 32; ++b) {
-        z = fmax(z, (b < bmax) ? q : -__builtin_inf());
-        q = q - (((ww >> b) & 1u) ? vB : vA);
+      const int nb = min(32, L + 1 - 32 * k);
+      const uint32_t vm = (nb >= 32) ? 0xffffffffu : ((1u << nb) - 1u);
+      const int w0 = 32 * k;
+      /* q at entry w0 from exact counts */
+      const double qs = (w0 <= o) ? ((double)((o - w0) - (POo - O)) * vA + (double)(POo - O) * vB)
+                                  : -((double)((w0 - o) - (O - POo)) * vA + (double)(O - POo) * vB);
+      const int ones = __popc(ww & vm);
+      const double ub = qs - (double)(nb - ones) * vA;   /* every zero raises q by -vA */
+      if (ub > -SR_WIN_T) {
+        if (k < klo) { klo = k; qlo = qs; }
+        khi = k;
       }
+      O += __popc(ww);
     }
   }
-  /* pass 2: S_k = sum 2^(q - z), checkpoint after every 32 entries */
+  /* pass 1: S over the window, checkpoints */
+  const double y0 = exp2_split(qlo);
   double S = 0.0;
   {
-    double q = q0 - z;
-    double S1 = 0.0;
-    for (int k = 0; k < nk; ++k) {
+    double y = y0;
+    for (int k = klo; k <= khi; ++k) {
       const uint32_t ww = walk_word(Pm, M, N, NW, rev, k);
-      const int bmax = min(32, L + 1 - 32 * k);
+      const int nb = min(32, L + 1 - 32 * k);
 #pragma unroll
-      for (int b = 0; b < 32; b += 2) {
-        const double y0 = exp2_split(q);
-        q = q - (((ww >> b) & 1u) ? vB : vA);
-        const double y1 = exp2_split(q);
-        q = q - (((ww >> (b + 1)) & 1u) ? vB : vA);
-        S += (b < bmax) ? y0 : 0.0;
-        S1 += (b + 1 < bmax) ? y1 : 0.0;
+      for (int b = 0; b < 32; ++b) {
+        S += (b < nb) ? y : 0.0;
+        y = y * (((ww >> b) & 1u) ? rB : rA);
       }
-      ck[k * ckstride] = S + S1;
+      ck[k * ckstride] = S;
     }
-    S = S + S1;
   }
-  /* pass 3: locate the segment, recompute it, certify */
+  /* pass 2: locate the word, replay the chain to it, certify inside it */
   int res = -1;
-  if (S > 0.0) {
+  if (S > 0.0 && S < 0x1p1000) {
     const double inv = 1.0 / S;
-    int j = 0;
-    while (j < nk - 1 && ck[j * ckstride] * inv < u) ++j;
-    double Sp = (j == 0) ? 0.0 : ck[(j - 1) * ckstride];
+    const double REL = (double)(N + 1) * 0x1p-50;
+    const double ABS = (double)(N + 1) * 0x1p-39;
+    int j = klo;
+    while (j < khi && ck[j * ckstride] * inv < u) ++j;
+    double y = y0;
+    for (int k = klo; k < j; ++k) {
+      const uint32_t ww = walk_word(Pm, M, N, NW, rev, k);
+#pragma unroll
+      for (int b = 0; b < 32; ++b) y = y * (((ww >> b) & 1u) ? rB : rA);
+    }
+    double Sp = (j == klo) ? 0.0 : ck[(j - 1) * ckstride];
     double tprev = u - Sp * inv;
-    double eprev = SR_CERT_REL * fmin(Sp, S - Sp) * inv + SR_CERT_ABS;
+    double eprev = 2.0 * REL * fmin(Sp, S - Sp) * inv + ABS;
     const int w0 = 32 * j;
-    const int PO0 = walk_prefix(Pm, M, N, NW, rev, w0);
-    double q = (w0 <= o) ? ((double)((o - w0) - (POo - PO0)) * vA + (double)(POo - PO0) * vB)
-                         : -((double)((w0 - o) - (PO0 - POo)) * vA + (double)(PO0 - POo) * vB);
-    q = q - z;
     const uint32_t ww = walk_word(Pm, M, N, NW, rev, j);
-    const int bmax = min(32, L + 1 - w0);
-    for (int b = 0; b < bmax; ++b) {
+    const int nb = min(32, L + 1 - w0);
+    const int wend = (j == khi) ? L : w0 + nb - 1;   /* last window entry: the pick must land by here */
+    for (int b = 0; b < nb; ++b) {
       const int w = w0 + b;
-      Sp += exp2_split(q);
+      Sp += y;
       const double t = u - Sp * inv;
-      const double e = SR_CERT_REL * fmin(Sp, S - Sp) * inv + SR_CERT_ABS;
-      if (t < 0.0 || w == L) {
+      const double e = 2.0 * REL * fmin(Sp, S - Sp) * inv + ABS;
+      if (t < 0.0 || w == wend) {
         const bool prev_ok = (w == 0) || (tprev > eprev);
         const bool here_ok = (w == L) || (t < -e);
         if (prev_ok && here_ok) res = w;
@@ -540,7 +561,7 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
       }
       tprev = t;
       eprev = e;
-      q = q - (((ww >> b) & 1u) ? vB : vA);
+      y = y * (((ww >> b) & 1u) ? rB : rA);
     }
   }
   if (res < 0) {
@@ -619,12 +640,12 @@ __device__ __forceinline__ void wsync()
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-/* Exact delta on wave 0: the reference's sequential `delta += term` over ascending m
- * (mcmc.c:1214, 1435, 1630).  Zero terms are skipped (adding +-0 is exact; s is never -0.0).
- * Nonzero terms were compacted per 64-taxon chunk (ascending m) into cbuf with counts ccnt. */
-__device__ __forceinline__ double exact_sum_w0(const double *cbuf, const int *ccnt, int nch, double *slot, int lane)
+/* Exact delta: the reference's sequential `delta += term` over ascending m (mcmc.c:1214,
+ * 1435, 1630), computed by lane 0 of the calling wave and broadcast through its slot.
+ * Zero terms are skipped (adding +-0 is exact; s is never -0.0).  Nonzero terms were
+ * compacted per 64-taxon chunk (ascending m) into cbuf with counts ccnt. */
+__device__ __forceinline__ double exact_sum_wave(const double *cbuf, const int *ccnt, int nch, double *slot, int lane)
 {
-  wsync();
   if (lane == 0) {
     double s = 0.0;
     for (int ch = 0; ch < nch; ++ch) {
@@ -640,22 +661,31 @@ __device__ __forceinline__ double exact_sum_w0(const double *cbuf, const int *cc
     *slot = s;
   }
   wsync();
-  return *slot;
+  const double r = *slot;
+  wsync();
+  return r;
 }
 
+/* words of slack kept resident after the Gibbs draws: the proposals and the next c, d
+ * draws consume ~100 words; a refill inside them is still correct (block-uniform), only slower */
+#define SR_RNG_SLACK 1024
+
 /* ---------------------------------------------------------------- kernel */
-/* One workgroup per chain.  Phases of one sweep (mcmc.c:225-244):
- *   A  wave 0:   totals, c and d (GSL beta via gamma/ziggurat)          -> barrier
- *   B  all:      Gibbs (a_m, b_m) for all taxa (thread per taxon)         -> barrier
- *   C  wave 0:   logl (last sweep of a call), 16 MH permutation proposals
- * Per-taxon state (a, b, t0, f0, t1, f1) and the position-ordered columns P live in LDS;
- * in phase C lane l owns taxa l, l+64, ..., so phase C needs no block barrier at all. */
+/* One workgroup per chain, thread t owns taxa t, t+TB, ... for the whole launch (their
+ * a, b, counts and position-ordered columns P live in LDS).  Every thread walks the same
+ * MT19937 stream (ring in LDS) and computes every uniform decision itself -- the c, d
+ * draws, the proposal draws, vetoes and MH decisions are identical in all threads, so
+ * nothing is broadcast.  Phases of one sweep (mcmc.c:225-244):
+ *   A  per-wave count totals -> barrier -> c, d (GSL beta via gamma/ziggurat)
+ *   B  Gibbs (a_m, b_m) of own taxa (mcmc_sampleab); [barrier + logl on the last sweep]
+ *   C  16 MH permutation proposals: draws, own taxa's count deltas and terms, per-wave
+ *      partial sums -> one barrier -> certified decision -> apply to own taxa. */
 template <int TB>
 __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const bool w0 = tid < 64;
+  constexpr int NWV = TB / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int chain = blockIdx.x;
   const int N = A.N, M = A.M, NW = A.NW, nh = A.nh;
   const int KT = (M + 63) >> 6;
@@ -667,15 +697,17 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   uint32_t *P = (uint32_t *)(smem + L.P);
   int32_t *rpiA = (int32_t *)(smem + L.rpi0);
   int32_t *rpiB = (int32_t *)(smem + L.rpi1);
-  int32_t *nhpos = (int32_t *)(smem + L.nhpos);
-  uint32_t *Hb = (uint32_t *)(smem + L.hb);
+  int32_t *nhpos = (int32_t *)(smem + L.nhpos) + wave * N;   /* this wave's copy */
+  uint32_t *Hb = (uint32_t *)(smem + L.hb) + wave * NW;      /* this wave's copy */
   double *ckb = (double *)(smem + L.ck);
   int *ccnt = (int *)(smem + L.ccnt);
   int32_t *sab = (int32_t *)(smem + L.sab);     /* a[M], b[M] */
   int32_t *scnt = (int32_t *)(smem + L.scnt);   /* t0[M], f0[M], t1[M], f1[M] */
   int32_t *sd = (int32_t *)(smem + L.sd);       /* proposal deltas [4][KT*64] */
+  double *part = (double *)(smem + L.part);
+  int *tot = (int *)(smem + L.tot);
+  double *xs = (double *)(smem + L.xs) + wave;
   uint64_t *misc = (uint64_t *)(smem + L.misc);
-  double *dmisc = (double *)misc;
 
   /* ---- load tables and state */
   for (int i = tid; i < 128; i += TB) {
@@ -706,7 +738,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   for (int k = 0; k < SR_NHMAX; ++k) hp[k] = (k < nh) ? A.hp[(size_t)chain * SR_NHMAX + k] : -1;
   double c = A.cdl[(size_t)chain * 4 + 0];
   double d = A.cdl[(size_t)chain * 4 + 1];
-  double loglik = A.cdl[(size_t)chain * 4 + 2];   /* maintained by wave 0 */
+  double loglik = A.cdl[(size_t)chain * 4 + 2];   /* identical in every thread */
   DRng R;
   R.ring = ring;
   {
@@ -719,7 +751,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   unsigned long long acc[7];
 #pragma unroll
   for (int k = 0; k < 7; ++k) acc[k] = 0;
-  int rcur = 0;   /* current rpi buffer (wave 0 only writes rpi) */
+  int rcur = 0;     /* current rpi buffer */
+  int par = 0;      /* parity of the double-buffered exchange slots */
   __syncthreads();
 
   const double ec = sr_exp_m(SR_LOGEPSILON, &tb);
@@ -732,43 +765,40 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   for (int call = 0; call < A.calls; ++call) {
     for (int sw = 0; sw < A.spc; ++sw) {
       const bool want_logl = (sw == A.spc - 1);
-      /* ============ phase A (wave 0): totals and the c, d draws (mcmc.c:768-825) */
-      if (w0) {
+      /* ============ phase A: totals and the c, d draws (mcmc.c:768-825) */
+      {
         int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-        for (int m = lane; m < M; m += 64) { s0 += scnt[m]; s1 += scnt[M + m]; s2 += scnt[2 * M + m]; s3 += scnt[3 * M + m]; }
+        for (int m = tid; m < M; m += TB) { s0 += scnt[m]; s1 += scnt[M + m]; s2 += scnt[2 * M + m]; s3 += scnt[3 * M + m]; }
         for (int off = 32; off > 0; off >>= 1) {
           s0 += __shfl_xor(s0, off); s1 += __shfl_xor(s1, off);
           s2 += __shfl_xor(s2, off); s3 += __shfl_xor(s3, off);
         }
-        double ncd[2] = {c, d};
-        for (int which = 0; which < 2; ++which) {   /* mcmc_samplec then mcmc_sampled */
-          const double ba = which ? (double)s1 : (double)s3, bb = which ? (double)s2 : (double)s0;
-          ncd[which] = d_samplebeta(R, ncd[which], ba, bb, which ? SR_MIND : SR_MINC, which ? SR_MAXD : SR_MAXC, lane, tb);
-        }
-        c = ncd[0];
-        d = ncd[1];
-        if (lane == 0) {
-          dmisc[MS_C] = c;
-          dmisc[MS_D] = d;
-          dmisc[MS_CC] = sr_log_m(1. - sr_exp_m(c, &tb), &tb);
-          dmisc[MS_DD] = sr_log_m(1. - sr_exp_m(d, &tb), &tb);
-          misc[MS_BLK] = R.blk; misc[MS_OFF] = R.off; misc[MS_GEN] = R.gen;
-          acc[0]++; acc[1]++;
-        }
+        int *tw = tot + (par * NWV + wave) * 4;
+        if (lane == 0) { tw[0] = s0; tw[1] = s1; tw[2] = s2; tw[3] = s3; }
       }
       STAMP(0);
       __syncthreads();
-      c = dmisc[MS_C];
-      d = dmisc[MS_D];
+      {
+        int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll
+        for (int w = 0; w < NWV; ++w) {
+          const int *tw = tot + (par * NWV + w) * 4;
+          s0 += tw[0]; s1 += tw[1]; s2 += tw[2]; s3 += tw[3];
+        }
+        /* mcmc_samplec then mcmc_sampled: Beta(1 + f1, 1 + t0), Beta(1 + f0, 1 + t1) */
+        c = d_samplebeta<false>(R, c, (double)s3, (double)s0, SR_MINC, SR_MAXC, tid, TB, tb);
+        d = d_samplebeta<false>(R, d, (double)s1, (double)s2, SR_MIND, SR_MAXD, tid, TB, tb);
+        if (tid == 0) { acc[0]++; acc[1]++; }
+      }
       CD K;
-      K.c = c; K.d = d; K.cc = dmisc[MS_CC]; K.dd = dmisc[MS_DD]; K.ec = ec;
-      R.blk = (uint32_t)misc[MS_BLK]; R.off = (uint32_t)misc[MS_OFF]; R.gen = (uint32_t)misc[MS_GEN];
+      K.c = c; K.d = d; K.cc = sr_log_m(1. - sr_exp_m(c, &tb), &tb); K.dd = sr_log_m(1. - sr_exp_m(d, &tb), &tb); K.ec = ec;
       /* one position's value in q (log2 units): zero -> d - cc, one -> dd - c */
       const double vA = (K.d - K.cc) * 1.4426950408889634;
       const double vB = (K.dd - K.c) * 1.4426950408889634;
+      const double rA = sr_exp_m(K.cc - K.d, &tb), rB = sr_exp_m(K.c - K.dd, &tb);   /* 2^-vA, 2^-vB */
 
-      /* ============ phase B (all): Gibbs update of every (a_m, b_m) (mcmc_sampleab) */
-      rng_ensure(R, 2 * M, tid, TB);
+      /* ============ phase B: Gibbs update of own (a_m, b_m) (mcmc_sampleab) */
+      rng_ensure(R, min(2 * M + SR_RNG_SLACK, (SR_RING - 1) * SR_MT_N - (SR_MT_N - 1)), tid, TB);
       {
         unsigned long long nchg = 0;
         for (int m = tid; m < M; m += TB) {
@@ -778,9 +808,9 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           const int a0 = sab[m], b0 = sab[M + m];
           int t0 = scnt[m], f0 = scnt[M + m], t1 = scnt[2 * M + m], f1 = scnt[3 * M + m];
           int d0, e0, d1, e1;
-          const int na = draw_fast(Pm, M, N, NW, false, a0, b0, ua, K, tb, vA, vB, ckb + tid, TB, &misc[MS_FBK], d0, e0, d1, e1);
+          const int na = draw_fast(Pm, M, N, NW, false, a0, b0, ua, K, tb, vA, vB, rA, rB, ckb + tid, TB, &misc[MS_FBK], d0, e0, d1, e1);
           t0 += d0; f0 += e0; t1 += d1; f1 += e1;
-          const int tt = draw_fast(Pm, M, N, NW, true, N - b0, N - na, ub, K, tb, vA, vB, ckb + tid, TB, &misc[MS_FBK], d0, e0, d1, e1);
+          const int tt = draw_fast(Pm, M, N, NW, true, N - b0, N - na, ub, K, tb, vA, vB, rA, rB, ckb + tid, TB, &misc[MS_FBK], d0, e0, d1, e1);
           t0 += d0; f0 += e0; t1 += d1; f1 += e1;
           const int nb = N - tt;
           nchg += (na != a0) + (nb != b0);
@@ -794,312 +824,329 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       }
       rng_skip(R, 2 * M);
       STAMP(1);
-      __syncthreads();
+      if (want_logl) {   /* mcmc_logl (mcmc.c:639-645), sequential over m, lane 0 of every wave */
+        __syncthreads();
+        if (lane == 0) {
+          double s = 0.0;
+          int m = 0;
+          for (; m + 4 <= M; m += 4) {
+            const double a0 = lbuf[m], a1 = lbuf[m + 1], a2 = lbuf[m + 2], a3 = lbuf[m + 3];
+            s = s + a0; s = s + a1; s = s + a2; s = s + a3;
+          }
+          for (; m < M; ++m) s = s + lbuf[m];
+          *xs = s;
+        }
+        wsync();
+        loglik = *xs;
+        wsync();
+      }
       STAMP(2);
 
-      /* ============ phase C (wave 0): logl and the permutation proposals */
-      if (w0) {
-        if (want_logl) {
-          if (lane == 0) {   /* mcmc_logl (mcmc.c:639-645), sequential over m */
-            double s = 0.0;
-            int m = 0;
-            for (; m + 4 <= M; m += 4) {
-              const double a0 = lbuf[m], a1 = lbuf[m + 1], a2 = lbuf[m + 2], a3 = lbuf[m + 3];
-              s = s + a0; s = s + a1; s = s + a2; s = s + a3;
-            }
-            for (; m < M; ++m) s = s + lbuf[m];
-            dmisc[MS_LLS] = s;
-          }
-          wsync();
-          loglik = dmisc[MS_LLS];
-        }
-        for (int pr = 0; pr < 16; ++pr) {
-          /* order: pi2(swap), then 5 x (pi1, pi2, pi3) (mcmc.c:237-243) */
-          const int kind = (pr == 0) ? 21 : ((pr - 1) % 3 == 0 ? 1 : ((pr - 1) % 3 == 1 ? 20 : 3));
-          int i, j, inc1 = 0, inc2 = 0, ii = 0, jj = 0, Kn = 0;
-          bool veto = false;
-          if (kind == 1) {
-            i = (int)rng_uint_fast<true>(R, udN, lane, 64);
-            j = (int)rng_uint_fast<true>(R, udN1, lane, 64);
+      /* ============ phase C: the permutation proposals (mcmc.c:237-243) */
+      for (int pr = 0; pr < 16; ++pr) {
+        /* order: pi2(swap), then 5 x (pi1, pi2, pi3) */
+        const int kind = (pr == 0) ? 21 : ((pr - 1) % 3 == 0 ? 1 : ((pr - 1) % 3 == 1 ? 20 : 3));
+        int i, j, inc1 = 0, inc2 = 0, ii = 0, jj = 0, Kn = 0;
+        bool veto = false;
+        if (kind == 1) {                                   /* mcmc.c:1133-1160 */
+          i = (int)rng_uint_fast<false>(R, udN, tid, TB);
+          j = (int)rng_uint_fast<false>(R, udN1, tid, TB);
+          if (j >= i) j++;
+          ii = min(i, j); jj = max(i, j);
+          if (is_hard(hp, nh, i) && hard_count(hp, nh, ii, jj) > 1) veto = true;
+        } else if (kind == 20 || kind == 21) {             /* mcmc.c:1317-1364 */
+          if (kind == 20) {
+            i = (int)rng_uint_fast<false>(R, udN, tid, TB);
+            j = (int)rng_uint_fast<false>(R, udN1, tid, TB);
             if (j >= i) j++;
-            ii = min(i, j); jj = max(i, j);
-            if (is_hard(hp, nh, i) && hard_count(hp, nh, ii, jj) > 1) veto = true;
-          } else if (kind == 20 || kind == 21) {
-            if (kind == 20) {
-              i = (int)rng_uint_fast<true>(R, udN, lane, 64);
-              j = (int)rng_uint_fast<true>(R, udN1, lane, 64);
-              if (j >= i) j++;
-              else { int t = i; i = j; j = t; }
-            } else {
-              i = (int)rng_uint_fast<true>(R, udN1, lane, 64);
-              j = i + 1;
-            }
-            if (hard_count(hp, nh, i, j) > 1) veto = true;
-            if (!veto) {
-              inc1 = (int)rng_uint_fast<true>(R, ud2, lane, 64);
-              inc2 = (int)rng_uint_fast<true>(R, ud2, lane, 64);
-            }
+            else { int t = i; i = j; j = t; }
           } else {
-            if ((uint32_t)N - nhard < 2) { veto = true; i = j = 0; }
-            else {
-              int n0 = (int)rng_uint_fast<true>(R, udH, lane, 64);
-              int m0 = (int)rng_uint_fast<true>(R, udH1, lane, 64);
-              if (n0 <= m0) { i = n0; j = m0 + 1; } else { i = m0; j = n0; }
-              /* rank -> position (mcmc.c:1518-1533), hard positions ascending */
+            i = (int)rng_uint_fast<false>(R, udN1, tid, TB);
+            j = i + 1;
+          }
+          if (hard_count(hp, nh, i, j) > 1) veto = true;
+          if (!veto) {
+            inc1 = (int)rng_uint_fast<false>(R, ud2, tid, TB);
+            inc2 = (int)rng_uint_fast<false>(R, ud2, tid, TB);
+          }
+        } else {                                           /* mcmc.c:1495-1565 */
+          if ((uint32_t)N - nhard < 2) { veto = true; i = j = 0; }
+          else {
+            int n0 = (int)rng_uint_fast<false>(R, udH, tid, TB);
+            int m0 = (int)rng_uint_fast<false>(R, udH1, tid, TB);
+            if (n0 <= m0) { i = n0; j = m0 + 1; } else { i = m0; j = n0; }
+            /* rank -> position (mcmc.c:1518-1533), hard positions ascending */
 #pragma unroll
-              for (int k = 0; k < SR_NHMAX; ++k) {
-                if (k >= nh) break;
-                if (hp[k] <= i) { i++; j++; }
-                else if (hp[k] <= j) j++;
-              }
-              inc1 = (int)rng_uint_fast<true>(R, ud2, lane, 64);
-              inc2 = (int)rng_uint_fast<true>(R, ud2, lane, 64);
-              Kn = (j - i + 1) - hard_count(hp, nh, i, j);
-              /* non-hard positions of [i, j] in order (nhpos[rank]) and the hard bitmap */
-              for (int n = i + lane; n <= j; n += 64)
-                if (!is_hard(hp, nh, n)) nhpos[(n - i) - hard_count(hp, nh, i, n - 1)] = n;
-              for (int w = lane; w < NW; w += 64) {
-                uint32_t hbits = 0;
-#pragma unroll
-                for (int q = 0; q < SR_NHMAX; ++q) {
-                  if (q >= nh) break;
-                  if ((hp[q] >> 5) == w) hbits |= 1u << (hp[q] & 31);
-                }
-                Hb[w] = hbits;
-              }
-              wsync();
+            for (int k = 0; k < SR_NHMAX; ++k) {
+              if (k >= nh) break;
+              if (hp[k] <= i) { i++; j++; }
+              else if (hp[k] <= j) j++;
             }
-          }
-          STAMP(3);
-          if (veto) continue;
-
-          /* ---- per-taxon count changes and terms (lane owns m = lane + 64k) */
-          double tsum = 0.0, tabs_ = 0.0;
-          int Kt = 0;
-          for (int k = 0; k < KT; ++k) {
-            const int m = lane + 64 * k;
-            int dt0 = 0, df0 = 0, dt1 = 0, df1 = 0;
-            if (m < M) {
-              const uint32_t *Pm = P + m;
-              const int a = sab[m], b = sab[M + m];
-              if (kind == 1) {                                   /* mcmc.c:1175-1256 */
-                int ain, bin;
-                const int v = (Pm[(i >> 5) * M] >> (i & 31)) & 1;
-                if (i < j) {
-                  ain = (ii < a && a <= jj + 1);
-                  bin = (ii < b && b <= jj + 1);
-                  if (ain && !bin) { if (v) { dt1++; df1--; } else { dt0--; df0++; } }
-                  else if (!ain && bin) { if (v) { dt1--; df1++; } else { dt0++; df0--; } }
-                } else {
-                  ain = (ii <= a && a <= jj);
-                  bin = (ii <= b && b <= jj);
-                  if (!ain && bin) { if (v) { dt1++; df1--; } else { dt0--; df0++; } }
-                  else if (ain && !bin) { if (v) { dt1--; df1++; } else { dt0++; df0--; } }
-                }
-              } else if (kind != 3) {                            /* mcmc.c:1367-1436 */
-                const int ain = ininterval(a, i, j + 1, inc1, inc2);
-                const int bin = ininterval(b, i, j + 1, inc1, inc2);
-                if (ain && !bin) {
-                  int O1, O2;
-                  ones_split(Pm, M, i, a, j + 1, O1, O2);
-                  const int Z1 = (a - i) - O1, Z2 = (j + 1 - a) - O2;
-                  dt1 = O1 - O2; df1 = -O1 + O2; dt0 = -Z1 + Z2; df0 = Z1 - Z2;
-                } else if (!ain && bin) {
-                  int O1, O2;
-                  ones_split(Pm, M, i, b, j + 1, O1, O2);
-                  const int Z1 = (b - i) - O1, Z2 = (j + 1 - b) - O2;
-                  dt1 = -O1 + O2; df1 = O1 - O2; dt0 = Z1 - Z2; df0 = -Z1 + Z2;
-                }
-              } else {                                           /* mcmc.c:1568-1631 */
-                const int ain = ininterval(a, i, j + 1, inc1, inc2);
-                const int bin = ininterval(b, i, j + 1, inc1, inc2);
-                int na, nb;
-                if (ain && !bin) { na = i + j + 1 - a; nb = b; }
-                else if (!ain && bin) { na = a; nb = i + j + 1 - b; }
-                else if (ain && bin) { na = i + j + 1 - b; nb = i + j + 1 - a; }
-                else { na = a; nb = b; }
-                /* by words: was-alive = [a,b) n [i,j]; is-alive after the move (the site at n
-                   goes to p[n]) = hard positions in [na,nb) plus the non-hard positions whose
-                   mirrored rank lands in [na,nb): ranks [Kn-s_hi, Kn-s_lo) */
-                const int xa = min(max(na, i), j + 1), xb = min(max(nb, i), j + 1);
-                const int s_lo = (xa - i) - hard_count(hp, nh, i, xa - 1);
-                const int s_hi = (xb - i) - hard_count(hp, nh, i, xb - 1);
-                int pl = 1, ph = 0;
-                if (s_lo < s_hi) { pl = nhpos[Kn - s_hi]; ph = nhpos[Kn - s_lo - 1]; }
-                for (int w = i >> 5; w <= (j >> 5); ++w) {
-                  const uint32_t rng = range_mask(w, i, j);
-                  const uint32_t H = Hb[w];
-                  const uint32_t Wm = range_mask(w, max(a, i), min(b - 1, j)) & rng;
-                  const uint32_t Im = ((range_mask(w, pl, ph) & ~H) | (range_mask(w, max(na, i), min(nb - 1, j)) & H)) & rng;
-                  const uint32_t dying = Wm & ~Im, born = Im & ~Wm;
-                  const uint32_t col = Pm[w * M];
-                  const int od = __popc(col & dying), zd = __popc(dying) - od;
-                  const int ob = __popc(col & born), zb = __popc(born) - ob;
-                  dt1 += ob - od; df1 += od - ob; dt0 += zd - zb; df0 += zb - zd;
-                }
-              }
+            inc1 = (int)rng_uint_fast<false>(R, ud2, tid, TB);
+            inc2 = (int)rng_uint_fast<false>(R, ud2, tid, TB);
+            Kn = (j - i + 1) - hard_count(hp, nh, i, j);
+            /* this wave's copy of the non-hard positions of [i, j] in order and the hard bitmap */
+            int base = 0;
+            for (int n0b = i; n0b <= j; n0b += 64) {
+              const int n = n0b + lane;
+              const bool nhp = (n <= j) && !is_hard(hp, nh, n);
+              const uint64_t msk = __ballot(nhp);
+              const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
+              if (nhp) nhpos[base + pos] = n;
+              base += __popcll(msk);
             }
-            const double tv = (m < M) ? qval(dt0, df0, dt1, df1, K) : 0.0;
-            const uint64_t msk = __ballot(tv != 0.0);
-            const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
-            if (tv != 0.0) cbuf[k * 64 + pos] = tv;
-            if (lane == 0) ccnt[k] = __popcll(msk);
-            Kt += __popcll(msk);
-            tsum += tv;
-            tabs_ += __builtin_fabs(tv);
-            sd[k * 64 + lane] = dt0; sd[(KT + k) * 64 + lane] = df0;
-            sd[(2 * KT + k) * 64 + lane] = dt1; sd[(3 * KT + k) * 64 + lane] = df1;
-          }
-          for (int off = 32; off > 0; off >>= 1) {
-            tsum += __shfl_xor(tsum, off);
-            tabs_ += __shfl_xor(tabs_, off);
-          }
-          STAMP(4);
-          /* ---- certified MH decision (mcmc.c:1261 / 1441 / 1636).  S = tree sum of the terms,
-             A = sum |t|, Kt = #nonzero: |sequential delta - S| <= (Kt + 14) 2^-53 A (1+eps), so
-             E = (Kt + 64) 2^-52 A decides "delta >= 0" and "delta > log u" unless the true value
-             is within E; then (and whenever the exact delta feeds a saved loglik) the exact
-             sequential sum runs.  uniform_pos is drawn only once delta < 0 is known. */
-          const double Eb = ((double)Kt + 64.0) * 0x1p-52 * tabs_;
-          double delta = 0.0, lu = 0.0;
-          bool have_exact = false, drew = false;
-          int state;   /* 0 reject, 1 accept, 2 undecided */
-          if (Kt == 0) { have_exact = true; state = 1; }
-          else if (tsum > Eb) state = 1;
-          else if (tsum < -Eb) {
-            lu = sr_log_m(rng_uniform_pos<true>(R, lane, 64), &tb);
-            drew = true;
-            state = (tsum - Eb > lu) ? 1 : ((tsum + Eb < lu) ? 0 : 2);
-          } else state = 2;
-          if (state == 2) {
-            delta = exact_sum_w0(cbuf, ccnt, KT, &dmisc[MS_DELTA], lane);
-            have_exact = true;
-            if (lane == 0) misc[MS_NEXACT]++;
-            if (delta >= 0.) state = 1;
-            else {
-              if (!drew) lu = sr_log_m(rng_uniform_pos<true>(R, lane, 64), &tb);
-              state = (delta > lu) ? 1 : 0;
-            }
-          }
-          STAMP(5);
-          if (state == 0) continue;
-          if (want_logl && !have_exact) delta = exact_sum_w0(cbuf, ccnt, KT, &dmisc[MS_DELTA], lane);
-          if (lane == 0) acc[kind == 1 ? 3 : kind == 20 ? 4 : kind == 21 ? 5 : 6]++;
-          loglik += delta;
-          /* ---- apply: limits, counts, columns (lane-private taxa) */
-          for (int k = 0; k < KT; ++k) {
-            const int m = lane + 64 * k;
-            if (m >= M) continue;
-            uint32_t *Pm = P + m;
-            const int a = sab[m], b = sab[M + m];
-            scnt[m] += sd[k * 64 + lane];
-            scnt[M + m] += sd[(KT + k) * 64 + lane];
-            scnt[2 * M + m] += sd[(2 * KT + k) * 64 + lane];
-            scnt[3 * M + m] += sd[(3 * KT + k) * 64 + lane];
-            if (kind == 1) {                                     /* mcmc.c:1266-1297 */
-              if (i < j) {
-                if (ii < a && a <= jj + 1) sab[m] = a - 1;
-                if (ii < b && b <= jj + 1) sab[M + m] = b - 1;
-                const uint32_t vb = (Pm[(i >> 5) * M] >> (i & 31)) & 1u;
-                for (int w = i >> 5; w <= (j >> 5); ++w) {
-                  const uint32_t old = Pm[w * M];
-                  const uint32_t nxt = (w + 1 < NW) ? Pm[(w + 1) * M] : 0u;
-                  const uint32_t sh = (old >> 1) | (nxt << 31);
-                  const uint32_t m1 = range_mask(w, i, j - 1);
-                  uint32_t nw = (old & ~m1) | (sh & m1);
-                  if ((j >> 5) == w) nw = (nw & ~(1u << (j & 31))) | (vb << (j & 31));
-                  Pm[w * M] = nw;
-                }
-              } else {
-                if (ii <= a && a <= jj) sab[m] = a + 1;
-                if (ii <= b && b <= jj) sab[M + m] = b + 1;
-                const uint32_t vb = (Pm[(i >> 5) * M] >> (i & 31)) & 1u;
-                for (int w = i >> 5; w >= (j >> 5); --w) {
-                  const uint32_t old = Pm[w * M];
-                  const uint32_t prv = (w > 0) ? Pm[(w - 1) * M] : 0u;
-                  const uint32_t sh = (old << 1) | (prv >> 31);
-                  const uint32_t m1 = range_mask(w, j + 1, i);
-                  uint32_t nw = (old & ~m1) | (sh & m1);
-                  if ((j >> 5) == w) nw = (nw & ~(1u << (j & 31))) | (vb << (j & 31));
-                  Pm[w * M] = nw;
-                }
-              }
-            } else {                                             /* mcmc.c:1446-1474, 1641-1670 */
-              const int ain = ininterval(a, i, j + 1, inc1, inc2);
-              const int bin = ininterval(b, i, j + 1, inc1, inc2);
-              if (ain && !bin) sab[m] = i + j + 1 - a;
-              else if (!ain && bin) sab[M + m] = i + j + 1 - b;
-              else if (ain && bin) { sab[M + m] = i + j + 1 - a; sab[m] = i + j + 1 - b; }
-              if (kind != 3) {
-                for (int n = i; n < i + j - n; ++n) {
-                  const int p2 = i + j - n;
-                  const uint32_t b1 = (Pm[(n >> 5) * M] >> (n & 31)) & 1u, b2 = (Pm[(p2 >> 5) * M] >> (p2 & 31)) & 1u;
-                  if (b1 != b2) { Pm[(n >> 5) * M] ^= (1u << (n & 31)); Pm[(p2 >> 5) * M] ^= (1u << (p2 & 31)); }
-                }
-              } else {
-                for (int r = 0; r < Kn - 1 - r; ++r) {
-                  const int n = nhpos[r], p2 = nhpos[Kn - 1 - r];
-                  const uint32_t b1 = (Pm[(n >> 5) * M] >> (n & 31)) & 1u, b2 = (Pm[(p2 >> 5) * M] >> (p2 & 31)) & 1u;
-                  if (b1 != b2) { Pm[(n >> 5) * M] ^= (1u << (n & 31)); Pm[(p2 >> 5) * M] ^= (1u << (p2 & 31)); }
-                }
-              }
-            }
-          }
-          /* ---- rpi (double-buffered full permutation) and hard positions */
-          {
-            const int32_t *ro = rcur ? rpiB : rpiA;
-            int32_t *rn = rcur ? rpiA : rpiB;
-            if (kind == 1) {
-              for (int n = lane; n < N; n += 64) {
-                int src = n;
-                if (i < j) { if (n >= i && n < j) src = n + 1; else if (n == j) src = i; }
-                else { if (n > j && n <= i) src = n - 1; else if (n == j) src = i; }
-                rn[n] = ro[src];
-              }
+            for (int w = lane; w < NW; w += 64) {
+              uint32_t hbits = 0;
 #pragma unroll
               for (int q = 0; q < SR_NHMAX; ++q) {
                 if (q >= nh) break;
-                const int h = hp[q];
-                if (h == i) hp[q] = j;
-                else if (i < j && h > i && h <= j) hp[q] = h - 1;
-                else if (i > j && h >= j && h < i) hp[q] = h + 1;
+                if ((hp[q] >> 5) == w) hbits |= 1u << (hp[q] & 31);
               }
-            } else if (kind != 3) {
-              for (int n = lane; n < N; n += 64) rn[n] = ro[(n >= i && n <= j) ? (i + j - n) : n];
-#pragma unroll
-              for (int q = 0; q < SR_NHMAX; ++q) {
-                if (q >= nh) break;
-                if (hp[q] >= i && hp[q] <= j) hp[q] = i + j - hp[q];
-              }
-            } else {
-              for (int n = lane; n < N; n += 64)
-                if (n < i || n > j || is_hard(hp, nh, n)) rn[n] = ro[n];
-              for (int r = lane; r < Kn; r += 64) rn[nhpos[r]] = ro[nhpos[Kn - 1 - r]];
+              Hb[w] = hbits;
             }
-            rcur ^= 1;
             wsync();
           }
-          STAMP(6);
-        } /* proposals */
-      }   /* wave 0 */
+        }
+        STAMP(3);
+        if (veto) continue;
+
+        /* ---- own taxa's count changes and terms (chunk ch = m >> 6 of 64 taxa per wave) */
+        double *cb = cbuf + par * KT * 64;
+        int *cc = ccnt + par * KT;
+        double tsum = 0.0, tabs_ = 0.0;
+        int Kt = 0;
+        for (int m0 = wave * 64; m0 < KT * 64; m0 += TB) {
+          const int ch = m0 >> 6, m = m0 + lane;
+          int dt0 = 0, df0 = 0, dt1 = 0, df1 = 0;
+          if (m < M) {
+            const uint32_t *Pm = P + m;
+            const int a = sab[m], b = sab[M + m];
+            if (kind == 1) {                                   /* mcmc.c:1175-1256 */
+              int ain, bin;
+              const int v = (Pm[(i >> 5) * M] >> (i & 31)) & 1;
+              if (i < j) {
+                ain = (ii < a && a <= jj + 1);
+                bin = (ii < b && b <= jj + 1);
+                if (ain && !bin) { if (v) { dt1++; df1--; } else { dt0--; df0++; } }
+                else if (!ain && bin) { if (v) { dt1--; df1++; } else { dt0++; df0--; } }
+              } else {
+                ain = (ii <= a && a <= jj);
+                bin = (ii <= b && b <= jj);
+                if (!ain && bin) { if (v) { dt1++; df1--; } else { dt0--; df0++; } }
+                else if (ain && !bin) { if (v) { dt1--; df1++; } else { dt0++; df0--; } }
+              }
+            } else if (kind != 3) {                            /* mcmc.c:1367-1436 */
+              const int ain = ininterval(a, i, j + 1, inc1, inc2);
+              const int bin = ininterval(b, i, j + 1, inc1, inc2);
+              if (ain && !bin) {
+                int O1, O2;
+                ones_split(Pm, M, i, a, j + 1, O1, O2);
+                const int Z1 = (a - i) - O1, Z2 = (j + 1 - a) - O2;
+                dt1 = O1 - O2; df1 = -O1 + O2; dt0 = -Z1 + Z2; df0 = Z1 - Z2;
+              } else if (!ain && bin) {
+                int O1, O2;
+                ones_split(Pm, M, i, b, j + 1, O1, O2);
+                const int Z1 = (b - i) - O1, Z2 = (j + 1 - b) - O2;
+                dt1 = -O1 + O2; df1 = O1 - O2; dt0 = Z1 - Z2; df0 = -Z1 + Z2;
+              }
+            } else {                                           /* mcmc.c:1568-1631 */
+              const int ain = ininterval(a, i, j + 1, inc1, inc2);
+              const int bin = ininterval(b, i, j + 1, inc1, inc2);
+              int na, nb;
+              if (ain && !bin) { na = i + j + 1 - a; nb = b; }
+              else if (!ain && bin) { na = a; nb = i + j + 1 - b; }
+              else if (ain && bin) { na = i + j + 1 - b; nb = i + j + 1 - a; }
+              else { na = a; nb = b; }
+              /* by words: was-alive = [a,b) n [i,j]; is-alive after the move (the site at n
+                 goes to p[n]) = hard positions in [na,nb) plus the non-hard positions whose
+                 mirrored rank lands in [na,nb): ranks [Kn-s_hi, Kn-s_lo) */
+              const int xa = min(max(na, i), j + 1), xb = min(max(nb, i), j + 1);
+              const int s_lo = (xa - i) - hard_count(hp, nh, i, xa - 1);
+              const int s_hi = (xb - i) - hard_count(hp, nh, i, xb - 1);
+              int pl = 1, ph = 0;
+              if (s_lo < s_hi) { pl = nhpos[Kn - s_hi]; ph = nhpos[Kn - s_lo - 1]; }
+              for (int w = i >> 5; w <= (j >> 5); ++w) {
+                const uint32_t rng = range_mask(w, i, j);
+                const uint32_t H = Hb[w];
+                const uint32_t Wm = range_mask(w, max(a, i), min(b - 1, j)) & rng;
+                const uint32_t Im = ((range_mask(w, pl, ph) & ~H) | (range_mask(w, max(na, i), min(nb - 1, j)) & H)) & rng;
+                const uint32_t dying = Wm & ~Im, born = Im & ~Wm;
+                const uint32_t col = Pm[w * M];
+                const int od = __popc(col & dying), zd = __popc(dying) - od;
+                const int ob = __popc(col & born), zb = __popc(born) - ob;
+                dt1 += ob - od; df1 += od - ob; dt0 += zd - zb; df0 += zb - zd;
+              }
+            }
+          }
+          const double tv = (m < M) ? qval(dt0, df0, dt1, df1, K) : 0.0;
+          const uint64_t msk = __ballot(tv != 0.0);
+          const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
+          if (tv != 0.0) cb[ch * 64 + pos] = tv;
+          if (lane == 0) cc[ch] = __popcll(msk);
+          Kt += __popcll(msk);
+          tsum += tv;
+          tabs_ += __builtin_fabs(tv);
+          sd[ch * 64 + lane] = dt0; sd[(KT + ch) * 64 + lane] = df0;
+          sd[(2 * KT + ch) * 64 + lane] = dt1; sd[(3 * KT + ch) * 64 + lane] = df1;
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+          tsum += __shfl_xor(tsum, off);
+          tabs_ += __shfl_xor(tabs_, off);
+        }
+        {
+          double *pw = part + (par * NWV + wave) * 4;
+          if (lane == 0) { pw[0] = tsum; pw[1] = tabs_; pw[2] = (double)Kt; }
+        }
+        STAMP(4);
+        __syncthreads();
+        /* ---- certified MH decision (mcmc.c:1261 / 1441 / 1636), identical in every thread.
+           S = tree sum of the terms, A = sum |t|, Kt = #nonzero: |sequential delta - S| <=
+           2 Kt 2^-53 A (1+eps), so E = (Kt + 64) 2^-52 A decides "delta >= 0" and "delta > log u"
+           unless the true value is within E; then (and whenever the exact delta feeds a saved
+           loglik) the exact sequential sum runs.  uniform_pos is drawn only once delta < 0 is known. */
+        double S = 0.0, Aabs = 0.0, Ktd = 0.0;
+#pragma unroll
+        for (int w = 0; w < NWV; ++w) {
+          const double *pw = part + (par * NWV + w) * 4;
+          S += pw[0]; Aabs += pw[1]; Ktd += pw[2];
+        }
+        const double Eb = (Ktd + 64.0) * 0x1p-52 * Aabs;
+        double delta = S, lu = 0.0;
+        bool have_exact = false, drew = false;
+        int state;   /* 0 reject, 1 accept, 2 undecided */
+        if (Ktd == 0.0) { have_exact = true; delta = 0.0; state = 1; }
+        else if (S > Eb) state = 1;
+        else if (S < -Eb) {
+          lu = sr_log_m(rng_uniform_pos<false>(R, tid, TB), &tb);
+          drew = true;
+          state = (S - Eb > lu) ? 1 : ((S + Eb < lu) ? 0 : 2);
+        } else state = 2;
+        if (state == 2) {
+          delta = exact_sum_wave(cb, cc, KT, xs, lane);
+          have_exact = true;
+          if (tid == 0) misc[MS_NEXACT]++;
+          if (delta >= 0.) state = 1;
+          else {
+            if (!drew) lu = sr_log_m(rng_uniform_pos<false>(R, tid, TB), &tb);
+            state = (delta > lu) ? 1 : 0;
+          }
+        }
+        par ^= 1;
+        STAMP(5);
+        if (state == 0) continue;
+        if (want_logl && !have_exact) delta = exact_sum_wave(cb, cc, KT, xs, lane);
+        if (tid == 0) acc[kind == 1 ? 3 : kind == 20 ? 4 : kind == 21 ? 5 : 6]++;
+        loglik += delta;
+        /* ---- apply to own taxa: limits, counts, columns */
+        for (int m0 = wave * 64; m0 < KT * 64; m0 += TB) {
+          const int ch = m0 >> 6, m = m0 + lane;
+          if (m >= M) continue;
+          uint32_t *Pm = P + m;
+          const int a = sab[m], b = sab[M + m];
+          scnt[m] += sd[ch * 64 + lane];
+          scnt[M + m] += sd[(KT + ch) * 64 + lane];
+          scnt[2 * M + m] += sd[(2 * KT + ch) * 64 + lane];
+          scnt[3 * M + m] += sd[(3 * KT + ch) * 64 + lane];
+          if (kind == 1) {                                     /* mcmc.c:1266-1297 */
+            if (i < j) {
+              if (ii < a && a <= jj + 1) sab[m] = a - 1;
+              if (ii < b && b <= jj + 1) sab[M + m] = b - 1;
+              const uint32_t vb = (Pm[(i >> 5) * M] >> (i & 31)) & 1u;
+              for (int w = i >> 5; w <= (j >> 5); ++w) {
+                const uint32_t old = Pm[w * M];
+                const uint32_t nxt = (w + 1 < NW) ? Pm[(w + 1) * M] : 0u;
+                const uint32_t sh = (old >> 1) | (nxt << 31);
+                const uint32_t m1 = range_mask(w, i, j - 1);
+                uint32_t nw = (old & ~m1) | (sh & m1);
+                if ((j >> 5) == w) nw = (nw & ~(1u << (j & 31))) | (vb << (j & 31));
+                Pm[w * M] = nw;
+              }
+            } else {
+              if (ii <= a && a <= jj) sab[m] = a + 1;
+              if (ii <= b && b <= jj) sab[M + m] = b + 1;
+              const uint32_t vb = (Pm[(i >> 5) * M] >> (i & 31)) & 1u;
+              for (int w = i >> 5; w >= (j >> 5); --w) {
+                const uint32_t old = Pm[w * M];
+                const uint32_t prv = (w > 0) ? Pm[(w - 1) * M] : 0u;
+                const uint32_t sh = (old << 1) | (prv >> 31);
+                const uint32_t m1 = range_mask(w, j + 1, i);
+                uint32_t nw = (old & ~m1) | (sh & m1);
+                if ((j >> 5) == w) nw = (nw & ~(1u << (j & 31))) | (vb << (j & 31));
+                Pm[w * M] = nw;
+              }
+            }
+          } else {                                             /* mcmc.c:1446-1474, 1641-1670 */
+            const int ain = ininterval(a, i, j + 1, inc1, inc2);
+            const int bin = ininterval(b, i, j + 1, inc1, inc2);
+            if (ain && !bin) sab[m] = i + j + 1 - a;
+            else if (!ain && bin) sab[M + m] = i + j + 1 - b;
+            else if (ain && bin) { sab[M + m] = i + j + 1 - a; sab[m] = i + j + 1 - b; }
+            if (kind != 3) {
+              for (int n = i; n < i + j - n; ++n) {
+                const int p2 = i + j - n;
+                const uint32_t b1 = (Pm[(n >> 5) * M] >> (n & 31)) & 1u, b2 = (Pm[(p2 >> 5) * M] >> (p2 & 31)) & 1u;
+                if (b1 != b2) { Pm[(n >> 5) * M] ^= (1u << (n & 31)); Pm[(p2 >> 5) * M] ^= (1u << (p2 & 31)); }
+              }
+            } else {
+              for (int r = 0; r < Kn - 1 - r; ++r) {
+                const int n = nhpos[r], p2 = nhpos[Kn - 1 - r];
+                const uint32_t b1 = (Pm[(n >> 5) * M] >> (n & 31)) & 1u, b2 = (Pm[(p2 >> 5) * M] >> (p2 & 31)) & 1u;
+                if (b1 != b2) { Pm[(n >> 5) * M] ^= (1u << (n & 31)); Pm[(p2 >> 5) * M] ^= (1u << (p2 & 31)); }
+              }
+            }
+          }
+        }
+        /* ---- rpi (double-buffered full permutation, read only at save time) and hard positions */
+        {
+          const int32_t *ro = rcur ? rpiB : rpiA;
+          int32_t *rn = rcur ? rpiA : rpiB;
+          if (kind == 1) {
+            for (int n = tid; n < N; n += TB) {
+              int src = n;
+              if (i < j) { if (n >= i && n < j) src = n + 1; else if (n == j) src = i; }
+              else { if (n > j && n <= i) src = n - 1; else if (n == j) src = i; }
+              rn[n] = ro[src];
+            }
+#pragma unroll
+            for (int q = 0; q < SR_NHMAX; ++q) {
+              if (q >= nh) break;
+              const int h = hp[q];
+              if (h == i) hp[q] = j;
+              else if (i < j && h > i && h <= j) hp[q] = h - 1;
+              else if (i > j && h >= j && h < i) hp[q] = h + 1;
+            }
+          } else if (kind != 3) {
+            for (int n = tid; n < N; n += TB) rn[n] = ro[(n >= i && n <= j) ? (i + j - n) : n];
+#pragma unroll
+            for (int q = 0; q < SR_NHMAX; ++q) {
+              if (q >= nh) break;
+              if (hp[q] >= i && hp[q] <= j) hp[q] = i + j - hp[q];
+            }
+          } else {
+            for (int n = tid; n < N; n += TB)
+              if (n < i || n > j || is_hard(hp, nh, n)) rn[n] = ro[n];
+            for (int r = tid; r < Kn; r += TB) rn[nhpos[r]] = ro[nhpos[Kn - 1 - r]];   /* own wave's full copy */
+          }
+          rcur ^= 1;
+        }
+        STAMP(6);
+      } /* proposals */
       STAMP(6);
+      __syncthreads();
     } /* sweeps */
 
     /* ---------------- saved sample (mcmc_save_chain, mcmc.c:69-92) */
     if (A.save) {
-      if (w0 && lane == 0) { dmisc[MS_LLS] = loglik; misc[MS_RCUR] = (uint64_t)rcur; }
-      __syncthreads();
       const int slot = A.rec_base + call;
       const int W = 2 * M + N;
       int16_t *rec = A.rec_abpi + ((size_t)chain * A.rec_cap + slot) * W;
       for (int m = tid; m < 2 * M; m += TB) rec[m] = (int16_t)sab[m];
-      const int32_t *rc = misc[MS_RCUR] ? rpiB : rpiA;
+      const int32_t *rc = rcur ? rpiB : rpiA;
       for (int n = tid; n < N; n += TB) rec[2 * M + rc[n]] = (int16_t)n;
       if (tid == 0) {
         double *rd = A.rec_cdl + ((size_t)chain * A.rec_cap + slot) * 3;
-        rd[0] = c; rd[1] = d; rd[2] = dmisc[MS_LLS];
+        rd[0] = c; rd[1] = d; rd[2] = loglik;
       }
-      __syncthreads();
     }
   } /* calls */
 
@@ -1109,11 +1156,10 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 #ifdef SR_STAMPS
   if (tid == 0) { A.dbg[blockIdx.x * 17 * 8 + 0] += misc[MS_NEXACT]; for (int q_ = 0; q_ < 4; ++q_) A.dbg[blockIdx.x * 17 * 8 + 1 + q_] += misc[MS_FBK + q_]; }
 #endif
-  if (w0 && lane == 0) { misc[MS_RCUR] = (uint64_t)rcur; dmisc[MS_LLS] = loglik; }
   __syncthreads();
   uint32_t *oP = A.P + (size_t)chain * NW * M;
   for (int i = tid; i < NW * M; i += TB) oP[i] = P[i];
-  const int32_t *rc = misc[MS_RCUR] ? rpiB : rpiA;
+  const int32_t *rc = rcur ? rpiB : rpiA;
   int32_t *orpi = A.rpi + (size_t)chain * N;
   for (int i = tid; i < N; i += TB) orpi[i] = rc[i];
   uint32_t *omt = A.mt + (size_t)chain * SR_RING * SR_MT_N;
@@ -1128,7 +1174,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       if (k < nh) A.hp[(size_t)chain * SR_NHMAX + k] = hp[k];
     A.cdl[(size_t)chain * 4 + 0] = c;
     A.cdl[(size_t)chain * 4 + 1] = d;
-    A.cdl[(size_t)chain * 4 + 2] = dmisc[MS_LLS];
+    A.cdl[(size_t)chain * 4 + 2] = loglik;
     A.rng[(size_t)chain * 2 + 0] = (uint64_t)R.blk * SR_MT_N + R.off;
     A.rng[(size_t)chain * 2 + 1] = R.gen;
     for (int k = 0; k < 7; ++k) A.acc[(size_t)chain * 8 + k] += acc[k];

@@ -104,6 +104,7 @@ __host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB)
 #define MS_NEXACT 13
 #define MS_FBK 14   /* +1 prev fail, +2 here fail, +3 S==0 (slots 15,16,17) */
 #define MS_RCUR 18
+#define MS_ACC 24   /* 7 acceptance counters (thread 0) */
 
 /* ---------------------------------------------------------------- sync */
 template <bool WAVE>
@@ -236,6 +237,31 @@ __device__ __forceinline__ uint32_t rng_uint_fast(DRng &r, const UDiv &u, int t,
   return k;
 }
 
+/* quotient get()/scale of gsl_rng_uniform_int for a tempered word g (k >= n means GSL rejects g) */
+__device__ __forceinline__ uint32_t udiv_word(uint32_t g, const UDiv &u)
+{
+  uint32_t q = (uint32_t)((double)g * u.rs);
+  const uint64_t qs = (uint64_t)q * u.scale;
+  if (qs > g) q--;
+  else if (g - (uint32_t)qs >= u.scale) q++;
+  return q;
+}
+
+/* the next 8 tempered words from the cursor, loaded together, if they are resident (the ring
+ * is a circular buffer of SR_RING * 624 words: block b lives at (b mod SR_RING) * 624) */
+__device__ __forceinline__ bool rng_window8(const DRng &r, uint32_t (&w)[8])
+{
+  if (r.blk + (r.off + 7) / SR_MT_N >= r.gen) return false;
+  const uint32_t base = (r.blk & (SR_RING - 1)) * SR_MT_N + r.off;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    uint32_t idx = base + k;
+    idx = (idx >= SR_RING * SR_MT_N) ? idx - SR_RING * SR_MT_N : idx;
+    w[k] = sr_mt_temper(r.ring[idx]);
+  }
+  return true;
+}
+
 /* ------------------------------------------------ GSL beta/gamma/ziggurat */
 template <bool WAVE>
 __device__ __forceinline__ double d_gauss_zig(DRng &r, int lane, int nthr, const sr_mtab &tb)
@@ -294,8 +320,9 @@ template <bool WAVE>
 __device__ __forceinline__ double d_samplebeta(DRng &r, double x, double a, double b, double low, double high, int lane,
                                                int nthr, const sr_mtab &tb)
 {
-  double x1 = d_gamma<WAVE>(r, 1. + a, lane, nthr, tb);
-  double x2 = d_gamma<WAVE>(r, 1. + b, lane, nthr, tb);
+  double g[2];
+  for (int k = 0; k < 2; ++k) g[k] = d_gamma<WAVE>(r, 1. + (k ? b : a), lane, nthr, tb);   /* one inlined copy */
+  const double x1 = g[0], x2 = g[1];
   double y = x1 / (x1 + x2);
   if (y > 0.) {
     y = sr_log_m(y, &tb);
@@ -356,7 +383,7 @@ struct BitWalk {
 /* mcmc_auxa + mcmc_logtop + mcmc_randompick for one limit of one taxon, in walk
  * coordinates (fwd: walk w = position w; rev: walk w = position N-1-w).  o = current limit,
  * entries w = 0..L.  Returns the picked entry and the count deltas dt0,df0,dt1,df1 there. */
-__device__ __forceinline__ int draw_exact(const uint32_t *Pm, int M, int N, bool rev, int o, int L, double u,
+__device__ __noinline__ int draw_exact(const uint32_t *Pm, int M, int N, bool rev, int o, int L, double u,
                                       const CD &k, const sr_mtab &tb, int &dt0, int &df0, int &dt1, int &df1)
 {
   const int POo = rev ? ones_range(Pm, M, N - o, N) : ones_range(Pm, M, 0, o);
@@ -748,9 +775,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
     R.off = (uint32_t)(pos % SR_MT_N);
     R.gen = (uint32_t)gen;
   }
-  unsigned long long acc[7];
-#pragma unroll
-  for (int k = 0; k < 7; ++k) acc[k] = 0;
+  if (tid == 0) for (int k = 0; k < 7; ++k) misc[MS_ACC + k] = 0;
   int rcur = 0;     /* current rpi buffer */
   int par = 0;      /* parity of the double-buffered exchange slots */
   __syncthreads();
@@ -786,9 +811,13 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           s0 += tw[0]; s1 += tw[1]; s2 += tw[2]; s3 += tw[3];
         }
         /* mcmc_samplec then mcmc_sampled: Beta(1 + f1, 1 + t0), Beta(1 + f0, 1 + t1) */
-        c = d_samplebeta<false>(R, c, (double)s3, (double)s0, SR_MINC, SR_MAXC, tid, TB, tb);
-        d = d_samplebeta<false>(R, d, (double)s1, (double)s2, SR_MIND, SR_MAXD, tid, TB, tb);
-        if (tid == 0) { acc[0]++; acc[1]++; }
+        double cd2[2] = {c, d};
+        for (int k = 0; k < 2; ++k)
+          cd2[k] = d_samplebeta<false>(R, cd2[k], (double)(k ? s1 : s3), (double)(k ? s2 : s0), k ? SR_MIND : SR_MINC,
+                                       k ? SR_MAXD : SR_MAXC, tid, TB, tb);
+        c = cd2[0];
+        d = cd2[1];
+        if (tid == 0) { misc[MS_ACC + 0]++; misc[MS_ACC + 1]++; }
       }
       CD K;
       K.c = c; K.d = d; K.cc = sr_log_m(1. - sr_exp_m(c, &tb), &tb); K.dd = sr_log_m(1. - sr_exp_m(d, &tb), &tb); K.ec = ec;
@@ -807,12 +836,17 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           const double ub = rng_peek(R, 2 * m + 1) / 4294967296.0;
           const int a0 = sab[m], b0 = sab[M + m];
           int t0 = scnt[m], f0 = scnt[M + m], t1 = scnt[2 * M + m], f1 = scnt[3 * M + m];
-          int d0, e0, d1, e1;
-          const int na = draw_fast(Pm, M, N, NW, false, a0, b0, ua, K, tb, vA, vB, rA, rB, ckb + tid, TB, &misc[MS_FBK], d0, e0, d1, e1);
-          t0 += d0; f0 += e0; t1 += d1; f1 += e1;
-          const int tt = draw_fast(Pm, M, N, NW, true, N - b0, N - na, ub, K, tb, vA, vB, rA, rB, ckb + tid, TB, &misc[MS_FBK], d0, e0, d1, e1);
-          t0 += d0; f0 += e0; t1 += d1; f1 += e1;
-          const int nb = N - tt;
+          /* a_m over [0, b_m], then b_m over the reversed column with limit N - a_new: one
+             inlined copy of the draw, two trips */
+          int na = a0, nb = b0;
+          for (int pass = 0; pass < 2; ++pass) {
+            int d0, e0, d1, e1;
+            const bool rev = pass != 0;
+            const int res = draw_fast(Pm, M, N, NW, rev, rev ? N - b0 : a0, rev ? N - na : b0, rev ? ub : ua, K, tb,
+                                      vA, vB, rA, rB, ckb + tid, TB, &misc[MS_FBK], d0, e0, d1, e1);
+            t0 += d0; f0 += e0; t1 += d1; f1 += e1;
+            if (rev) nb = N - res; else na = res;
+          }
           nchg += (na != a0) + (nb != b0);
           sab[m] = na; sab[M + m] = nb;
           scnt[m] = t0; scnt[M + m] = f0; scnt[2 * M + m] = t1; scnt[3 * M + m] = f1;
@@ -848,32 +882,62 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         const int kind = (pr == 0) ? 21 : ((pr - 1) % 3 == 0 ? 1 : ((pr - 1) % 3 == 1 ? 20 : 3));
         int i, j, inc1 = 0, inc2 = 0, ii = 0, jj = 0, Kn = 0;
         bool veto = false;
+        /* draws (GSL order): taken from 8 prefetched words when none of them
+           is a uniform_int rejection, else word by word */
+        uint32_t W8[8];
+        const bool fw = rng_window8(R, W8);
         if (kind == 1) {                                   /* mcmc.c:1133-1160 */
-          i = (int)rng_uint_fast<false>(R, udN, tid, TB);
-          j = (int)rng_uint_fast<false>(R, udN1, tid, TB);
+          const uint32_t x0 = udiv_word(W8[0], udN), x1 = udiv_word(W8[1], udN1);
+          if (fw && x0 < udN.n && x1 < udN1.n) { i = (int)x0; j = (int)x1; rng_skip(R, 2); }
+          else {
+            i = (int)rng_uint_fast<false>(R, udN, tid, TB);
+            j = (int)rng_uint_fast<false>(R, udN1, tid, TB);
+          }
           if (j >= i) j++;
           ii = min(i, j); jj = max(i, j);
           if (is_hard(hp, nh, i) && hard_count(hp, nh, ii, jj) > 1) veto = true;
         } else if (kind == 20 || kind == 21) {             /* mcmc.c:1317-1364 */
+          bool got = false;
           if (kind == 20) {
-            i = (int)rng_uint_fast<false>(R, udN, tid, TB);
-            j = (int)rng_uint_fast<false>(R, udN1, tid, TB);
+            const uint32_t x0 = udiv_word(W8[0], udN), x1 = udiv_word(W8[1], udN1);
+            if (fw && x0 < udN.n && x1 < udN1.n) { i = (int)x0; j = (int)x1; rng_skip(R, 2); got = true; }
+            else {
+              i = (int)rng_uint_fast<false>(R, udN, tid, TB);
+              j = (int)rng_uint_fast<false>(R, udN1, tid, TB);
+            }
             if (j >= i) j++;
             else { int t = i; i = j; j = t; }
           } else {
-            i = (int)rng_uint_fast<false>(R, udN1, tid, TB);
+            const uint32_t x0 = udiv_word(W8[0], udN1);
+            if (fw && x0 < udN1.n) { i = (int)x0; rng_skip(R, 1); got = true; }
+            else i = (int)rng_uint_fast<false>(R, udN1, tid, TB);
             j = i + 1;
           }
           if (hard_count(hp, nh, i, j) > 1) veto = true;
           if (!veto) {
-            inc1 = (int)rng_uint_fast<false>(R, ud2, tid, TB);
-            inc2 = (int)rng_uint_fast<false>(R, ud2, tid, TB);
+            const uint32_t g2 = (kind == 21) ? W8[1] : W8[2], g3 = (kind == 21) ? W8[2] : W8[3];
+            const uint32_t x2 = udiv_word(g2, ud2), x3 = udiv_word(g3, ud2);
+            if (got && x2 < 2u && x3 < 2u) { inc1 = (int)x2; inc2 = (int)x3; rng_skip(R, 2); }
+            else {
+              inc1 = (int)rng_uint_fast<false>(R, ud2, tid, TB);
+              inc2 = (int)rng_uint_fast<false>(R, ud2, tid, TB);
+            }
           }
         } else {                                           /* mcmc.c:1495-1565 */
           if ((uint32_t)N - nhard < 2) { veto = true; i = j = 0; }
           else {
-            int n0 = (int)rng_uint_fast<false>(R, udH, tid, TB);
-            int m0 = (int)rng_uint_fast<false>(R, udH1, tid, TB);
+            int n0, m0;
+            const uint32_t x0 = udiv_word(W8[0], udH), x1 = udiv_word(W8[1], udH1);
+            const uint32_t x2 = udiv_word(W8[2], ud2), x3 = udiv_word(W8[3], ud2);
+            if (fw && x0 < udH.n && x1 < udH1.n && x2 < 2u && x3 < 2u) {
+              n0 = (int)x0; m0 = (int)x1; inc1 = (int)x2; inc2 = (int)x3;
+              rng_skip(R, 4);
+            } else {
+              n0 = (int)rng_uint_fast<false>(R, udH, tid, TB);
+              m0 = (int)rng_uint_fast<false>(R, udH1, tid, TB);
+              inc1 = (int)rng_uint_fast<false>(R, ud2, tid, TB);
+              inc2 = (int)rng_uint_fast<false>(R, ud2, tid, TB);
+            }
             if (n0 <= m0) { i = n0; j = m0 + 1; } else { i = m0; j = n0; }
             /* rank -> position (mcmc.c:1518-1533), hard positions ascending */
 #pragma unroll
@@ -882,28 +946,32 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               if (hp[k] <= i) { i++; j++; }
               else if (hp[k] <= j) j++;
             }
-            inc1 = (int)rng_uint_fast<false>(R, ud2, tid, TB);
-            inc2 = (int)rng_uint_fast<false>(R, ud2, tid, TB);
             Kn = (j - i + 1) - hard_count(hp, nh, i, j);
-            /* this wave's copy of the non-hard positions of [i, j] in order and the hard bitmap */
+            /* this wave's hard bitmap (lane w holds word w) and its non-hard positions of [i, j] */
+            uint32_t hbl = 0;
+#pragma unroll
+            for (int q = 0; q < SR_NHMAX; ++q) {
+              if (q >= nh) break;
+              if ((hp[q] >> 5) == lane) hbl |= 1u << (hp[q] & 31);
+            }
+            if (lane < NW) Hb[lane] = hbl;
             int base = 0;
             for (int n0b = i; n0b <= j; n0b += 64) {
               const int n = n0b + lane;
-              const bool nhp = (n <= j) && !is_hard(hp, nh, n);
+              const uint32_t hw = (NW <= 64) ? (uint32_t)__shfl((int)hbl, min(n, N - 1) >> 5) : 0u;
+              const bool hard = (NW <= 64) ? (((hw >> (n & 31)) & 1u) != 0u) : is_hard(hp, nh, n);
+              const bool nhp = (n <= j) && !hard;
               const uint64_t msk = __ballot(nhp);
               const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
               if (nhp) nhpos[base + pos] = n;
               base += __popcll(msk);
             }
-            for (int w = lane; w < NW; w += 64) {
-              uint32_t hbits = 0;
-#pragma unroll
-              for (int q = 0; q < SR_NHMAX; ++q) {
-                if (q >= nh) break;
-                if ((hp[q] >> 5) == w) hbits |= 1u << (hp[q] & 31);
+            if (NW > 64)
+              for (int w = 64 + lane; w < NW; w += 64) {
+                uint32_t hbits = 0;
+                for (int q = 0; q < nh; ++q) if ((hp[q] >> 5) == w) hbits |= 1u << (hp[q] & 31);
+                Hb[w] = hbits;
               }
-              Hb[w] = hbits;
-            }
             wsync();
           }
         }
@@ -1035,7 +1103,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         STAMP(5);
         if (state == 0) continue;
         if (want_logl && !have_exact) delta = exact_sum_wave(cb, cc, KT, xs, lane);
-        if (tid == 0) acc[kind == 1 ? 3 : kind == 20 ? 4 : kind == 21 ? 5 : 6]++;
+        if (tid == 0) misc[MS_ACC + (kind == 1 ? 3 : kind == 20 ? 4 : kind == 21 ? 5 : 6)]++;
         loglik += delta;
         /* ---- apply to own taxa: limits, counts, columns */
         for (int m0 = wave * 64; m0 < KT * 64; m0 += TB) {
@@ -1177,7 +1245,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
     A.cdl[(size_t)chain * 4 + 2] = loglik;
     A.rng[(size_t)chain * 2 + 0] = (uint64_t)R.blk * SR_MT_N + R.off;
     A.rng[(size_t)chain * 2 + 1] = R.gen;
-    for (int k = 0; k < 7; ++k) A.acc[(size_t)chain * 8 + k] += acc[k];
+    for (int k = 0; k < 7; ++k) A.acc[(size_t)chain * 8 + k] += misc[MS_ACC + k];
     A.acc[(size_t)chain * 8 + 2] += misc[MS_CAB];
     A.acc[(size_t)chain * 8 + 7] += misc[MS_NEXACT];
   }

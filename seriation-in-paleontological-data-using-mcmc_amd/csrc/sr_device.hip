@@ -42,6 +42,9 @@ __constant__ double c_log_invc[128] = SR_LOG_INVC_INIT;
 __constant__ double c_log_lhi[128] = SR_LOG_LHI_INIT;
 __constant__ double c_log_llo[128] = SR_LOG_LLO_INIT;
 
+#ifndef SR_EXP
+#define SR_EXP 0   /* timing experiments only (breaks the sampler): 1 skip proposals, 2 skip Gibbs */
+#endif
 #define SR_ZIGR 3.44428647676
 
 struct KArgs {
@@ -59,9 +62,11 @@ struct KArgs {
 
 /* ---------------------------------------------------------------- LDS carve */
 struct Lay {
-  size_t tab, cbuf, lbuf, mt, P, rpi0, rpi1, nhpos, hb, ck, ccnt, sab, scnt, sd, part, tot, xs, misc, total;
+  size_t tab, cbuf, lbuf, mt, P, rpi0, rpi1, ht, ck, ccnt, sab, scnt, pinfo, part, tot, xs, misc, total;
 };
 __host__ __device__ static inline size_t sr_al16(size_t x) { return (x + 15) & ~(size_t)15; }
+/* Gibbs checkpoint slots per word: one per thread that owns a taxon */
+__host__ __device__ static inline int sr_ckstride(int M, int TB) { return M >= TB ? TB : ((M + 63) & ~63); }
 __host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB)
 {
   Lay L;
@@ -74,14 +79,13 @@ __host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB)
   L.P = o;     o = sr_al16(o + (size_t)NW * M * 4);
   L.rpi0 = o;  o = sr_al16(o + (size_t)N * 4);
   L.rpi1 = o;  o = sr_al16(o + (size_t)N * 4);
-  L.nhpos = o; o = sr_al16(o + (size_t)NWV * N * 4);                     /* per wave */
-  L.hb = o;    o = sr_al16(o + (size_t)NWV * NW * 4);                    /* per wave */
-  L.ck = o;    o = sr_al16(o + (size_t)((N >> 5) + 1) * TB * sizeof(double));
+  L.ht = o;    o = sr_al16(o + (size_t)NWV * (2 * N + 2) * 2);           /* per wave: hcnt[N+1], nhall[N] (int16) */
+  L.ck = o;    o = sr_al16(o + (size_t)((N >> 5) + 1) * sr_ckstride(M, TB) * sizeof(double));
   L.ccnt = o;  o = sr_al16(o + (size_t)2 * KT * 4);
   L.sab = o;   o = sr_al16(o + (size_t)2 * M * 4);
   L.scnt = o;  o = sr_al16(o + (size_t)4 * M * 4);
-  L.sd = o;    o = sr_al16(o + (size_t)4 * KT * 64 * 4);
-  L.part = o;  o = sr_al16(o + (size_t)2 * NWV * 4 * sizeof(double));  /* [2][wave] tsum, tabs, Kt */
+  L.pinfo = o; o = sr_al16(o + (size_t)NWV * 16 * 8 * 4);             /* per wave: drawn proposals */
+  L.part = o;  o = sr_al16(o + (size_t)2 * 16 * NWV * 8 * 4);         /* [2][proposal][wave] count sums */
   L.tot = o;   o = sr_al16(o + (size_t)2 * NWV * 4 * 4);               /* [2][wave] t0, f0, t1, f1 */
   L.xs = o;    o = sr_al16(o + (size_t)NWV * sizeof(double));          /* per-wave broadcast slot */
   L.misc = o;  o = sr_al16(o + 64 * 8);
@@ -667,6 +671,27 @@ __device__ __forceinline__ void wsync()
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
+/* Wave-wide integer sum with DPP row operations (no LDS round trips); every lane of the wave
+ * must be active.  Result is wave-uniform. */
+__device__ __forceinline__ int wave_sum_i32(int x)
+{
+  x += __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);    /* quad_perm [1,0,3,2] */
+  x += __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);    /* quad_perm [2,3,0,1] */
+  x += __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false);   /* row_half_mirror */
+  x += __builtin_amdgcn_update_dpp(0, x, 0x140, 0xF, 0xF, false);   /* row_mirror: row sums */
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);   /* row_bcast:15 -> rows 1, 3 */
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);   /* row_bcast:31 -> rows 2, 3 */
+  return __builtin_amdgcn_readlane(x, 63);
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int l)
+{
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
 /* Exact delta: the reference's sequential `delta += term` over ascending m (mcmc.c:1214,
  * 1435, 1630), computed by lane 0 of the calling wave and broadcast through its slot.
  * Zero terms are skipped (adding +-0 is exact; s is never -0.0).  Nonzero terms were
@@ -691,6 +716,146 @@ __device__ __forceinline__ double exact_sum_wave(const double *cbuf, const int *
   const double r = *slot;
   wsync();
   return r;
+}
+
+/* ---------------------------------------------------------------- proposals */
+#define PK_PI1 1
+#define PK_PI2 20
+#define PK_SWAP 21
+#define PK_PI3 3
+/* order within a sweep: pi2(swap), then 5 x (pi1, pi2, pi3) (mcmc.c:237-243) */
+__device__ __forceinline__ int prop_kind(int p) { return p == 0 ? PK_SWAP : ((p - 1) % 3 == 0 ? PK_PI1 : ((p - 1) % 3 == 1 ? PK_PI2 : PK_PI3)); }
+
+/* a drawn proposal (block-uniform values) */
+struct Prop { int i, j, ii, jj, inc1, inc2, Kn, r0; };   /* r0: non-hard rank of i (pi3) */
+
+/* Per-wave hard-site tables (hard positions hp[] ascending): hcnt[x] = #hard positions < x
+ * (x = 0..N), nhall[r] = position of the r-th non-hard position.  Rebuilt whenever hp moves. */
+__device__ __forceinline__ void build_hard_tables(const int *hp, int nh, int N, int16_t *hcnt, int16_t *nhall, int lane)
+{
+  int base = 0;
+  for (int x0 = 0; x0 <= N; x0 += 64) {
+    const int x = x0 + lane;
+    bool h = false;
+#pragma unroll
+    for (int k = 0; k < SR_NHMAX; ++k) {
+      if (k >= nh) break;
+      h |= (hp[k] == x);
+    }
+    const uint64_t msk = __ballot(h && x < N);
+    const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
+    if (x <= N) hcnt[x] = (int16_t)(base + below);
+    if (x < N && !h) nhall[x - (base + below)] = (int16_t)x;
+    base += __popcll(msk);
+  }
+  wsync();
+}
+
+/* Count changes of one taxon (limits a, b; position-ordered column Pm) under proposal q:
+ * dt0 (zeros inside), dt1 (ones inside); the reference's df0 = -dt0 and df1 = -dt1 always
+ * (mcmc.c:1175-1256 pi1, 1367-1436 pi2, 1568-1631 pi3).  hcnt/nhall: the wave's hard-site tables. */
+__device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, const uint32_t *Pm, int M,
+                                         const int *hp, int nh, const int16_t *hcnt, const int16_t *nhall, int &dt0, int &dt1)
+{
+  const int i = q.i, j = q.j;
+  dt0 = 0; dt1 = 0;
+  if (kind == PK_PI1) {
+    const int ii = q.ii, jj = q.jj;
+    const int v = (Pm[(i >> 5) * M] >> (i & 31)) & 1;
+    int sgn = 0;   /* +1: the moved site enters the taxon's range, -1: leaves it */
+    if (i < j) {
+      const bool ain = (ii < a && a <= jj + 1), bin = (ii < b && b <= jj + 1);
+      sgn = (ain && !bin) ? 1 : ((!ain && bin) ? -1 : 0);
+    } else {
+      const bool ain = (ii <= a && a <= jj), bin = (ii <= b && b <= jj);
+      sgn = (!ain && bin) ? 1 : ((ain && !bin) ? -1 : 0);
+    }
+    if (v) dt1 = sgn; else dt0 = -sgn;
+  } else if (kind != PK_PI3) {
+    const int ain = ininterval(a, i, j + 1, q.inc1, q.inc2);
+    const int bin = ininterval(b, i, j + 1, q.inc1, q.inc2);
+    if (ain != bin) {
+      const int sp = ain ? a : b;
+      int O1, O2;
+      ones_split(Pm, M, i, sp, j + 1, O1, O2);
+      const int Z1 = (sp - i) - O1, Z2 = (j + 1 - sp) - O2;
+      if (ain) { dt1 = O1 - O2; dt0 = Z2 - Z1; }
+      else { dt1 = O2 - O1; dt0 = Z1 - Z2; }
+    }
+  } else {
+    const int ain = ininterval(a, i, j + 1, q.inc1, q.inc2);
+    const int bin = ininterval(b, i, j + 1, q.inc1, q.inc2);
+    int na, nb;
+    if (ain && !bin) { na = i + j + 1 - a; nb = b; }
+    else if (!ain && bin) { na = a; nb = i + j + 1 - b; }
+    else if (ain && bin) { na = i + j + 1 - b; nb = i + j + 1 - a; }
+    else { na = a; nb = b; }
+    /* Sets of pre-move positions inside [i, j]: W = alive before = [max(a,i), min(b-1,j)];
+       I = alive after = the non-hard positions whose mirrored non-hard rank lands in [na, nb)
+       (ranks [Kn-s_hi, Kn-s_lo) -> positions nhall[r0 + ...]) plus the hard positions of
+       [na, nb) (fixed points).  dt1 = ones(I) - ones(W), dt0 = zeros(W) - zeros(I). */
+    const int xa = min(max(na, i), j + 1), xb = min(max(nb, i), j + 1);
+    const int ri = q.r0;                                   /* = i - hcnt[i] */
+    const int s_lo = (xa - hcnt[xa]) - ri, s_hi = (xb - hcnt[xb]) - ri;
+    /* column bits at the hard positions, bit k = hard site k */
+    uint32_t hbm = 0;
+#pragma unroll
+    for (int k = 0; k < SR_NHMAX; ++k) {
+      if (k >= nh) break;
+      hbm |= ((Pm[(hp[k] >> 5) * M] >> (hp[k] & 31)) & 1u) << k;
+    }
+    auto hard_ones = [&](int lo, int hi, int &cnt) -> int {   /* hard positions in [lo, hi] */
+      if (hi < lo) { cnt = 0; return 0; }
+      const int kl = hcnt[lo], kh = hcnt[hi + 1];
+      cnt = kh - kl;
+      const uint32_t km = ((kh >= 32) ? 0xffffffffu : ((1u << kh) - 1u)) & ~((kl >= 32) ? 0xffffffffu : ((1u << kl) - 1u));
+      return __popc(hbm & km);
+    };
+    const int wlo = max(a, i), whi = min(b - 1, j);
+    const int sizeW = max(0, whi - wlo + 1);
+    const int onesW = ones_range(Pm, M, wlo, whi + 1);
+    int onesI = 0, sizeI = 0;
+    if (s_lo < s_hi) {
+      const int pl = nhall[ri + q.Kn - s_hi], ph = nhall[ri + q.Kn - s_lo - 1];
+      int hc;
+      const int ho = hard_ones(pl, ph, hc);
+      onesI = ones_range(Pm, M, pl, ph + 1) - ho;
+      sizeI = s_hi - s_lo;
+    }
+    {
+      int hc;
+      const int ho = hard_ones(max(na, i), min(nb - 1, j), hc);
+      onesI += ho;
+      sizeI += hc;
+    }
+    dt1 = onesI - onesW;
+    dt0 = (sizeW - onesW) - (sizeI - onesI);
+  }
+}
+
+/* pinfo record (ints): i, j, flags (bit0 inc1, bit1 inc2, bit2 veto), Kn, uniform word, words
+ * consumed through the draws, words consumed through the uniform_pos draw */
+#define PI_STRIDE 8
+
+/* The exact delta of one proposal: the reference's per-taxon terms (qval, mcmc.c:1214,
+ * 1435, 1630 term order) compacted per 64-taxon chunk into cb, then summed sequentially in
+ * ascending m by lane 0 of every wave.  Block-uniform call (contains a barrier). */
+__device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const int32_t *sab, const uint32_t *P, int M, int KT,
+                                              const int *hp, int nh, const int16_t *hcnt, const int16_t *nhall, double *cb, int *cc, double *xs,
+                                              int lane, int wave, int TB)
+{
+  for (int m0 = wave * 64; m0 < KT * 64; m0 += TB) {
+    const int ch = m0 >> 6, m = m0 + lane;
+    int dt0 = 0, dt1 = 0;
+    if (m < M) taxon_dt(kind, q, sab[m], sab[M + m], P + m, M, hp, nh, hcnt, nhall, dt0, dt1);
+    const double tv = (m < M) ? qval(dt0, -dt0, dt1, -dt1, K) : 0.0;
+    const uint64_t msk = __ballot(tv != 0.0);
+    const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
+    if (tv != 0.0) cb[ch * 64 + pos] = tv;
+    if (lane == 0) cc[ch] = __popcll(msk);
+  }
+  __syncthreads();
+  return exact_sum_wave(cb, cc, KT, xs, lane);
 }
 
 /* words of slack kept resident after the Gibbs draws: the proposals and the next c, d
@@ -724,14 +889,15 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   uint32_t *P = (uint32_t *)(smem + L.P);
   int32_t *rpiA = (int32_t *)(smem + L.rpi0);
   int32_t *rpiB = (int32_t *)(smem + L.rpi1);
-  int32_t *nhpos = (int32_t *)(smem + L.nhpos) + wave * N;   /* this wave's copy */
-  uint32_t *Hb = (uint32_t *)(smem + L.hb) + wave * NW;      /* this wave's copy */
+  int16_t *hcnt = (int16_t *)(smem + L.ht) + wave * (2 * N + 2);    /* this wave's hard-site tables */
+  int16_t *nhall = hcnt + N + 1;
+  const int CKS = sr_ckstride(M, TB);
   double *ckb = (double *)(smem + L.ck);
   int *ccnt = (int *)(smem + L.ccnt);
   int32_t *sab = (int32_t *)(smem + L.sab);     /* a[M], b[M] */
   int32_t *scnt = (int32_t *)(smem + L.scnt);   /* t0[M], f0[M], t1[M], f1[M] */
-  int32_t *sd = (int32_t *)(smem + L.sd);       /* proposal deltas [4][KT*64] */
-  double *part = (double *)(smem + L.part);
+  int *pinfo = (int *)(smem + L.pinfo);
+  int *part = (int *)(smem + L.part);
   int *tot = (int *)(smem + L.tot);
   double *xs = (double *)(smem + L.xs) + wave;
   uint64_t *misc = (uint64_t *)(smem + L.misc);
@@ -758,7 +924,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
     const int32_t *gcnt = A.cnt + (size_t)chain * 4 * M;
     for (int i = tid; i < 4 * M; i += TB) scnt[i] = gcnt[i];
   }
-  if (tid == 0) for (int q = 0; q < 24; ++q) misc[MS_CAB + q] = 0;
+  if (tid == 0) for (int q = MS_CAB; q < 64; ++q) misc[q] = 0;
 
   int hp[SR_NHMAX];
 #pragma unroll
@@ -777,9 +943,12 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   }
   if (tid == 0) for (int k = 0; k < 7; ++k) misc[MS_ACC + k] = 0;
   int rcur = 0;     /* current rpi buffer */
-  int par = 0;      /* parity of the double-buffered exchange slots */
+  int par = 0;      /* parity of the double-buffered totals */
+  int bpar = 0;     /* parity of the double-buffered proposal count sums */
+  int xpar = 0;     /* parity of the double-buffered exact-delta term lists */
   __syncthreads();
 
+  build_hard_tables(hp, nh, N, hcnt, nhall, lane);
   const double ec = sr_exp_m(SR_LOGEPSILON, &tb);
   const uint32_t nhard = (uint32_t)nh;
   const UDiv udN = make_udiv((uint32_t)N), udN1 = make_udiv((uint32_t)(N - 1)), ud2 = make_udiv(2u);
@@ -794,10 +963,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       {
         int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
         for (int m = tid; m < M; m += TB) { s0 += scnt[m]; s1 += scnt[M + m]; s2 += scnt[2 * M + m]; s3 += scnt[3 * M + m]; }
-        for (int off = 32; off > 0; off >>= 1) {
-          s0 += __shfl_xor(s0, off); s1 += __shfl_xor(s1, off);
-          s2 += __shfl_xor(s2, off); s3 += __shfl_xor(s3, off);
-        }
+        s0 = wave_sum_i32(s0); s1 = wave_sum_i32(s1); s2 = wave_sum_i32(s2); s3 = wave_sum_i32(s3);
         int *tw = tot + (par * NWV + wave) * 4;
         if (lane == 0) { tw[0] = s0; tw[1] = s1; tw[2] = s2; tw[3] = s3; }
       }
@@ -830,7 +996,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       rng_ensure(R, min(2 * M + SR_RNG_SLACK, (SR_RING - 1) * SR_MT_N - (SR_MT_N - 1)), tid, TB);
       {
         unsigned long long nchg = 0;
-        for (int m = tid; m < M; m += TB) {
+        for (int m = tid; m < M && !(SR_EXP & 2); m += TB) {
           const uint32_t *Pm = P + m;
           const double ua = rng_peek(R, 2 * m) / 4294967296.0;
           const double ub = rng_peek(R, 2 * m + 1) / 4294967296.0;
@@ -843,7 +1009,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             int d0, e0, d1, e1;
             const bool rev = pass != 0;
             const int res = draw_fast(Pm, M, N, NW, rev, rev ? N - b0 : a0, rev ? N - na : b0, rev ? ub : ua, K, tb,
-                                      vA, vB, rA, rB, ckb + tid, TB, &misc[MS_FBK], d0, e0, d1, e1);
+                                      vA, vB, rA, rB, ckb + tid, CKS, &misc[MS_FBK], d0, e0, d1, e1);
             t0 += d0; f0 += e0; t1 += d1; f1 += e1;
             if (rev) nb = N - res; else na = res;
           }
@@ -853,8 +1019,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           if (want_logl)   /* mcmc_logl term (mcmc.c:643-644) */
             lbuf[m] = (double)t0 * K.cc + (double)f0 * K.d + (double)t1 * K.dd + (double)f1 * K.c;
         }
-        for (int off = 32; off > 0; off >>= 1) nchg += __shfl_xor(nchg, off);
-        if (lane == 0 && nchg) atomicAdd((unsigned long long *)&misc[MS_CAB], nchg);
+        const int nw = wave_sum_i32((int)nchg);
+        if (lane == 0 && nw) atomicAdd((unsigned long long *)&misc[MS_CAB], (unsigned long long)nw);
       }
       rng_skip(R, 2 * M);
       STAMP(1);
@@ -876,330 +1042,342 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       }
       STAMP(2);
 
-      /* ============ phase C: the permutation proposals (mcmc.c:237-243) */
-      for (int pr = 0; pr < 16; ++pr) {
-        /* order: pi2(swap), then 5 x (pi1, pi2, pi3) */
-        const int kind = (pr == 0) ? 21 : ((pr - 1) % 3 == 0 ? 1 : ((pr - 1) % 3 == 1 ? 20 : 3));
-        int i, j, inc1 = 0, inc2 = 0, ii = 0, jj = 0, Kn = 0;
-        bool veto = false;
-        /* draws (GSL order): taken from 8 prefetched words when none of them
-           is a uniform_int rejection, else word by word */
-        uint32_t W8[8];
-        const bool fw = rng_window8(R, W8);
-        if (kind == 1) {                                   /* mcmc.c:1133-1160 */
-          const uint32_t x0 = udiv_word(W8[0], udN), x1 = udiv_word(W8[1], udN1);
-          if (fw && x0 < udN.n && x1 < udN1.n) { i = (int)x0; j = (int)x1; rng_skip(R, 2); }
-          else {
-            i = (int)rng_uint_fast<false>(R, udN, tid, TB);
-            j = (int)rng_uint_fast<false>(R, udN1, tid, TB);
-          }
-          if (j >= i) j++;
-          ii = min(i, j); jj = max(i, j);
-          if (is_hard(hp, nh, i) && hard_count(hp, nh, ii, jj) > 1) veto = true;
-        } else if (kind == 20 || kind == 21) {             /* mcmc.c:1317-1364 */
-          bool got = false;
-          if (kind == 20) {
-            const uint32_t x0 = udiv_word(W8[0], udN), x1 = udiv_word(W8[1], udN1);
-            if (fw && x0 < udN.n && x1 < udN1.n) { i = (int)x0; j = (int)x1; rng_skip(R, 2); got = true; }
-            else {
-              i = (int)rng_uint_fast<false>(R, udN, tid, TB);
-              j = (int)rng_uint_fast<false>(R, udN1, tid, TB);
-            }
-            if (j >= i) j++;
-            else { int t = i; i = j; j = t; }
-          } else {
-            const uint32_t x0 = udiv_word(W8[0], udN1);
-            if (fw && x0 < udN1.n) { i = (int)x0; rng_skip(R, 1); got = true; }
-            else i = (int)rng_uint_fast<false>(R, udN1, tid, TB);
-            j = i + 1;
-          }
-          if (hard_count(hp, nh, i, j) > 1) veto = true;
-          if (!veto) {
-            const uint32_t g2 = (kind == 21) ? W8[1] : W8[2], g3 = (kind == 21) ? W8[2] : W8[3];
-            const uint32_t x2 = udiv_word(g2, ud2), x3 = udiv_word(g3, ud2);
-            if (got && x2 < 2u && x3 < 2u) { inc1 = (int)x2; inc2 = (int)x3; rng_skip(R, 2); }
-            else {
-              inc1 = (int)rng_uint_fast<false>(R, ud2, tid, TB);
-              inc2 = (int)rng_uint_fast<false>(R, ud2, tid, TB);
-            }
-          }
-        } else {                                           /* mcmc.c:1495-1565 */
-          if ((uint32_t)N - nhard < 2) { veto = true; i = j = 0; }
-          else {
-            int n0, m0;
-            const uint32_t x0 = udiv_word(W8[0], udH), x1 = udiv_word(W8[1], udH1);
-            const uint32_t x2 = udiv_word(W8[2], ud2), x3 = udiv_word(W8[3], ud2);
-            if (fw && x0 < udH.n && x1 < udH1.n && x2 < 2u && x3 < 2u) {
-              n0 = (int)x0; m0 = (int)x1; inc1 = (int)x2; inc2 = (int)x3;
-              rng_skip(R, 4);
-            } else {
-              n0 = (int)rng_uint_fast<false>(R, udH, tid, TB);
-              m0 = (int)rng_uint_fast<false>(R, udH1, tid, TB);
-              inc1 = (int)rng_uint_fast<false>(R, ud2, tid, TB);
-              inc2 = (int)rng_uint_fast<false>(R, ud2, tid, TB);
-            }
-            if (n0 <= m0) { i = n0; j = m0 + 1; } else { i = m0; j = n0; }
-            /* rank -> position (mcmc.c:1518-1533), hard positions ascending */
-#pragma unroll
-            for (int k = 0; k < SR_NHMAX; ++k) {
-              if (k >= nh) break;
-              if (hp[k] <= i) { i++; j++; }
-              else if (hp[k] <= j) j++;
-            }
-            Kn = (j - i + 1) - hard_count(hp, nh, i, j);
-            /* this wave's hard bitmap (lane w holds word w) and its non-hard positions of [i, j] */
-            uint32_t hbl = 0;
-#pragma unroll
-            for (int q = 0; q < SR_NHMAX; ++q) {
-              if (q >= nh) break;
-              if ((hp[q] >> 5) == lane) hbl |= 1u << (hp[q] & 31);
-            }
-            if (lane < NW) Hb[lane] = hbl;
-            int base = 0;
-            for (int n0b = i; n0b <= j; n0b += 64) {
-              const int n = n0b + lane;
-              const uint32_t hw = (NW <= 64) ? (uint32_t)__shfl((int)hbl, min(n, N - 1) >> 5) : 0u;
-              const bool hard = (NW <= 64) ? (((hw >> (n & 31)) & 1u) != 0u) : is_hard(hp, nh, n);
-              const bool nhp = (n <= j) && !hard;
-              const uint64_t msk = __ballot(nhp);
-              const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
-              if (nhp) nhpos[base + pos] = n;
-              base += __popcll(msk);
-            }
-            if (NW > 64)
-              for (int w = 64 + lane; w < NW; w += 64) {
-                uint32_t hbits = 0;
-                for (int q = 0; q < nh; ++q) if ((hp[q] >> 5) == w) hbits |= 1u << (hp[q] & 31);
-                Hb[w] = hbits;
-              }
-            wsync();
-          }
-        }
-        STAMP(3);
-        if (veto) continue;
-
-        /* ---- own taxa's count changes and terms (chunk ch = m >> 6 of 64 taxa per wave) */
-        double *cb = cbuf + par * KT * 64;
-        int *cc = ccnt + par * KT;
-        double tsum = 0.0, tabs_ = 0.0;
-        int Kt = 0;
-        for (int m0 = wave * 64; m0 < KT * 64; m0 += TB) {
-          const int ch = m0 >> 6, m = m0 + lane;
-          int dt0 = 0, df0 = 0, dt1 = 0, df1 = 0;
-          if (m < M) {
-            const uint32_t *Pm = P + m;
-            const int a = sab[m], b = sab[M + m];
-            if (kind == 1) {                                   /* mcmc.c:1175-1256 */
-              int ain, bin;
-              const int v = (Pm[(i >> 5) * M] >> (i & 31)) & 1;
-              if (i < j) {
-                ain = (ii < a && a <= jj + 1);
-                bin = (ii < b && b <= jj + 1);
-                if (ain && !bin) { if (v) { dt1++; df1--; } else { dt0--; df0++; } }
-                else if (!ain && bin) { if (v) { dt1--; df1++; } else { dt0++; df0--; } }
+      /* ============ phase C: the permutation proposals (mcmc.c:237-243), speculatively batched.
+         Hypothesis: every remaining proposal is rejected.  A rejected non-vetoed proposal has
+         delta < 0, so it drew exactly one uniform_pos after its index draws; this fixes every
+         proposal's RNG words in advance.  All remaining proposals are drawn, their count sums
+         computed against the current state (one barrier), and decided lane-parallel; the first
+         one that is accepted (or needs the exact delta) ends the batch: it is applied with the
+         cursor it really consumed, and the proposals after it are re-batched. */
+      if (!(SR_EXP & 1)) {
+        int p0 = 0;
+        while (p0 < 16) {
+          /* ---- draws of proposals p0.. under the hypothesis (identical in every thread) */
+          int *pin = pinfo + wave * 16 * PI_STRIDE;
+          const int avail = (int)((R.gen - R.blk) * SR_MT_N - R.off);   /* resident words */
+          const uint32_t base = (R.blk & (SR_RING - 1)) * SR_MT_N + R.off;
+          int off = 0, pend = p0;
+          for (int p = p0; p < 16; ++p) {
+            const int kind = prop_kind(p);
+            bool bad = false;
+            auto word = [&](void) -> uint32_t {
+              if (off >= avail) { bad = true; return 0u; }
+              uint32_t idx = base + (uint32_t)off++;
+              idx = (idx >= SR_RING * SR_MT_N) ? idx - SR_RING * SR_MT_N : idx;
+              return sr_mt_temper(ring[idx]);
+            };
+            auto uint_draw = [&](const UDiv &u) -> int {   /* gsl_rng_uniform_int */
+              uint32_t k;
+              do { k = udiv_word(word(), u); } while (!bad && k >= u.n);
+              return (int)k;
+            };
+            int i = 0, j = 0, inc1 = 0, inc2 = 0, Kn = 0, r0 = 0;
+            bool veto = false;
+            if (kind == PK_PI1) {                                  /* mcmc.c:1133-1160 */
+              i = uint_draw(udN);
+              j = uint_draw(udN1);
+              if (j >= i) j++;
+              if (hcnt[i + 1] != hcnt[i] && hcnt[max(i, j) + 1] - hcnt[min(i, j)] > 1) veto = true;
+            } else if (kind == PK_PI2 || kind == PK_SWAP) {        /* mcmc.c:1317-1364 */
+              if (kind == PK_PI2) {
+                i = uint_draw(udN);
+                j = uint_draw(udN1);
+                if (j >= i) j++;
+                else { const int t = i; i = j; j = t; }
               } else {
-                ain = (ii <= a && a <= jj);
-                bin = (ii <= b && b <= jj);
-                if (!ain && bin) { if (v) { dt1++; df1--; } else { dt0--; df0++; } }
-                else if (ain && !bin) { if (v) { dt1--; df1++; } else { dt0++; df0--; } }
+                i = uint_draw(udN1);
+                j = i + 1;
               }
-            } else if (kind != 3) {                            /* mcmc.c:1367-1436 */
+              if (hcnt[j + 1] - hcnt[i] > 1) veto = true;
+              if (!veto) { inc1 = uint_draw(ud2); inc2 = uint_draw(ud2); }
+            } else {                                               /* mcmc.c:1495-1565 */
+              if ((uint32_t)N - nhard < 2) veto = true;
+              else {
+                const int n0 = uint_draw(udH), m0 = uint_draw(udH1);
+                inc1 = uint_draw(ud2);
+                inc2 = uint_draw(ud2);
+                /* non-hard ranks -> positions (mcmc.c:1505-1533) */
+                int ri, rj;
+                if (n0 <= m0) { ri = n0; rj = m0 + 1; } else { ri = m0; rj = n0; }
+                if (!bad) { i = nhall[ri]; j = nhall[rj]; }
+                Kn = rj - ri + 1;
+                r0 = ri;
+              }
+            }
+            const int nd = off;
+            uint32_t uw = 0;
+            if (!veto) { do { uw = word(); } while (!bad && uw == 0u); }   /* gsl_rng_uniform_pos */
+            if (bad) break;
+            if (lane == 0) {
+              int *r = pin + p * PI_STRIDE;
+              r[0] = i; r[1] = j; r[2] = inc1 | (inc2 << 1) | (veto ? 4 : 0); r[3] = Kn;
+              r[4] = (int)uw; r[5] = nd; r[6] = off; r[7] = r0;
+            }
+            pend = p + 1;
+          }
+          if (pend == p0) {   /* not enough resident words for one proposal: make more, retry */
+            rng_ensure(R, min(avail + 256, (SR_RING - 1) * SR_MT_N - (SR_MT_N - 1)), tid, TB);
+            continue;
+          }
+          wsync();
+
+          /* ---- exact integer count sums of every drawn proposal over own taxa, per wave */
+          int *pw = part + (bpar * 16) * NWV * 8;
+          const bool pack = N * ((M + TB - 1) / TB) < 512;   /* per-wave sums fit 16-bit fields */
+          STAMP(3);
+          for (int p = p0; p < pend; ++p) {
+            const int *r = pin + p * PI_STRIDE;
+            const int fl = __builtin_amdgcn_readfirstlane(r[2]);
+            if (fl & 4) continue;
+#ifdef SR_STAMPS
+            if (tid == 0) misc[40 + (prop_kind(p) == PK_PI1 ? 0 : prop_kind(p) == PK_PI3 ? 2 : 1)]++;
+#endif
+            const int kind = prop_kind(p);
+            Prop q;
+            q.i = __builtin_amdgcn_readfirstlane(r[0]);
+            q.j = __builtin_amdgcn_readfirstlane(r[1]);
+            q.ii = min(q.i, q.j); q.jj = max(q.i, q.j);
+            q.inc1 = fl & 1; q.inc2 = (fl >> 1) & 1;
+            q.Kn = __builtin_amdgcn_readfirstlane(r[3]);
+            q.r0 = __builtin_amdgcn_readfirstlane(r[7]);
+            int x0 = 0, x1 = 0, y0 = 0, y1 = 0, nzc = 0;
+            for (int m0 = wave * 64; m0 < M; m0 += TB) {
+              const int m = m0 + lane;
+              int dt0 = 0, dt1 = 0;
+              if (m < M) taxon_dt(kind, q, sab[m], sab[M + m], P + m, M, hp, nh, hcnt, nhall, dt0, dt1);
+              x0 += dt0; x1 += dt1; y0 += abs(dt0); y1 += abs(dt1);
+              nzc += __popcll(__ballot((dt0 | dt1) != 0));
+            }
+            int X0, X1, Y0, Y1;
+            if (pack) {
+              const int tpl = (M + TB - 1) / TB;   /* taxa per lane: each lane adds bias N per slot */
+              uint32_t u1 = (uint32_t)((x0 + N * tpl) | ((x1 + N * tpl) << 16));
+              uint32_t u2 = (uint32_t)(y0 | (y1 << 16));
+              u1 = (uint32_t)wave_sum_i32((int)u1);
+              u2 = (uint32_t)wave_sum_i32((int)u2);
+              const int bias = 64 * N * tpl;
+              X0 = (int)(u1 & 0xffffu) - bias; X1 = (int)(u1 >> 16) - bias;
+              Y0 = (int)(u2 & 0xffffu); Y1 = (int)(u2 >> 16);
+            } else {
+              X0 = wave_sum_i32(x0); X1 = wave_sum_i32(x1); Y0 = wave_sum_i32(y0); Y1 = wave_sum_i32(y1);
+            }
+            if (lane == 0) {
+              int *o = pw + (p * NWV + wave) * 8;
+              o[0] = X0; o[1] = X1; o[2] = Y0; o[3] = Y1; o[4] = nzc;
+            }
+            STAMP(kind == PK_PI1 ? 4 : (kind == PK_PI3 ? 6 : 5));
+          }
+          __syncthreads();
+
+          /* ---- lane-parallel certified decisions (lane p decides proposal p).  With
+             X = sum dt, Y = sum |dt| (exact integers), S = X0 (cc - d) + X1 (dd - c) is the exact
+             sum of the exact per-taxon terms and B = Y0 (|cc|+|d|) + Y1 (|dd|+|c|) bounds their
+             magnitudes; the reference's rounded terms and sequential sum stay within
+             (K + 7) 2^-53 B of S, K = #nonzero terms <= Knz, so Eb = (Knz + 16) 2^-52 B decides
+             delta >= 0 and delta > log u whenever the true value is farther than Eb.  log u is
+             first taken in f32 (error << 2^-16 (1 + |log u|)), exactly only when that is too close.
+             cls: 0 rejected, 1 accepted, 2 needs the exact delta or the exact log. */
+          const double aC = __builtin_fabs(K.cc) + __builtin_fabs(K.d), aD = __builtin_fabs(K.dd) + __builtin_fabs(K.c);
+          double Sp = 0.0, Ebp = 0.0;
+          int cls = 0, Knz = 0;
+          uint32_t uwp = 1;
+          {
+            const int p = lane;
+            if (p >= p0 && p < pend) {
+              const int *r = pin + p * PI_STRIDE;
+              if (!(r[2] & 4)) {
+                int X0 = 0, X1 = 0, Y0 = 0, Y1 = 0;
+#pragma unroll
+                for (int w = 0; w < NWV; ++w) {
+                  const int *o = pw + (p * NWV + w) * 8;
+                  X0 += o[0]; X1 += o[1]; Y0 += o[2]; Y1 += o[3]; Knz += o[4];
+                }
+                Sp = ((double)X0 * K.cc - (double)X0 * K.d) + ((double)X1 * K.dd - (double)X1 * K.c);
+                const double B = (double)Y0 * aC + (double)Y1 * aD;
+                Ebp = ((double)Knz + 16.0) * 0x1p-52 * B;
+                uwp = (uint32_t)r[4];
+                if (Knz == 0 || Sp > Ebp) cls = 1;
+                else if (Sp < -Ebp) {
+                  const float uf = (float)((double)uwp / 4294967296.0);
+                  const double lua = (double)__builtin_amdgcn_logf(uf) * 0.69314718055994531;
+                  const double dl = 0x1p-16 * (1.0 + __builtin_fabs(lua));
+                  cls = (Sp - Ebp > lua + dl) ? 1 : ((Sp + Ebp < lua - dl) ? 0 : 2);
+                } else cls = 2;
+              }
+            }
+          }
+          uint64_t pend_mask = __ballot(cls != 0);
+          pend_mask = __builtin_amdgcn_readfirstlane((uint32_t)pend_mask) | ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(pend_mask >> 32)) << 32);
+          bpar ^= 1;
+          int acc_p = -1, used = 0;
+          bool udrawn = false;
+          double delta = 0.0;
+          while (pend_mask) {
+            const int p = __builtin_ctzll(pend_mask);
+            pend_mask &= pend_mask - 1;
+            const int kind = prop_kind(p);
+            const int *r = pin + p * PI_STRIDE;
+            Prop q;
+            q.i = __builtin_amdgcn_readfirstlane(r[0]);
+            q.j = __builtin_amdgcn_readfirstlane(r[1]);
+            q.ii = min(q.i, q.j); q.jj = max(q.i, q.j);
+            const int fl = __builtin_amdgcn_readfirstlane(r[2]);
+            q.inc1 = fl & 1; q.inc2 = (fl >> 1) & 1;
+            q.Kn = __builtin_amdgcn_readfirstlane(r[3]);
+            q.r0 = __builtin_amdgcn_readfirstlane(r[7]);
+            const double S = readlane_f64(Sp, p), Eb = readlane_f64(Ebp, p);
+            const int c0 = __builtin_amdgcn_readlane(cls, p), kz = __builtin_amdgcn_readlane(Knz, p);
+            const double u = (double)(uint32_t)__builtin_amdgcn_readlane((int)uwp, p) / 4294967296.0;
+            bool accept = false, decided = true, have_exact = false;
+            double dl = S;
+            if (kz == 0) { accept = true; udrawn = false; have_exact = true; dl = 0.0; }
+            else if (c0 == 1 && S > Eb) { accept = true; udrawn = false; }
+            else if (c0 == 1) { accept = true; udrawn = true; }
+            else {   /* near a threshold: the exact log first */
+              decided = false;
+              if (S < -Eb) {
+                const double lu = sr_log_m(u, &tb);
+                udrawn = true;
+                if (S - Eb > lu) { accept = true; decided = true; }
+                else if (S + Eb < lu) { accept = false; decided = true; }
+              }
+            }
+            if (!decided || (accept && want_logl && !have_exact)) {   /* the exact sequential delta */
+              dl = sr_exact_delta(kind, q, K, sab, P, M, KT, hp, nh, hcnt, nhall, cbuf + xpar * KT * 64, ccnt + xpar * KT,
+                                  xs, lane, wave, TB);
+              xpar ^= 1;
+              if (!decided) {
+                if (tid == 0) misc[MS_NEXACT]++;
+                if (dl >= 0.) { accept = true; udrawn = false; }
+                else { udrawn = true; accept = dl > sr_log_m(u, &tb); }
+              }
+            }
+            if (!accept) continue;
+            delta = dl;
+            acc_p = p;
+            used = udrawn ? __builtin_amdgcn_readfirstlane(r[6]) : __builtin_amdgcn_readfirstlane(r[5]);
+            break;
+          }
+          STAMP(7);
+          if (acc_p < 0) {   /* all of p0..pend-1 rejected or vetoed, as hypothesised */
+            rng_skip(R, (uint32_t)__builtin_amdgcn_readfirstlane(pin[(pend - 1) * PI_STRIDE + 6]));
+            p0 = pend;
+            continue;
+          }
+          rng_skip(R, (uint32_t)used);
+          p0 = acc_p + 1;
+
+          /* ---- apply the accepted proposal acc_p */
+          const int kind = prop_kind(acc_p);
+          Prop q;
+          {
+            const int *r = pin + acc_p * PI_STRIDE;
+            q.i = __builtin_amdgcn_readfirstlane(r[0]);
+            q.j = __builtin_amdgcn_readfirstlane(r[1]);
+            q.ii = min(q.i, q.j); q.jj = max(q.i, q.j);
+            const int fl = __builtin_amdgcn_readfirstlane(r[2]);
+            q.inc1 = fl & 1; q.inc2 = (fl >> 1) & 1;
+            q.Kn = __builtin_amdgcn_readfirstlane(r[3]);
+            q.r0 = __builtin_amdgcn_readfirstlane(r[7]);
+          }
+          const int i = q.i, j = q.j, ii = q.ii, jj = q.jj, inc1 = q.inc1, inc2 = q.inc2, Kn = q.Kn;
+          if (tid == 0) misc[MS_ACC + (kind == PK_PI1 ? 3 : kind == PK_PI2 ? 4 : kind == PK_SWAP ? 5 : 6)]++;
+          loglik += delta;
+          const int16_t *nhp = nhall + q.r0;   /* pi3: the non-hard positions of [i, j] in order */
+          for (int m = tid; m < M; m += TB) {
+            uint32_t *Pm = P + m;
+            const int a = sab[m], b = sab[M + m];
+            int dt0, dt1;
+            taxon_dt(kind, q, a, b, Pm, M, hp, nh, hcnt, nhall, dt0, dt1);
+            scnt[m] += dt0; scnt[M + m] -= dt0; scnt[2 * M + m] += dt1; scnt[3 * M + m] -= dt1;
+            if (kind == PK_PI1) {                                  /* mcmc.c:1266-1297 */
+              if (i < j) {
+                if (ii < a && a <= jj + 1) sab[m] = a - 1;
+                if (ii < b && b <= jj + 1) sab[M + m] = b - 1;
+                const uint32_t vb = (Pm[(i >> 5) * M] >> (i & 31)) & 1u;
+                for (int w = i >> 5; w <= (j >> 5); ++w) {
+                  const uint32_t old = Pm[w * M];
+                  const uint32_t nxt = (w + 1 < NW) ? Pm[(w + 1) * M] : 0u;
+                  const uint32_t sh = (old >> 1) | (nxt << 31);
+                  const uint32_t m1 = range_mask(w, i, j - 1);
+                  uint32_t nw = (old & ~m1) | (sh & m1);
+                  if ((j >> 5) == w) nw = (nw & ~(1u << (j & 31))) | (vb << (j & 31));
+                  Pm[w * M] = nw;
+                }
+              } else {
+                if (ii <= a && a <= jj) sab[m] = a + 1;
+                if (ii <= b && b <= jj) sab[M + m] = b + 1;
+                const uint32_t vb = (Pm[(i >> 5) * M] >> (i & 31)) & 1u;
+                for (int w = i >> 5; w >= (j >> 5); --w) {
+                  const uint32_t old = Pm[w * M];
+                  const uint32_t prv = (w > 0) ? Pm[(w - 1) * M] : 0u;
+                  const uint32_t sh = (old << 1) | (prv >> 31);
+                  const uint32_t m1 = range_mask(w, j + 1, i);
+                  uint32_t nw = (old & ~m1) | (sh & m1);
+                  if ((j >> 5) == w) nw = (nw & ~(1u << (j & 31))) | (vb << (j & 31));
+                  Pm[w * M] = nw;
+                }
+              }
+            } else {                                               /* mcmc.c:1446-1474, 1641-1670 */
               const int ain = ininterval(a, i, j + 1, inc1, inc2);
               const int bin = ininterval(b, i, j + 1, inc1, inc2);
-              if (ain && !bin) {
-                int O1, O2;
-                ones_split(Pm, M, i, a, j + 1, O1, O2);
-                const int Z1 = (a - i) - O1, Z2 = (j + 1 - a) - O2;
-                dt1 = O1 - O2; df1 = -O1 + O2; dt0 = -Z1 + Z2; df0 = Z1 - Z2;
-              } else if (!ain && bin) {
-                int O1, O2;
-                ones_split(Pm, M, i, b, j + 1, O1, O2);
-                const int Z1 = (b - i) - O1, Z2 = (j + 1 - b) - O2;
-                dt1 = -O1 + O2; df1 = O1 - O2; dt0 = Z1 - Z2; df0 = -Z1 + Z2;
-              }
-            } else {                                           /* mcmc.c:1568-1631 */
-              const int ain = ininterval(a, i, j + 1, inc1, inc2);
-              const int bin = ininterval(b, i, j + 1, inc1, inc2);
-              int na, nb;
-              if (ain && !bin) { na = i + j + 1 - a; nb = b; }
-              else if (!ain && bin) { na = a; nb = i + j + 1 - b; }
-              else if (ain && bin) { na = i + j + 1 - b; nb = i + j + 1 - a; }
-              else { na = a; nb = b; }
-              /* by words: was-alive = [a,b) n [i,j]; is-alive after the move (the site at n
-                 goes to p[n]) = hard positions in [na,nb) plus the non-hard positions whose
-                 mirrored rank lands in [na,nb): ranks [Kn-s_hi, Kn-s_lo) */
-              const int xa = min(max(na, i), j + 1), xb = min(max(nb, i), j + 1);
-              const int s_lo = (xa - i) - hard_count(hp, nh, i, xa - 1);
-              const int s_hi = (xb - i) - hard_count(hp, nh, i, xb - 1);
-              int pl = 1, ph = 0;
-              if (s_lo < s_hi) { pl = nhpos[Kn - s_hi]; ph = nhpos[Kn - s_lo - 1]; }
-              for (int w = i >> 5; w <= (j >> 5); ++w) {
-                const uint32_t rng = range_mask(w, i, j);
-                const uint32_t H = Hb[w];
-                const uint32_t Wm = range_mask(w, max(a, i), min(b - 1, j)) & rng;
-                const uint32_t Im = ((range_mask(w, pl, ph) & ~H) | (range_mask(w, max(na, i), min(nb - 1, j)) & H)) & rng;
-                const uint32_t dying = Wm & ~Im, born = Im & ~Wm;
-                const uint32_t col = Pm[w * M];
-                const int od = __popc(col & dying), zd = __popc(dying) - od;
-                const int ob = __popc(col & born), zb = __popc(born) - ob;
-                dt1 += ob - od; df1 += od - ob; dt0 += zd - zb; df0 += zb - zd;
+              if (ain && !bin) sab[m] = i + j + 1 - a;
+              else if (!ain && bin) sab[M + m] = i + j + 1 - b;
+              else if (ain && bin) { sab[M + m] = i + j + 1 - a; sab[m] = i + j + 1 - b; }
+              if (kind != PK_PI3) {
+                for (int n = i; n < i + j - n; ++n) {
+                  const int p2 = i + j - n;
+                  const uint32_t b1 = (Pm[(n >> 5) * M] >> (n & 31)) & 1u, b2 = (Pm[(p2 >> 5) * M] >> (p2 & 31)) & 1u;
+                  if (b1 != b2) { Pm[(n >> 5) * M] ^= (1u << (n & 31)); Pm[(p2 >> 5) * M] ^= (1u << (p2 & 31)); }
+                }
+              } else {
+                for (int r = 0; r < Kn - 1 - r; ++r) {
+                  const int n = nhp[r], p2 = nhp[Kn - 1 - r];
+                  const uint32_t b1 = (Pm[(n >> 5) * M] >> (n & 31)) & 1u, b2 = (Pm[(p2 >> 5) * M] >> (p2 & 31)) & 1u;
+                  if (b1 != b2) { Pm[(n >> 5) * M] ^= (1u << (n & 31)); Pm[(p2 >> 5) * M] ^= (1u << (p2 & 31)); }
+                }
               }
             }
           }
-          const double tv = (m < M) ? qval(dt0, df0, dt1, df1, K) : 0.0;
-          const uint64_t msk = __ballot(tv != 0.0);
-          const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
-          if (tv != 0.0) cb[ch * 64 + pos] = tv;
-          if (lane == 0) cc[ch] = __popcll(msk);
-          Kt += __popcll(msk);
-          tsum += tv;
-          tabs_ += __builtin_fabs(tv);
-          sd[ch * 64 + lane] = dt0; sd[(KT + ch) * 64 + lane] = df0;
-          sd[(2 * KT + ch) * 64 + lane] = dt1; sd[(3 * KT + ch) * 64 + lane] = df1;
-        }
-        for (int off = 32; off > 0; off >>= 1) {
-          tsum += __shfl_xor(tsum, off);
-          tabs_ += __shfl_xor(tabs_, off);
-        }
-        {
-          double *pw = part + (par * NWV + wave) * 4;
-          if (lane == 0) { pw[0] = tsum; pw[1] = tabs_; pw[2] = (double)Kt; }
-        }
-        STAMP(4);
-        __syncthreads();
-        /* ---- certified MH decision (mcmc.c:1261 / 1441 / 1636), identical in every thread.
-           S = tree sum of the terms, A = sum |t|, Kt = #nonzero: |sequential delta - S| <=
-           2 Kt 2^-53 A (1+eps), so E = (Kt + 64) 2^-52 A decides "delta >= 0" and "delta > log u"
-           unless the true value is within E; then (and whenever the exact delta feeds a saved
-           loglik) the exact sequential sum runs.  uniform_pos is drawn only once delta < 0 is known. */
-        double S = 0.0, Aabs = 0.0, Ktd = 0.0;
+          /* rpi (double-buffered full permutation, read only at save time) and hard positions */
+          {
+            const int32_t *ro = rcur ? rpiB : rpiA;
+            int32_t *rn = rcur ? rpiA : rpiB;
+            if (kind == PK_PI1) {
+              for (int n = tid; n < N; n += TB) {
+                int src = n;
+                if (i < j) { if (n >= i && n < j) src = n + 1; else if (n == j) src = i; }
+                else { if (n > j && n <= i) src = n - 1; else if (n == j) src = i; }
+                rn[n] = ro[src];
+              }
 #pragma unroll
-        for (int w = 0; w < NWV; ++w) {
-          const double *pw = part + (par * NWV + w) * 4;
-          S += pw[0]; Aabs += pw[1]; Ktd += pw[2];
-        }
-        const double Eb = (Ktd + 64.0) * 0x1p-52 * Aabs;
-        double delta = S, lu = 0.0;
-        bool have_exact = false, drew = false;
-        int state;   /* 0 reject, 1 accept, 2 undecided */
-        if (Ktd == 0.0) { have_exact = true; delta = 0.0; state = 1; }
-        else if (S > Eb) state = 1;
-        else if (S < -Eb) {
-          lu = sr_log_m(rng_uniform_pos<false>(R, tid, TB), &tb);
-          drew = true;
-          state = (S - Eb > lu) ? 1 : ((S + Eb < lu) ? 0 : 2);
-        } else state = 2;
-        if (state == 2) {
-          delta = exact_sum_wave(cb, cc, KT, xs, lane);
-          have_exact = true;
-          if (tid == 0) misc[MS_NEXACT]++;
-          if (delta >= 0.) state = 1;
-          else {
-            if (!drew) lu = sr_log_m(rng_uniform_pos<false>(R, tid, TB), &tb);
-            state = (delta > lu) ? 1 : 0;
-          }
-        }
-        par ^= 1;
-        STAMP(5);
-        if (state == 0) continue;
-        if (want_logl && !have_exact) delta = exact_sum_wave(cb, cc, KT, xs, lane);
-        if (tid == 0) misc[MS_ACC + (kind == 1 ? 3 : kind == 20 ? 4 : kind == 21 ? 5 : 6)]++;
-        loglik += delta;
-        /* ---- apply to own taxa: limits, counts, columns */
-        for (int m0 = wave * 64; m0 < KT * 64; m0 += TB) {
-          const int ch = m0 >> 6, m = m0 + lane;
-          if (m >= M) continue;
-          uint32_t *Pm = P + m;
-          const int a = sab[m], b = sab[M + m];
-          scnt[m] += sd[ch * 64 + lane];
-          scnt[M + m] += sd[(KT + ch) * 64 + lane];
-          scnt[2 * M + m] += sd[(2 * KT + ch) * 64 + lane];
-          scnt[3 * M + m] += sd[(3 * KT + ch) * 64 + lane];
-          if (kind == 1) {                                     /* mcmc.c:1266-1297 */
-            if (i < j) {
-              if (ii < a && a <= jj + 1) sab[m] = a - 1;
-              if (ii < b && b <= jj + 1) sab[M + m] = b - 1;
-              const uint32_t vb = (Pm[(i >> 5) * M] >> (i & 31)) & 1u;
-              for (int w = i >> 5; w <= (j >> 5); ++w) {
-                const uint32_t old = Pm[w * M];
-                const uint32_t nxt = (w + 1 < NW) ? Pm[(w + 1) * M] : 0u;
-                const uint32_t sh = (old >> 1) | (nxt << 31);
-                const uint32_t m1 = range_mask(w, i, j - 1);
-                uint32_t nw = (old & ~m1) | (sh & m1);
-                if ((j >> 5) == w) nw = (nw & ~(1u << (j & 31))) | (vb << (j & 31));
-                Pm[w * M] = nw;
+              for (int k = 0; k < SR_NHMAX; ++k) {
+                if (k >= nh) break;
+                const int h = hp[k];
+                if (h == i) hp[k] = j;
+                else if (i < j && h > i && h <= j) hp[k] = h - 1;
+                else if (i > j && h >= j && h < i) hp[k] = h + 1;
+              }
+            } else if (kind != PK_PI3) {
+              for (int n = tid; n < N; n += TB) rn[n] = ro[(n >= i && n <= j) ? (i + j - n) : n];
+#pragma unroll
+              for (int k = 0; k < SR_NHMAX; ++k) {
+                if (k >= nh) break;
+                if (hp[k] >= i && hp[k] <= j) hp[k] = i + j - hp[k];
               }
             } else {
-              if (ii <= a && a <= jj) sab[m] = a + 1;
-              if (ii <= b && b <= jj) sab[M + m] = b + 1;
-              const uint32_t vb = (Pm[(i >> 5) * M] >> (i & 31)) & 1u;
-              for (int w = i >> 5; w >= (j >> 5); --w) {
-                const uint32_t old = Pm[w * M];
-                const uint32_t prv = (w > 0) ? Pm[(w - 1) * M] : 0u;
-                const uint32_t sh = (old << 1) | (prv >> 31);
-                const uint32_t m1 = range_mask(w, j + 1, i);
-                uint32_t nw = (old & ~m1) | (sh & m1);
-                if ((j >> 5) == w) nw = (nw & ~(1u << (j & 31))) | (vb << (j & 31));
-                Pm[w * M] = nw;
-              }
+              for (int n = tid; n < N; n += TB)
+                if (n < i || n > j || hcnt[n + 1] != hcnt[n]) rn[n] = ro[n];
+              for (int r = tid; r < Kn; r += TB) rn[nhp[r]] = ro[nhp[Kn - 1 - r]];
             }
-          } else {                                             /* mcmc.c:1446-1474, 1641-1670 */
-            const int ain = ininterval(a, i, j + 1, inc1, inc2);
-            const int bin = ininterval(b, i, j + 1, inc1, inc2);
-            if (ain && !bin) sab[m] = i + j + 1 - a;
-            else if (!ain && bin) sab[M + m] = i + j + 1 - b;
-            else if (ain && bin) { sab[M + m] = i + j + 1 - a; sab[m] = i + j + 1 - b; }
-            if (kind != 3) {
-              for (int n = i; n < i + j - n; ++n) {
-                const int p2 = i + j - n;
-                const uint32_t b1 = (Pm[(n >> 5) * M] >> (n & 31)) & 1u, b2 = (Pm[(p2 >> 5) * M] >> (p2 & 31)) & 1u;
-                if (b1 != b2) { Pm[(n >> 5) * M] ^= (1u << (n & 31)); Pm[(p2 >> 5) * M] ^= (1u << (p2 & 31)); }
-              }
-            } else {
-              for (int r = 0; r < Kn - 1 - r; ++r) {
-                const int n = nhpos[r], p2 = nhpos[Kn - 1 - r];
-                const uint32_t b1 = (Pm[(n >> 5) * M] >> (n & 31)) & 1u, b2 = (Pm[(p2 >> 5) * M] >> (p2 & 31)) & 1u;
-                if (b1 != b2) { Pm[(n >> 5) * M] ^= (1u << (n & 31)); Pm[(p2 >> 5) * M] ^= (1u << (p2 & 31)); }
-              }
-            }
+            rcur ^= 1;
           }
-        }
-        /* ---- rpi (double-buffered full permutation, read only at save time) and hard positions */
-        {
-          const int32_t *ro = rcur ? rpiB : rpiA;
-          int32_t *rn = rcur ? rpiA : rpiB;
-          if (kind == 1) {
-            for (int n = tid; n < N; n += TB) {
-              int src = n;
-              if (i < j) { if (n >= i && n < j) src = n + 1; else if (n == j) src = i; }
-              else { if (n > j && n <= i) src = n - 1; else if (n == j) src = i; }
-              rn[n] = ro[src];
-            }
-#pragma unroll
-            for (int q = 0; q < SR_NHMAX; ++q) {
-              if (q >= nh) break;
-              const int h = hp[q];
-              if (h == i) hp[q] = j;
-              else if (i < j && h > i && h <= j) hp[q] = h - 1;
-              else if (i > j && h >= j && h < i) hp[q] = h + 1;
-            }
-          } else if (kind != 3) {
-            for (int n = tid; n < N; n += TB) rn[n] = ro[(n >= i && n <= j) ? (i + j - n) : n];
-#pragma unroll
-            for (int q = 0; q < SR_NHMAX; ++q) {
-              if (q >= nh) break;
-              if (hp[q] >= i && hp[q] <= j) hp[q] = i + j - hp[q];
-            }
-          } else {
-            for (int n = tid; n < N; n += TB)
-              if (n < i || n > j || is_hard(hp, nh, n)) rn[n] = ro[n];
-            for (int r = tid; r < Kn; r += TB) rn[nhpos[r]] = ro[nhpos[Kn - 1 - r]];   /* own wave's full copy */
-          }
-          rcur ^= 1;
-        }
-        STAMP(6);
-      } /* proposals */
-      STAMP(6);
+          if (kind != PK_PI3) build_hard_tables(hp, nh, N, hcnt, nhall, lane);   /* hard sites may have moved */
+          wsync();
+          STAMP(7);
+        } /* batches */
+      }
+      STAMP(7);
       __syncthreads();
     } /* sweeps */
 
@@ -1222,7 +1400,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   STAMP(7);
   STAMP_STORE(A.dbg);
 #ifdef SR_STAMPS
-  if (tid == 0) { A.dbg[blockIdx.x * 17 * 8 + 0] += misc[MS_NEXACT]; for (int q_ = 0; q_ < 4; ++q_) A.dbg[blockIdx.x * 17 * 8 + 1 + q_] += misc[MS_FBK + q_]; }
+  if (tid == 0) { A.dbg[blockIdx.x * 17 * 8 + 0] += misc[MS_NEXACT]; for (int q_ = 0; q_ < 4; ++q_) A.dbg[blockIdx.x * 17 * 8 + 1 + q_] += misc[MS_FBK + q_];
+                  for (int q_ = 0; q_ < 3; ++q_) A.dbg[blockIdx.x * 17 * 8 + 5 + q_] += misc[40 + q_]; }
 #endif
   __syncthreads();
   uint32_t *oP = A.P + (size_t)chain * NW * M;

@@ -335,7 +335,8 @@ SR_API int sr_session_create(const sr_dataset *ds, const sr_chain_spec *specs, i
   if (opts) o = *opts; else sr_default_opts(&o);
   if (o.sweeps_per_call <= 0) return SR_EINVAL;
   if (o.manycd != 0) return SR_EUNSUPPORTED;
-  if (ds->nh > SR_NHMAX || ds->N > 32767 || ds->M > 32767) return SR_EUNSUPPORTED;
+  /* nh <= 32 hard sites (register-held), N <= 2048 (a wave holds the hard bitmap, one word per lane) */
+  if (ds->nh > SR_NHMAX || ds->N > 2048 || ds->M > 32767) return SR_EUNSUPPORTED;
   sr_session *s = (sr_session *)calloc(1, sizeof(*s));
   if (!s) return SR_ENOMEM;
   s->ds.N = ds->N; s->ds.M = ds->M; s->ds.nh = ds->nh;

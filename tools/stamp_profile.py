@@ -13,7 +13,7 @@ sys.path.insert(0, os.path.join(ROOT, "seriation-in-paleontological-data-using-m
 import numpy as np  # noqa: E402
 import seriation_amd as sa  # noqa: E402
 
-PH = ["totals+c,d", "sampleab", "logl", "prop draw/veto/decide", "prop terms", "ordered sum", "apply", "tail"]
+PH = ["totals+c,d", "sampleab", "logl", "prop draws", "terms pi1", "terms pi2/swap", "terms pi3", "decide/apply/tail"]
 path = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "tests/golden/datasets/synth_256x512.txt")
 C = int(sys.argv[2]) if len(sys.argv) > 2 else 100
 calls = int(sys.argv[3]) if len(sys.argv) > 3 else 10
@@ -41,3 +41,6 @@ print("  total wave0 %.0f; exact-sum fallbacks/sweep %.3f; sampleab fallbacks/sw
     out[:, 0, 1].astype(np.float64).mean() / 2 / sweeps))
 print("  sampleab fallback reasons/sweep: prev %.3f here %.3f S0 %.3f (rest = no crossing in segment)" % tuple(
     out[:, 0, 2 + q].astype(np.float64).mean() / 2 / sweeps for q in range(3)))
+ev = out[:, 0, 5:8].astype(np.float64).mean(0) / 2 / sweeps
+print("  term evaluations/sweep: pi1 %.2f pi2/swap %.2f pi3 %.2f" % tuple(ev))
+print("  cycles per evaluation (wave-mean): pi1 %.0f pi2/swap %.0f pi3 %.0f" % tuple(per[:, :, 4 + k].mean() / max(ev[k], 1e-9) for k in range(3)))

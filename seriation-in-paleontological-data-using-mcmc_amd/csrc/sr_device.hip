@@ -62,7 +62,7 @@ struct KArgs {
 
 /* ---------------------------------------------------------------- LDS carve */
 struct Lay {
-  size_t tab, cbuf, lbuf, mt, P, rpi0, rpi1, ht, ck, ccnt, sab, scnt, pinfo, part, tot, xs, misc, total;
+  size_t tab, cbuf, lbuf, mt, P, rpi0, rpi1, ht, ck, ccnt, sab, scnt, hpw, part, tot, xs, misc, total;
 };
 __host__ __device__ static inline size_t sr_al16(size_t x) { return (x + 15) & ~(size_t)15; }
 /* Gibbs checkpoint slots per word: one per thread that owns a taxon */
@@ -84,7 +84,7 @@ __host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB)
   L.ccnt = o;  o = sr_al16(o + (size_t)2 * KT * 4);
   L.sab = o;   o = sr_al16(o + (size_t)2 * M * 4);
   L.scnt = o;  o = sr_al16(o + (size_t)4 * M * 4);
-  L.pinfo = o; o = sr_al16(o + (size_t)NWV * 16 * 8 * 4);             /* per wave: drawn proposals */
+  L.hpw = o;   o = sr_al16(o + (size_t)NWV * SR_NHMAX * 4);           /* per wave: hard positions */
   L.part = o;  o = sr_al16(o + (size_t)2 * 16 * NWV * 8 * 4);         /* [2][proposal][wave] count sums */
   L.tot = o;   o = sr_al16(o + (size_t)2 * NWV * 4 * 4);               /* [2][wave] t0, f0, t1, f1 */
   L.xs = o;    o = sr_al16(o + (size_t)NWV * sizeof(double));          /* per-wave broadcast slot */
@@ -249,6 +249,24 @@ __device__ __forceinline__ uint32_t udiv_word(uint32_t g, const UDiv &u)
   if (qs > g) q--;
   else if (g - (uint32_t)qs >= u.scale) q++;
   return q;
+}
+
+/* gsl_rng_uniform_int's quotient g / scale by an invariant-divisor multiply (Hacker's Delight
+ * round-up method, exact for every 32-bit g; scale >= 2 here since n <= 2048): scalar ALU only */
+struct UDivM { uint32_t n, m; int l; };
+__device__ __forceinline__ UDivM make_udivm(uint32_t n)
+{
+  UDivM u;
+  const uint32_t d = 0xffffffffu / n;
+  u.n = n;
+  u.l = 32 - __builtin_clz(d - 1);
+  u.m = (uint32_t)(((((uint64_t)1) << 32) * ((((uint64_t)1) << u.l) - d)) / d + 1);
+  return u;
+}
+__device__ __forceinline__ uint32_t udivm(uint32_t g, const UDivM &u)
+{
+  const uint32_t t = __umulhi(u.m, g);
+  return (t + ((g - t) >> 1)) >> (u.l - 1);
 }
 
 /* the next 8 tempered words from the cursor, loaded together, if they are resident (the ring
@@ -645,22 +663,14 @@ __device__ __forceinline__ int ininterval(int i, int a, int b, int inc1, int inc
 __device__ __forceinline__ int hard_count(const int *hp, int nh, int lo, int hi)
 {
   int s = 0;
-#pragma unroll
-  for (int k = 0; k < SR_NHMAX; ++k) {
-    if (k >= nh) break;
-    s += (hp[k] >= lo && hp[k] <= hi) ? 1 : 0;
-  }
+  for (int k = 0; k < nh; ++k) s += (hp[k] >= lo && hp[k] <= hi) ? 1 : 0;
   return s;
 }
 
 __device__ __forceinline__ bool is_hard(const int *hp, int nh, int p)
 {
   bool h = false;
-#pragma unroll
-  for (int k = 0; k < SR_NHMAX; ++k) {
-    if (k >= nh) break;
-    h |= (hp[k] == p);
-  }
+  for (int k = 0; k < nh; ++k) h |= (hp[k] == p);
   return h;
 }
 
@@ -737,11 +747,7 @@ __device__ __forceinline__ void build_hard_tables(const int *hp, int nh, int N, 
   for (int x0 = 0; x0 <= N; x0 += 64) {
     const int x = x0 + lane;
     bool h = false;
-#pragma unroll
-    for (int k = 0; k < SR_NHMAX; ++k) {
-      if (k >= nh) break;
-      h |= (hp[k] == x);
-    }
+    for (int k = 0; k < nh; ++k) h |= (hp[k] == x);
     const uint64_t msk = __ballot(h && x < N);
     const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
     if (x <= N) hcnt[x] = (int16_t)(base + below);
@@ -754,8 +760,19 @@ __device__ __forceinline__ void build_hard_tables(const int *hp, int nh, int N, 
 /* Count changes of one taxon (limits a, b; position-ordered column Pm) under proposal q:
  * dt0 (zeros inside), dt1 (ones inside); the reference's df0 = -dt0 and df1 = -dt1 always
  * (mcmc.c:1175-1256 pi1, 1367-1436 pi2, 1568-1631 pi3).  hcnt/nhall: the wave's hard-site tables. */
+/* column bits at the hard positions, bit k = hard site k (input of the pi3 count change) */
+__device__ __forceinline__ uint32_t hard_bits_col(const uint32_t *Pm, int M, const int *hp, int nh)
+{
+  uint32_t hbm = 0;
+  for (int k = 0; k < nh; ++k) {
+    const int h = __builtin_amdgcn_readfirstlane(hp[k]);
+    hbm |= ((Pm[(h >> 5) * M] >> (h & 31)) & 1u) << k;
+  }
+  return hbm;
+}
+
 __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, const uint32_t *Pm, int M,
-                                         const int *hp, int nh, const int16_t *hcnt, const int16_t *nhall, int &dt0, int &dt1)
+                                         uint32_t hbm, const int16_t *hcnt, const int16_t *nhall, int &dt0, int &dt1)
 {
   const int i = q.i, j = q.j;
   dt0 = 0; dt1 = 0;
@@ -797,13 +814,6 @@ __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, 
     const int xa = min(max(na, i), j + 1), xb = min(max(nb, i), j + 1);
     const int ri = q.r0;                                   /* = i - hcnt[i] */
     const int s_lo = (xa - hcnt[xa]) - ri, s_hi = (xb - hcnt[xb]) - ri;
-    /* column bits at the hard positions, bit k = hard site k */
-    uint32_t hbm = 0;
-#pragma unroll
-    for (int k = 0; k < SR_NHMAX; ++k) {
-      if (k >= nh) break;
-      hbm |= ((Pm[(hp[k] >> 5) * M] >> (hp[k] & 31)) & 1u) << k;
-    }
     auto hard_ones = [&](int lo, int hi, int &cnt) -> int {   /* hard positions in [lo, hi] */
       if (hi < lo) { cnt = 0; return 0; }
       const int kl = hcnt[lo], kh = hcnt[hi + 1];
@@ -833,9 +843,6 @@ __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, 
   }
 }
 
-/* pinfo record (ints): i, j, flags (bit0 inc1, bit1 inc2, bit2 veto), Kn, uniform word, words
- * consumed through the draws, words consumed through the uniform_pos draw */
-#define PI_STRIDE 8
 
 /* The exact delta of one proposal: the reference's per-taxon terms (qval, mcmc.c:1214,
  * 1435, 1630 term order) compacted per 64-taxon chunk into cb, then summed sequentially in
@@ -847,7 +854,8 @@ __device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const i
   for (int m0 = wave * 64; m0 < KT * 64; m0 += TB) {
     const int ch = m0 >> 6, m = m0 + lane;
     int dt0 = 0, dt1 = 0;
-    if (m < M) taxon_dt(kind, q, sab[m], sab[M + m], P + m, M, hp, nh, hcnt, nhall, dt0, dt1);
+    if (m < M) taxon_dt(kind, q, sab[m], sab[M + m], P + m, M, kind == PK_PI3 ? hard_bits_col(P + m, M, hp, nh) : 0u,
+                        hcnt, nhall, dt0, dt1);
     const double tv = (m < M) ? qval(dt0, -dt0, dt1, -dt1, K) : 0.0;
     const uint64_t msk = __ballot(tv != 0.0);
     const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
@@ -896,7 +904,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   int *ccnt = (int *)(smem + L.ccnt);
   int32_t *sab = (int32_t *)(smem + L.sab);     /* a[M], b[M] */
   int32_t *scnt = (int32_t *)(smem + L.scnt);   /* t0[M], f0[M], t1[M], f1[M] */
-  int *pinfo = (int *)(smem + L.pinfo);
+  int *hp = (int *)(smem + L.hpw) + wave * SR_NHMAX;   /* this wave's copy of the hard positions */
   int *part = (int *)(smem + L.part);
   int *tot = (int *)(smem + L.tot);
   double *xs = (double *)(smem + L.xs) + wave;
@@ -926,9 +934,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   }
   if (tid == 0) for (int q = MS_CAB; q < 64; ++q) misc[q] = 0;
 
-  int hp[SR_NHMAX];
-#pragma unroll
-  for (int k = 0; k < SR_NHMAX; ++k) hp[k] = (k < nh) ? A.hp[(size_t)chain * SR_NHMAX + k] : -1;
+  if (lane < SR_NHMAX) hp[lane] = (lane < nh) ? A.hp[(size_t)chain * SR_NHMAX + lane] : -1;
+  wsync();
   double c = A.cdl[(size_t)chain * 4 + 0];
   double d = A.cdl[(size_t)chain * 4 + 1];
   double loglik = A.cdl[(size_t)chain * 4 + 2];   /* identical in every thread */
@@ -951,9 +958,9 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   build_hard_tables(hp, nh, N, hcnt, nhall, lane);
   const double ec = sr_exp_m(SR_LOGEPSILON, &tb);
   const uint32_t nhard = (uint32_t)nh;
-  const UDiv udN = make_udiv((uint32_t)N), udN1 = make_udiv((uint32_t)(N - 1)), ud2 = make_udiv(2u);
-  const UDiv udH = make_udiv((uint32_t)N - nhard > 0 ? (uint32_t)N - nhard : 1u);
-  const UDiv udH1 = make_udiv((uint32_t)N - nhard > 1 ? (uint32_t)N - nhard - 1 : 1u);
+  const UDivM mdN = make_udivm((uint32_t)N), mdN1 = make_udivm((uint32_t)(N - 1)), md2 = make_udivm(2u);
+  const UDivM mdH = make_udivm((uint32_t)N - nhard > 0 ? (uint32_t)N - nhard : 1u);
+  const UDivM mdH1 = make_udivm((uint32_t)N - nhard > 1 ? (uint32_t)N - nhard - 1 : 1u);
   STAMP_DECL
 
   for (int call = 0; call < A.calls; ++call) {
@@ -1050,56 +1057,74 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
          one that is accepted (or needs the exact delta) ends the batch: it is applied with the
          cursor it really consumed, and the proposals after it are re-batched. */
       if (!(SR_EXP & 1)) {
+        int vi = 0, vj = 0, vfl = 4, vkn = 0, vuw = 1, vnd = 0, voff = 0, vr0 = 0;   /* lane p: proposal p */
         int p0 = 0;
         while (p0 < 16) {
-          /* ---- draws of proposals p0.. under the hypothesis (identical in every thread) */
-          int *pin = pinfo + wave * 16 * PI_STRIDE;
-          const int avail = (int)((R.gen - R.blk) * SR_MT_N - R.off);   /* resident words */
-          const uint32_t base = (R.blk & (SR_RING - 1)) * SR_MT_N + R.off;
+          p0 = __builtin_amdgcn_readfirstlane(p0);   /* block-uniform: keep the control flow scalar */
+          /* ---- draws of proposals p0.. under the hypothesis: block-uniform scalar code; the
+             record of proposal p lives in lane p of the v* registers */
+          const uint32_t rblk = __builtin_amdgcn_readfirstlane(R.blk), roff = __builtin_amdgcn_readfirstlane(R.off);
+          const uint32_t rgen = __builtin_amdgcn_readfirstlane(R.gen);
+          const int avail = min((int)((rgen - rblk) * SR_MT_N - roff), 128);   /* resident words, <= 2 per lane */
+          const uint32_t base = (rblk & (SR_RING - 1)) * SR_MT_N + roff;
+          /* the batch's next 128 tempered words: word k in lane k & 63 of vw[k >> 6] */
+          uint32_t vw0, vw1;
+          {
+            uint32_t i0 = base + (uint32_t)lane, i1 = base + 64u + (uint32_t)lane;
+            i0 = (i0 >= SR_RING * SR_MT_N) ? i0 - SR_RING * SR_MT_N : i0;
+            i1 = (i1 >= SR_RING * SR_MT_N) ? i1 - SR_RING * SR_MT_N : i1;
+            i1 = (i1 >= SR_RING * SR_MT_N) ? i1 - SR_RING * SR_MT_N : i1;
+            vw0 = sr_mt_temper(ring[i0]);
+            vw1 = sr_mt_temper(ring[i1]);
+          }
           int off = 0, pend = p0;
           for (int p = p0; p < 16; ++p) {
+            if (p0 == 0 && p == 1) break;   /* the swap (accepted ~40 %) forms its own batch */
             const int kind = prop_kind(p);
             bool bad = false;
             auto word = [&](void) -> uint32_t {
               if (off >= avail) { bad = true; return 0u; }
-              uint32_t idx = base + (uint32_t)off++;
-              idx = (idx >= SR_RING * SR_MT_N) ? idx - SR_RING * SR_MT_N : idx;
-              return sr_mt_temper(ring[idx]);
+              const int k = off++;
+              return (uint32_t)__builtin_amdgcn_readlane((int)(k < 64 ? vw0 : vw1), k & 63);
             };
-            auto uint_draw = [&](const UDiv &u) -> int {   /* gsl_rng_uniform_int */
+            auto uint_draw = [&](const UDivM &u) -> int {   /* gsl_rng_uniform_int */
               uint32_t k;
-              do { k = udiv_word(word(), u); } while (!bad && k >= u.n);
+              do { k = udivm(word(), u); } while (!bad && k >= u.n);
               return (int)k;
             };
+            auto hc = [&](int x) -> int { return __builtin_amdgcn_readfirstlane((int)hcnt[x]); };
             int i = 0, j = 0, inc1 = 0, inc2 = 0, Kn = 0, r0 = 0;
             bool veto = false;
             if (kind == PK_PI1) {                                  /* mcmc.c:1133-1160 */
-              i = uint_draw(udN);
-              j = uint_draw(udN1);
+              i = uint_draw(mdN);
+              j = uint_draw(mdN1);
               if (j >= i) j++;
-              if (hcnt[i + 1] != hcnt[i] && hcnt[max(i, j) + 1] - hcnt[min(i, j)] > 1) veto = true;
+              if (!bad && hc(i + 1) != hc(i) && hc(max(i, j) + 1) - hc(min(i, j)) > 1) veto = true;
             } else if (kind == PK_PI2 || kind == PK_SWAP) {        /* mcmc.c:1317-1364 */
               if (kind == PK_PI2) {
-                i = uint_draw(udN);
-                j = uint_draw(udN1);
+                i = uint_draw(mdN);
+                j = uint_draw(mdN1);
                 if (j >= i) j++;
                 else { const int t = i; i = j; j = t; }
               } else {
-                i = uint_draw(udN1);
+                i = uint_draw(mdN1);
                 j = i + 1;
               }
-              if (hcnt[j + 1] - hcnt[i] > 1) veto = true;
-              if (!veto) { inc1 = uint_draw(ud2); inc2 = uint_draw(ud2); }
+              if (!bad && hc(j + 1) - hc(i) > 1) veto = true;
+              if (!veto) { inc1 = uint_draw(md2); inc2 = uint_draw(md2); }
             } else {                                               /* mcmc.c:1495-1565 */
               if ((uint32_t)N - nhard < 2) veto = true;
               else {
-                const int n0 = uint_draw(udH), m0 = uint_draw(udH1);
-                inc1 = uint_draw(ud2);
-                inc2 = uint_draw(ud2);
+                const int n0 = uint_draw(mdH), m0 = uint_draw(mdH1);
+                inc1 = uint_draw(md2);
+                inc2 = uint_draw(md2);
                 /* non-hard ranks -> positions (mcmc.c:1505-1533) */
                 int ri, rj;
                 if (n0 <= m0) { ri = n0; rj = m0 + 1; } else { ri = m0; rj = n0; }
-                if (!bad) { i = nhall[ri]; j = nhall[rj]; }
+                if (!bad) {
+                  i = __builtin_amdgcn_readfirstlane((int)nhall[ri]);
+                  j = __builtin_amdgcn_readfirstlane((int)nhall[rj]);
+                }
                 Kn = rj - ri + 1;
                 r0 = ri;
               }
@@ -1108,43 +1133,58 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             uint32_t uw = 0;
             if (!veto) { do { uw = word(); } while (!bad && uw == 0u); }   /* gsl_rng_uniform_pos */
             if (bad) break;
-            if (lane == 0) {
-              int *r = pin + p * PI_STRIDE;
-              r[0] = i; r[1] = j; r[2] = inc1 | (inc2 << 1) | (veto ? 4 : 0); r[3] = Kn;
-              r[4] = (int)uw; r[5] = nd; r[6] = off; r[7] = r0;
-            }
+            vi = (lane == p) ? (i) : vi;
+            vj = (lane == p) ? (j) : vj;
+            vfl = (lane == p) ? (inc1 | (inc2 << 1) | (veto ? 4 : 0)) : vfl;
+            vkn = (lane == p) ? (Kn) : vkn;
+            vuw = (lane == p) ? ((int)uw) : vuw;
+            vnd = (lane == p) ? (nd) : vnd;
+            voff = (lane == p) ? (off) : voff;
+            vr0 = (lane == p) ? (r0) : vr0;
             pend = p + 1;
           }
+          pend = __builtin_amdgcn_readfirstlane(pend);
           if (pend == p0) {   /* not enough resident words for one proposal: make more, retry */
             rng_ensure(R, min(avail + 256, (SR_RING - 1) * SR_MT_N - (SR_MT_N - 1)), tid, TB);
             continue;
           }
-          wsync();
+          auto load_prop = [&](int p) -> Prop {
+            Prop q;
+            q.i = __builtin_amdgcn_readlane(vi, p);
+            q.j = __builtin_amdgcn_readlane(vj, p);
+            q.ii = min(q.i, q.j); q.jj = max(q.i, q.j);
+            const int fl = __builtin_amdgcn_readlane(vfl, p);
+            q.inc1 = fl & 1; q.inc2 = (fl >> 1) & 1;
+            q.Kn = __builtin_amdgcn_readlane(vkn, p);
+            q.r0 = __builtin_amdgcn_readlane(vr0, p);
+            return q;
+          };
 
           /* ---- exact integer count sums of every drawn proposal over own taxa, per wave */
           int *pw = part + (bpar * 16) * NWV * 8;
           const bool pack = N * ((M + TB - 1) / TB) < 512;   /* per-wave sums fit 16-bit fields */
+          /* own taxon's limits and hard-site bits, fixed for the batch (one taxon per thread) */
+          const bool one = M <= TB;
+          int a1 = 0, b1 = 0;
+          uint32_t hb1 = 0;
+          if (one && tid < M) { a1 = sab[tid]; b1 = sab[M + tid]; hb1 = hard_bits_col(P + tid, M, hp, nh); }
           STAMP(3);
           for (int p = p0; p < pend; ++p) {
-            const int *r = pin + p * PI_STRIDE;
-            const int fl = __builtin_amdgcn_readfirstlane(r[2]);
-            if (fl & 4) continue;
+            if (__builtin_amdgcn_readlane(vfl, p) & 4) continue;
 #ifdef SR_STAMPS
             if (tid == 0) misc[40 + (prop_kind(p) == PK_PI1 ? 0 : prop_kind(p) == PK_PI3 ? 2 : 1)]++;
 #endif
             const int kind = prop_kind(p);
-            Prop q;
-            q.i = __builtin_amdgcn_readfirstlane(r[0]);
-            q.j = __builtin_amdgcn_readfirstlane(r[1]);
-            q.ii = min(q.i, q.j); q.jj = max(q.i, q.j);
-            q.inc1 = fl & 1; q.inc2 = (fl >> 1) & 1;
-            q.Kn = __builtin_amdgcn_readfirstlane(r[3]);
-            q.r0 = __builtin_amdgcn_readfirstlane(r[7]);
+            const Prop q = load_prop(p);
             int x0 = 0, x1 = 0, y0 = 0, y1 = 0, nzc = 0;
             for (int m0 = wave * 64; m0 < M; m0 += TB) {
               const int m = m0 + lane;
               int dt0 = 0, dt1 = 0;
-              if (m < M) taxon_dt(kind, q, sab[m], sab[M + m], P + m, M, hp, nh, hcnt, nhall, dt0, dt1);
+              if (m < M) {
+                if (one) taxon_dt(kind, q, a1, b1, P + m, M, hb1, hcnt, nhall, dt0, dt1);
+                else taxon_dt(kind, q, sab[m], sab[M + m], P + m, M, kind == PK_PI3 ? hard_bits_col(P + m, M, hp, nh) : 0u,
+                              hcnt, nhall, dt0, dt1);
+              }
               x0 += dt0; x1 += dt1; y0 += abs(dt0); y1 += abs(dt1);
               nzc += __popcll(__ballot((dt0 | dt1) != 0));
             }
@@ -1165,7 +1205,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               int *o = pw + (p * NWV + wave) * 8;
               o[0] = X0; o[1] = X1; o[2] = Y0; o[3] = Y1; o[4] = nzc;
             }
-            STAMP(kind == PK_PI1 ? 4 : (kind == PK_PI3 ? 6 : 5));
+            if (kind == PK_PI1) STAMP(4); else if (kind == PK_PI3) STAMP(6); else STAMP(5);
           }
           __syncthreads();
 
@@ -1184,8 +1224,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           {
             const int p = lane;
             if (p >= p0 && p < pend) {
-              const int *r = pin + p * PI_STRIDE;
-              if (!(r[2] & 4)) {
+              if (!(vfl & 4)) {
                 int X0 = 0, X1 = 0, Y0 = 0, Y1 = 0;
 #pragma unroll
                 for (int w = 0; w < NWV; ++w) {
@@ -1195,7 +1234,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 Sp = ((double)X0 * K.cc - (double)X0 * K.d) + ((double)X1 * K.dd - (double)X1 * K.c);
                 const double B = (double)Y0 * aC + (double)Y1 * aD;
                 Ebp = ((double)Knz + 16.0) * 0x1p-52 * B;
-                uwp = (uint32_t)r[4];
+                uwp = (uint32_t)vuw;
                 if (Knz == 0 || Sp > Ebp) cls = 1;
                 else if (Sp < -Ebp) {
                   const float uf = (float)((double)uwp / 4294967296.0);
@@ -1216,15 +1255,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             const int p = __builtin_ctzll(pend_mask);
             pend_mask &= pend_mask - 1;
             const int kind = prop_kind(p);
-            const int *r = pin + p * PI_STRIDE;
-            Prop q;
-            q.i = __builtin_amdgcn_readfirstlane(r[0]);
-            q.j = __builtin_amdgcn_readfirstlane(r[1]);
-            q.ii = min(q.i, q.j); q.jj = max(q.i, q.j);
-            const int fl = __builtin_amdgcn_readfirstlane(r[2]);
-            q.inc1 = fl & 1; q.inc2 = (fl >> 1) & 1;
-            q.Kn = __builtin_amdgcn_readfirstlane(r[3]);
-            q.r0 = __builtin_amdgcn_readfirstlane(r[7]);
+            const Prop q = load_prop(p);
             const double S = readlane_f64(Sp, p), Eb = readlane_f64(Ebp, p);
             const int c0 = __builtin_amdgcn_readlane(cls, p), kz = __builtin_amdgcn_readlane(Knz, p);
             const double u = (double)(uint32_t)__builtin_amdgcn_readlane((int)uwp, p) / 4294967296.0;
@@ -1255,12 +1286,12 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             if (!accept) continue;
             delta = dl;
             acc_p = p;
-            used = udrawn ? __builtin_amdgcn_readfirstlane(r[6]) : __builtin_amdgcn_readfirstlane(r[5]);
+            used = udrawn ? __builtin_amdgcn_readlane(voff, p) : __builtin_amdgcn_readlane(vnd, p);
             break;
           }
           STAMP(7);
           if (acc_p < 0) {   /* all of p0..pend-1 rejected or vetoed, as hypothesised */
-            rng_skip(R, (uint32_t)__builtin_amdgcn_readfirstlane(pin[(pend - 1) * PI_STRIDE + 6]));
+            rng_skip(R, (uint32_t)__builtin_amdgcn_readlane(voff, pend - 1));
             p0 = pend;
             continue;
           }
@@ -1269,17 +1300,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 
           /* ---- apply the accepted proposal acc_p */
           const int kind = prop_kind(acc_p);
-          Prop q;
-          {
-            const int *r = pin + acc_p * PI_STRIDE;
-            q.i = __builtin_amdgcn_readfirstlane(r[0]);
-            q.j = __builtin_amdgcn_readfirstlane(r[1]);
-            q.ii = min(q.i, q.j); q.jj = max(q.i, q.j);
-            const int fl = __builtin_amdgcn_readfirstlane(r[2]);
-            q.inc1 = fl & 1; q.inc2 = (fl >> 1) & 1;
-            q.Kn = __builtin_amdgcn_readfirstlane(r[3]);
-            q.r0 = __builtin_amdgcn_readfirstlane(r[7]);
-          }
+          const Prop q = load_prop(acc_p);
           const int i = q.i, j = q.j, ii = q.ii, jj = q.jj, inc1 = q.inc1, inc2 = q.inc2, Kn = q.Kn;
           if (tid == 0) misc[MS_ACC + (kind == PK_PI1 ? 3 : kind == PK_PI2 ? 4 : kind == PK_SWAP ? 5 : 6)]++;
           loglik += delta;
@@ -1288,7 +1309,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             uint32_t *Pm = P + m;
             const int a = sab[m], b = sab[M + m];
             int dt0, dt1;
-            taxon_dt(kind, q, a, b, Pm, M, hp, nh, hcnt, nhall, dt0, dt1);
+            taxon_dt(kind, q, a, b, Pm, M, kind == PK_PI3 ? hard_bits_col(Pm, M, hp, nh) : 0u, hcnt, nhall, dt0, dt1);
             scnt[m] += dt0; scnt[M + m] -= dt0; scnt[2 * M + m] += dt1; scnt[3 * M + m] -= dt1;
             if (kind == PK_PI1) {                                  /* mcmc.c:1266-1297 */
               if (i < j) {
@@ -1350,21 +1371,15 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 else { if (n > j && n <= i) src = n - 1; else if (n == j) src = i; }
                 rn[n] = ro[src];
               }
-#pragma unroll
-              for (int k = 0; k < SR_NHMAX; ++k) {
-                if (k >= nh) break;
-                const int h = hp[k];
-                if (h == i) hp[k] = j;
-                else if (i < j && h > i && h <= j) hp[k] = h - 1;
-                else if (i > j && h >= j && h < i) hp[k] = h + 1;
+              if (lane < nh) {
+                const int h = hp[lane];
+                if (h == i) hp[lane] = j;
+                else if (i < j && h > i && h <= j) hp[lane] = h - 1;
+                else if (i > j && h >= j && h < i) hp[lane] = h + 1;
               }
             } else if (kind != PK_PI3) {
               for (int n = tid; n < N; n += TB) rn[n] = ro[(n >= i && n <= j) ? (i + j - n) : n];
-#pragma unroll
-              for (int k = 0; k < SR_NHMAX; ++k) {
-                if (k >= nh) break;
-                if (hp[k] >= i && hp[k] <= j) hp[k] = i + j - hp[k];
-              }
+              if (lane < nh && hp[lane] >= i && hp[lane] <= j) hp[lane] = i + j - hp[lane];
             } else {
               for (int n = tid; n < N; n += TB)
                 if (n < i || n > j || hcnt[n + 1] != hcnt[n]) rn[n] = ro[n];
@@ -1372,7 +1387,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             }
             rcur ^= 1;
           }
-          if (kind != PK_PI3) build_hard_tables(hp, nh, N, hcnt, nhall, lane);   /* hard sites may have moved */
+          if (kind != PK_PI3) { wsync(); build_hard_tables(hp, nh, N, hcnt, nhall, lane); }   /* hard sites may have moved */
           wsync();
           STAMP(7);
         } /* batches */
@@ -1416,9 +1431,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   int32_t *ocnt = A.cnt + (size_t)chain * 4 * M;
   for (int i = tid; i < 4 * M; i += TB) ocnt[i] = scnt[i];
   if (tid == 0) {
-#pragma unroll
-    for (int k = 0; k < SR_NHMAX; ++k)
-      if (k < nh) A.hp[(size_t)chain * SR_NHMAX + k] = hp[k];
+    for (int k = 0; k < nh; ++k) A.hp[(size_t)chain * SR_NHMAX + k] = hp[k];
     A.cdl[(size_t)chain * 4 + 0] = c;
     A.cdl[(size_t)chain * 4 + 1] = d;
     A.cdl[(size_t)chain * 4 + 2] = loglik;

@@ -62,7 +62,7 @@ struct KArgs {
 
 /* ---------------------------------------------------------------- LDS carve */
 struct Lay {
-  size_t tab, cbuf, lbuf, mt, P, rpi0, rpi1, ht, ck, ccnt, sab, scnt, hpw, part, tot, xs, misc, total;
+  size_t tab, cbuf, lbuf, mt, P, rpi0, rpi1, ht, ck, ccnt, sab, scnt, hpw, t4, part, tot, xs, misc, total;
 };
 __host__ __device__ static inline size_t sr_al16(size_t x) { return (x + 15) & ~(size_t)15; }
 /* Gibbs checkpoint slots per word: one per thread that owns a taxon */
@@ -85,6 +85,7 @@ __host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB)
   L.sab = o;   o = sr_al16(o + (size_t)2 * M * 4);
   L.scnt = o;  o = sr_al16(o + (size_t)4 * M * 4);
   L.hpw = o;   o = sr_al16(o + (size_t)NWV * SR_NHMAX * 4);           /* per wave: hard positions */
+  L.t4 = o;    o = sr_al16(o + (size_t)NWV * 96 * 8);                 /* per wave: 4-entry step tables */
   L.part = o;  o = sr_al16(o + (size_t)2 * 16 * NWV * 8 * 4);         /* [2][proposal][wave] count sums */
   L.tot = o;   o = sr_al16(o + (size_t)2 * NWV * 4 * 4);               /* [2][wave] t0, f0, t1, f1 */
   L.xs = o;    o = sr_al16(o + (size_t)NWV * sizeof(double));          /* per-wave broadcast slot */
@@ -531,7 +532,8 @@ __device__ __forceinline__ double exp2_split(double q)
  * overflow) the exact path runs.  ck: this lane's checkpoint slots (stride ckstride). */
 __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int NW, bool rev, int o, int L, double u,
                                          const CD &K, const sr_mtab &tb, double vA, double vB, double rA, double rB,
-                                         double *ck, int ckstride, uint64_t *fbk, int &dt0, int &df0, int &dt1, int &df1)
+                                         const double *T4, double *ck, int ckstride, uint64_t *fbk, int &dt0, int &df0,
+                                         int &dt1, int &df1)
 {
   const int POo = walk_prefix(Pm, M, N, NW, rev, o);
   const int nk = (L >> 5) + 1;
@@ -565,10 +567,14 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
     for (int k = klo; k <= khi; ++k) {
       const uint32_t ww = walk_word(Pm, M, N, NW, rev, k);
       const int nb = min(32, L + 1 - 32 * k);
+      /* 4 entries per step: T4[c][nibble] = sum of the first c prefix products of the nibble's
+         ratios (c = valid entries of the group, 0..4), T4[5][nibble] = product of all four */
 #pragma unroll
-      for (int b = 0; b < 32; ++b) {
-        S += (b < nb) ? y : 0.0;
-        y = y * (((ww >> b) & 1u) ? rB : rA);
+      for (int g = 0; g < 8; ++g) {
+        const uint32_t nib = (ww >> (4 * g)) & 15u;
+        const int c = min(max(nb - 4 * g, 0), 4);
+        S = __builtin_fma(y, T4[c * 16 + nib], S);
+        y = y * T4[80 + nib];
       }
       ck[k * ckstride] = S;
     }
@@ -582,10 +588,10 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
     int j = klo;
     while (j < khi && ck[j * ckstride] * inv < u) ++j;
     double y = y0;
-    for (int k = klo; k < j; ++k) {
+    for (int k = klo; k < j; ++k) {   /* words before j are full (only the walk's last word is partial) */
       const uint32_t ww = walk_word(Pm, M, N, NW, rev, k);
 #pragma unroll
-      for (int b = 0; b < 32; ++b) y = y * (((ww >> b) & 1u) ? rB : rA);
+      for (int g = 0; g < 8; ++g) y = y * T4[80 + ((ww >> (4 * g)) & 15u)];
     }
     double Sp = (j == klo) ? 0.0 : ck[(j - 1) * ckstride];
     double tprev = u - Sp * inv;
@@ -905,6 +911,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   int32_t *sab = (int32_t *)(smem + L.sab);     /* a[M], b[M] */
   int32_t *scnt = (int32_t *)(smem + L.scnt);   /* t0[M], f0[M], t1[M], f1[M] */
   int *hp = (int *)(smem + L.hpw) + wave * SR_NHMAX;   /* this wave's copy of the hard positions */
+  double *T4w = (double *)(smem + L.t4) + wave * 96;     /* this wave's 4-step tables */
   int *part = (int *)(smem + L.part);
   int *tot = (int *)(smem + L.tot);
   double *xs = (double *)(smem + L.xs) + wave;
@@ -998,6 +1005,17 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       const double vA = (K.d - K.cc) * 1.4426950408889634;
       const double vB = (K.dd - K.c) * 1.4426950408889634;
       const double rA = sr_exp_m(K.cc - K.d, &tb), rB = sr_exp_m(K.c - K.dd, &tb);   /* 2^-vA, 2^-vB */
+      if (lane < 16) {   /* per-wave tables for 4 walk entries with bits = lane */
+        double pr = 1.0, sm = 1.0;
+        T4w[lane] = 0.0;
+        T4w[16 + lane] = sm;
+        pr = pr * ((lane & 1) ? rB : rA); sm = sm + pr; T4w[32 + lane] = sm;
+        pr = pr * ((lane & 2) ? rB : rA); sm = sm + pr; T4w[48 + lane] = sm;
+        pr = pr * ((lane & 4) ? rB : rA); sm = sm + pr; T4w[64 + lane] = sm;
+        pr = pr * ((lane & 8) ? rB : rA);
+        T4w[80 + lane] = pr;
+      }
+      wsync();
 
       /* ============ phase B: Gibbs update of own (a_m, b_m) (mcmc_sampleab) */
       rng_ensure(R, min(2 * M + SR_RNG_SLACK, (SR_RING - 1) * SR_MT_N - (SR_MT_N - 1)), tid, TB);
@@ -1016,7 +1034,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             int d0, e0, d1, e1;
             const bool rev = pass != 0;
             const int res = draw_fast(Pm, M, N, NW, rev, rev ? N - b0 : a0, rev ? N - na : b0, rev ? ub : ua, K, tb,
-                                      vA, vB, rA, rB, ckb + tid, CKS, &misc[MS_FBK], d0, e0, d1, e1);
+                                      vA, vB, rA, rB, T4w, ckb + tid, CKS, &misc[MS_FBK], d0, e0, d1, e1);
             t0 += d0; f0 += e0; t1 += d1; f1 += e1;
             if (rev) nb = N - res; else na = res;
           }

@@ -75,7 +75,7 @@ def main():
     ap.add_argument("--chains-per-gpu", type=int, default=100)
     ap.add_argument("--calls-per-step", type=int, default=10)
     ap.add_argument("--dataset", default=SYNTH)
-    ap.add_argument("--cpu-calls", type=int, default=300)
+    ap.add_argument("--cpu-calls", type=int, default=800)
     ap.add_argument("--cpu-workers", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--block-threads", type=int, default=0)

@@ -135,6 +135,13 @@ __device__ __forceinline__ void gsync()
 #define STAMP(ph) do { } while (0)
 #define STAMP_STORE(dst) do { } while (0)
 #endif
+#ifdef SR_STAMP_DRAWS   /* alternative split of phase C: batch setup / draw loop / taxon cache / terms / rest */
+#define STAMP_D(ph) STAMP(ph)
+#define STAMP_K(kind) STAMP(6)
+#else
+#define STAMP_D(ph) do { } while (0)
+#define STAMP_K(kind) do { if ((kind) == PK_PI1) STAMP(4); else if ((kind) == PK_PI3) STAMP(6); else STAMP(5); } while (0)
+#endif
 
 /* ---------------------------------------------------------------- RNG */
 struct DRng {
@@ -1095,6 +1102,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             vw0 = sr_mt_temper(ring[i0]);
             vw1 = sr_mt_temper(ring[i1]);
           }
+          STAMP_D(3);
           int off = 0, pend = p0;
           for (int p = p0; p < 16; ++p) {
             if (p0 == 0 && p == 1) break;   /* the swap (accepted ~40 %) forms its own batch */
@@ -1162,6 +1170,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             pend = p + 1;
           }
           pend = __builtin_amdgcn_readfirstlane(pend);
+          STAMP_D(4);
           if (pend == p0) {   /* not enough resident words for one proposal: make more, retry */
             rng_ensure(R, min(avail + 256, (SR_RING - 1) * SR_MT_N - (SR_MT_N - 1)), tid, TB);
             continue;
@@ -1180,50 +1189,76 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 
           /* ---- exact integer count sums of every drawn proposal over own taxa, per wave */
           int *pw = part + (bpar * 16) * NWV * 8;
-          const bool pack = N * ((M + TB - 1) / TB) < 512;   /* per-wave sums fit 16-bit fields */
+          const bool pack = N < 512;   /* one taxon per thread: per-wave sums fit 16-bit fields */
           /* own taxon's limits and hard-site bits, fixed for the batch (one taxon per thread) */
           const bool one = M <= TB;
           int a1 = 0, b1 = 0;
           uint32_t hb1 = 0;
           if (one && tid < M) { a1 = sab[tid]; b1 = sab[M + tid]; hb1 = hard_bits_col(P + tid, M, hp, nh); }
+#ifdef SR_STAMP_DRAWS
+          STAMP(5);
+#else
           STAMP(3);
-          for (int p = p0; p < pend; ++p) {
-            if (__builtin_amdgcn_readlane(vfl, p) & 4) continue;
-#ifdef SR_STAMPS
-            if (tid == 0) misc[40 + (prop_kind(p) == PK_PI1 ? 0 : prop_kind(p) == PK_PI3 ? 2 : 1)]++;
 #endif
+          if (one) {
+            /* one taxon per thread: all 16 proposal slots unrolled; slot s has the compile-time
+               kind prop_kind(s), so each copy holds one kind's code and the slots' loads, ALU
+               and reductions are independent */
+            int d0s[16], d1s[16], nzs[16];
+#pragma unroll
+            for (int sI = 0; sI < 16; ++sI) {
+              d0s[sI] = 0; d1s[sI] = 0; nzs[sI] = 0;
+              const int fl = __builtin_amdgcn_readlane(vfl, sI);
+              if (sI >= p0 && sI < pend && !(fl & 4)) {
+                const Prop q = load_prop(sI);
+                int dt0 = 0, dt1 = 0;
+                if (tid < M) taxon_dt(prop_kind(sI), q, a1, b1, P + tid, M, hb1, hcnt, nhall, dt0, dt1);
+                d0s[sI] = dt0; d1s[sI] = dt1;
+                nzs[sI] = __popcll(__ballot((dt0 | dt1) != 0));
+              }
+            }
+#pragma unroll
+            for (int sI = 0; sI < 16; ++sI) {
+              const int fl = __builtin_amdgcn_readlane(vfl, sI);
+              if (sI >= p0 && sI < pend && !(fl & 4)) {
+                int X0, X1, Y0, Y1;
+                if (pack) {   /* per-wave sums of (dt + N) and |dt| fit 16-bit fields (N < 512) */
+                  const uint32_t u1 = (uint32_t)wave_sum_i32((int)((uint32_t)(d0s[sI] + N) | ((uint32_t)(d1s[sI] + N) << 16)));
+                  const uint32_t u2 = (uint32_t)wave_sum_i32((int)((uint32_t)abs(d0s[sI]) | ((uint32_t)abs(d1s[sI]) << 16)));
+                  X0 = (int)(u1 & 0xffffu) - 64 * N; X1 = (int)(u1 >> 16) - 64 * N;
+                  Y0 = (int)(u2 & 0xffffu); Y1 = (int)(u2 >> 16);
+                } else {
+                  X0 = wave_sum_i32(d0s[sI]); X1 = wave_sum_i32(d1s[sI]);
+                  Y0 = wave_sum_i32(abs(d0s[sI])); Y1 = wave_sum_i32(abs(d1s[sI]));
+                }
+                if (lane == 0) {
+                  int *o = pw + (sI * NWV + wave) * 8;
+                  o[0] = X0; o[1] = X1; o[2] = Y0; o[3] = Y1; o[4] = nzs[sI];
+                }
+              }
+            }
+            STAMP_K(PK_PI3);
+          } else
+          for (int p = p0; p < pend; ++p) {   /* several taxa per thread */
+            if (__builtin_amdgcn_readlane(vfl, p) & 4) continue;
             const int kind = prop_kind(p);
             const Prop q = load_prop(p);
             int x0 = 0, x1 = 0, y0 = 0, y1 = 0, nzc = 0;
             for (int m0 = wave * 64; m0 < M; m0 += TB) {
               const int m = m0 + lane;
               int dt0 = 0, dt1 = 0;
-              if (m < M) {
-                if (one) taxon_dt(kind, q, a1, b1, P + m, M, hb1, hcnt, nhall, dt0, dt1);
-                else taxon_dt(kind, q, sab[m], sab[M + m], P + m, M, kind == PK_PI3 ? hard_bits_col(P + m, M, hp, nh) : 0u,
-                              hcnt, nhall, dt0, dt1);
-              }
+              if (m < M)
+                taxon_dt(kind, q, sab[m], sab[M + m], P + m, M, kind == PK_PI3 ? hard_bits_col(P + m, M, hp, nh) : 0u,
+                         hcnt, nhall, dt0, dt1);
               x0 += dt0; x1 += dt1; y0 += abs(dt0); y1 += abs(dt1);
               nzc += __popcll(__ballot((dt0 | dt1) != 0));
             }
-            int X0, X1, Y0, Y1;
-            if (pack) {
-              const int tpl = (M + TB - 1) / TB;   /* taxa per lane: each lane adds bias N per slot */
-              uint32_t u1 = (uint32_t)((x0 + N * tpl) | ((x1 + N * tpl) << 16));
-              uint32_t u2 = (uint32_t)(y0 | (y1 << 16));
-              u1 = (uint32_t)wave_sum_i32((int)u1);
-              u2 = (uint32_t)wave_sum_i32((int)u2);
-              const int bias = 64 * N * tpl;
-              X0 = (int)(u1 & 0xffffu) - bias; X1 = (int)(u1 >> 16) - bias;
-              Y0 = (int)(u2 & 0xffffu); Y1 = (int)(u2 >> 16);
-            } else {
-              X0 = wave_sum_i32(x0); X1 = wave_sum_i32(x1); Y0 = wave_sum_i32(y0); Y1 = wave_sum_i32(y1);
-            }
+            const int X0 = wave_sum_i32(x0), X1 = wave_sum_i32(x1), Y0 = wave_sum_i32(y0), Y1 = wave_sum_i32(y1);
             if (lane == 0) {
               int *o = pw + (p * NWV + wave) * 8;
               o[0] = X0; o[1] = X1; o[2] = Y0; o[3] = Y1; o[4] = nzc;
             }
-            if (kind == PK_PI1) STAMP(4); else if (kind == PK_PI3) STAMP(6); else STAMP(5);
+            STAMP_K(kind);
           }
           __syncthreads();
 

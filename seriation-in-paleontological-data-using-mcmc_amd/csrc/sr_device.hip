@@ -277,6 +277,12 @@ __device__ __forceinline__ uint32_t udivm(uint32_t g, const UDivM &u)
   return (t + ((g - t) >> 1)) >> (u.l - 1);
 }
 
+__device__ __forceinline__ uint32_t udivm_v(uint32_t g, uint32_t m, int l)
+{
+  const uint32_t t = __umulhi(m, g);
+  return (t + ((g - t) >> 1)) >> (l - 1);
+}
+
 /* the next 8 tempered words from the cursor, loaded together, if they are resident (the ring
  * is a circular buffer of SR_RING * 624 words: block b lives at (b mod SR_RING) * 624) */
 __device__ __forceinline__ bool rng_window8(const DRng &r, uint32_t (&w)[8])
@@ -1104,8 +1110,95 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           }
           STAMP_D(3);
           int off = 0, pend = p0;
-          for (int p = p0; p < 16; ++p) {
-            if (p0 == 0 && p == 1) break;   /* the swap (accepted ~40 %) forms its own batch */
+          if (p0 > 0) {
+            /* Lane-parallel draws: lane l evaluates "a pi1 / pi2 / pi3 proposal starting at word
+               offset o" for o = l and o = l + 64 (words o..o+4); the scan below then walks the
+               batch's actual offsets reading those results.  ok = no GSL rejection and a nonzero
+               uniform_pos word (else the scalar path below takes over at that proposal). */
+            uint32_t rA1[2], rA2[2], rA3[2], rB3[2], rU1[2], rU2[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int o = lane + 64 * h;
+              uint32_t w[5];
+#pragma unroll
+              for (int k = 0; k < 5; ++k) {
+                uint32_t idx = base + (uint32_t)min(o + k, avail - 1);
+                idx = (idx >= SR_RING * SR_MT_N) ? idx - SR_RING * SR_MT_N : idx;
+                w[k] = sr_mt_temper(ring[idx]);
+              }
+              const bool in = o + 5 <= avail;
+              const uint32_t qN = udivm_v(w[0], mdN.m, mdN.l), qN1 = udivm_v(w[1], mdN1.m, mdN1.l);
+              const uint32_t qa = udivm_v(w[2], md2.m, md2.l), qb = udivm_v(w[3], md2.m, md2.l);
+              const bool okN = in && qN < mdN.n && qN1 < mdN1.n;
+              const bool okab = qa < 2u && qb < 2u;
+              /* pi1 (mcmc.c:1133-1160): words o, o+1, uniform_pos at o+2 */
+              {
+                const int i = (int)qN, j = (int)qN1 + ((int)qN1 >= (int)qN ? 1 : 0);
+                const int ic = min(i, N - 1), jc = min(j, N - 1);
+                const bool veto = (hcnt[ic + 1] != hcnt[ic]) && (hcnt[max(ic, jc) + 1] - hcnt[min(ic, jc)] > 1);
+                const bool ok = okN && (veto || w[2] != 0u);
+                rA1[h] = (uint32_t)ic | ((uint32_t)jc << 11) | (veto ? 1u << 22 : 0u) | (ok ? 1u << 23 : 0u);
+                rU1[h] = w[2];
+              }
+              /* pi2 (mcmc.c:1317-1364): words o, o+1, [o+2, o+3 inc], uniform_pos at o+4 */
+              {
+                int i = (int)qN, j = (int)qN1;
+                if (j >= i) j++; else { const int t = i; i = j; j = t; }
+                const int ic = min(i, N - 1), jc = min(j, N - 1);
+                const bool veto = hcnt[jc + 1] - hcnt[ic] > 1;
+                const bool ok = okN && (veto || (okab && w[4] != 0u));
+                rA2[h] = (uint32_t)ic | ((uint32_t)jc << 11) | (veto ? 1u << 22 : 0u) | (ok ? 1u << 23 : 0u) |
+                         (qa << 24) | (qb << 25);
+                rU2[h] = w[4];
+              }
+              /* pi3 (mcmc.c:1495-1565): words o..o+3, uniform_pos at o+4 */
+              {
+                const uint32_t qH = udivm_v(w[0], mdH.m, mdH.l), qH1 = udivm_v(w[1], mdH1.m, mdH1.l);
+                int ri, rj;
+                if ((int)qH <= (int)qH1) { ri = (int)qH; rj = (int)qH1 + 1; } else { ri = (int)qH1; rj = (int)qH; }
+                const int NH = N - nh;
+                ri = min(ri, max(NH - 1, 0)); rj = min(rj, max(NH - 1, 0));
+                const int i = nhall[ri], j = nhall[rj];
+                const bool ok = in && NH >= 2 && qH < mdH.n && qH1 < mdH1.n && okab && w[4] != 0u;
+                rA3[h] = (uint32_t)i | ((uint32_t)j << 11) | (ok ? 1u << 23 : 0u) | (qa << 24) | (qb << 25);
+                rB3[h] = (uint32_t)ri | ((uint32_t)(rj - ri + 1) << 16);
+              }
+            }
+            /* scan: the batch's proposals at their actual offsets (all-rejected hypothesis) */
+#pragma unroll
+            for (int sI = 1; sI < 16; ++sI) {
+              if (sI < p0 || pend != sI || off + 5 > 128) continue;
+              const int kind = prop_kind(sI);
+              const int h = off >> 6, l = off & 63;
+              uint32_t ra, rb = 0, ru;
+              if (kind == PK_PI1) { ra = (uint32_t)__builtin_amdgcn_readlane((int)(h ? rA1[1] : rA1[0]), l);
+                                    ru = (uint32_t)__builtin_amdgcn_readlane((int)(h ? rU1[1] : rU1[0]), l); }
+              else if (kind == PK_PI2) { ra = (uint32_t)__builtin_amdgcn_readlane((int)(h ? rA2[1] : rA2[0]), l);
+                                         ru = (uint32_t)__builtin_amdgcn_readlane((int)(h ? rU2[1] : rU2[0]), l); }
+              else { ra = (uint32_t)__builtin_amdgcn_readlane((int)(h ? rA3[1] : rA3[0]), l);
+                     rb = (uint32_t)__builtin_amdgcn_readlane((int)(h ? rB3[1] : rB3[0]), l);
+                     ru = (uint32_t)__builtin_amdgcn_readlane((int)(h ? rU2[1] : rU2[0]), l); }
+              if (!(ra & (1u << 23))) continue;   /* rejection or zero word: scalar path */
+              const bool veto = (ra >> 22) & 1u;
+              const int i = (int)(ra & 2047u), j = (int)((ra >> 11) & 2047u);
+              const int inc = (int)((ra >> 24) & 3u);
+              const int nd = off + (kind == PK_PI1 ? 2 : (kind == PK_PI2 ? (veto ? 2 : 4) : 4));
+              const int ofa = nd + (veto ? 0 : 1);
+              vi = (lane == sI) ? i : vi;
+              vj = (lane == sI) ? j : vj;
+              vfl = (lane == sI) ? (inc | (veto ? 4 : 0)) : vfl;
+              vkn = (lane == sI) ? (int)(rb >> 16) : vkn;
+              vr0 = (lane == sI) ? (int)(rb & 0xffffu) : vr0;
+              vuw = (lane == sI) ? (int)ru : vuw;
+              vnd = (lane == sI) ? nd : vnd;
+              voff = (lane == sI) ? ofa : voff;
+              off = ofa;
+              pend = sI + 1;
+            }
+          }
+          for (int p = pend; p < 16; ++p) {   /* scalar path: the swap batch, and after a fast-path stop */
+            if (p0 == 0 && p == 1) break;     /* the swap (accepted ~40 %) forms its own batch */
+            if (p > p0) break;                /* only the batch's first proposal goes scalar */
             const int kind = prop_kind(p);
             bool bad = false;
             auto word = [&](void) -> uint32_t {

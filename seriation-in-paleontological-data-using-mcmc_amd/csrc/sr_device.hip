@@ -135,10 +135,31 @@ __device__ __forceinline__ void gsync()
 #define STAMP(ph) do { } while (0)
 #define STAMP_STORE(dst) do { } while (0)
 #endif
-#ifdef SR_STAMP_DRAWS   /* alternative split of phase C: batch setup / draw loop / taxon cache / terms / rest */
+#ifdef SR_STAMP_GIBBS   /* phase B split: slots 1 prefix+pass0, 2 pass1, 3 pass2, 4 tail */
+#define GSTAMP(ph) do { unsigned long long t_ = __builtin_amdgcn_s_memtime(); gst[ph] += t_ - *gst_t; *gst_t = t_; } while (0)
+#define GSTAMP_ARGS , unsigned long long *gst, unsigned long long *gst_t
+#define GSTAMP_PASS , st_acc, &st_t
+#define GSTAMP_K4() STAMP(4)
+#else
+#define GSTAMP_K4() do { } while (0)
+#define GSTAMP(ph) do { } while (0)
+#define GSTAMP_ARGS
+#define GSTAMP_PASS
+#endif
+#if defined(SR_STAMP_GIBBS)
+#define STAMP_D(ph) do { } while (0)
+#define STAMP_K(kind) STAMP(6)
+#define STAMP_E(ph) do { } while (0)
+#elif defined(SR_STAMP_DRAWS)   /* alternative split of phase C: batch setup / draw loop / taxon cache / terms / rest */
 #define STAMP_D(ph) STAMP(ph)
 #define STAMP_K(kind) STAMP(6)
+#define STAMP_E(ph) do { } while (0)
+#elif defined(SR_STAMP_DECIDE)   /* draws+cache / terms / barrier wait / decide+scan / apply+rest */
+#define STAMP_D(ph) do { } while (0)
+#define STAMP_K(kind) STAMP(4)
+#define STAMP_E(ph) STAMP(ph)
 #else
+#define STAMP_E(ph) do { } while (0)
 #define STAMP_D(ph) do { } while (0)
 #define STAMP_K(kind) do { if ((kind) == PK_PI1) STAMP(4); else if ((kind) == PK_PI3) STAMP(6); else STAMP(5); } while (0)
 #endif
@@ -546,7 +567,7 @@ __device__ __forceinline__ double exp2_split(double q)
 __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int NW, bool rev, int o, int L, double u,
                                          const CD &K, const sr_mtab &tb, double vA, double vB, double rA, double rB,
                                          const double *T4, double *ck, int ckstride, uint64_t *fbk, int &dt0, int &df0,
-                                         int &dt1, int &df1)
+                                         int &dt1, int &df1 GSTAMP_ARGS)
 {
   const int POo = walk_prefix(Pm, M, N, NW, rev, o);
   const int nk = (L >> 5) + 1;
@@ -572,6 +593,7 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
       O += __popc(ww);
     }
   }
+  GSTAMP(1);
   /* pass 1: S over the window, checkpoints */
   const double y0 = exp2_split(qlo);
   double S = 0.0;
@@ -592,45 +614,68 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
       ck[k * ckstride] = S;
     }
   }
+  GSTAMP(2);
   /* pass 2: locate the word, replay the chain to it, certify inside it */
   int res = -1;
   if (S > 0.0 && S < 0x1p1000) {
     const double inv = 1.0 / S;
     const double REL = (double)(N + 1) * 0x1p-50;
     const double ABS = (double)(N + 1) * 0x1p-39;
-    int j = klo;
-    while (j < khi && ck[j * ckstride] * inv < u) ++j;
+    int j = klo;   /* first window word whose checkpoint reaches u (checkpoints ascend) */
+    for (int k = klo; k < khi; ++k) j += (ck[k * ckstride] * inv < u) ? 1 : 0;
     double y = y0;
     for (int k = klo; k < j; ++k) {   /* words before j are full (only the walk's last word is partial) */
       const uint32_t ww = walk_word(Pm, M, N, NW, rev, k);
 #pragma unroll
       for (int g = 0; g < 8; ++g) y = y * T4[80 + ((ww >> (4 * g)) & 15u)];
     }
-    double Sp = (j == klo) ? 0.0 : ck[(j - 1) * ckstride];
-    double tprev = u - Sp * inv;
-    double eprev = 2.0 * REL * fmin(Sp, S - Sp) * inv + ABS;
+    const double Sp0 = (j == klo) ? 0.0 : ck[(j - 1) * ckstride];
     const int w0 = 32 * j;
     const uint32_t ww = walk_word(Pm, M, N, NW, rev, j);
     const int nb = min(32, L + 1 - w0);
-    const int wend = (j == khi) ? L : w0 + nb - 1;   /* last window entry: the pick must land by here */
-    for (int b = 0; b < nb; ++b) {
-      const int w = w0 + b;
-      Sp += y;
-      const double t = u - Sp * inv;
-      const double e = 2.0 * REL * fmin(Sp, S - Sp) * inv + ABS;
-      if (t < 0.0 || w == wend) {
-        const bool prev_ok = (w == 0) || (tprev > eprev);
-        const bool here_ok = (w == L) || (t < -e);
-        if (prev_ok && here_ok) res = w;
-#ifdef SR_STAMPS
-        else atomicAdd((unsigned long long *)fbk + (prev_ok ? 2 : 1), 1ull);
-#endif
-        break;
+    const int nvg = (nb + 3) >> 2;   /* groups of 4 holding valid entries */
+    /* group-end sums of word j, then the group and the entry where u falls (branch-free) */
+    double gsum[8], gy[8];
+    int ng = 0;
+    {
+      double yy = y, acc = Sp0;
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        const uint32_t nib = (ww >> (4 * g)) & 15u;
+        const int c = min(max(nb - 4 * g, 0), 4);
+        gy[g] = yy;
+        acc = __builtin_fma(yy, T4[c * 16 + nib], acc);
+        gsum[g] = acc;
+        yy = yy * T4[80 + nib];
       }
-      tprev = t;
-      eprev = e;
-      y = y * (((ww >> b) & 1u) ? rB : rA);
+#pragma unroll
+      for (int g = 0; g < 8; ++g) ng += (g < nvg && gsum[g] * inv < u) ? 1 : 0;
     }
+    const int gsel = min(ng, nvg - 1);
+    double base = Sp0, ys = y;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      if (g == gsel) ys = gy[g];
+      if (g + 1 == gsel) base = gsum[g];
+    }
+    const uint32_t nibs = (ww >> (4 * gsel)) & 15u;
+    const int cmax = min(nb - 4 * gsel, 4);
+    const double P1 = __builtin_fma(ys, T4[16 + nibs], base), P2 = __builtin_fma(ys, T4[32 + nibs], base);
+    const double P3 = __builtin_fma(ys, T4[48 + nibs], base), P4 = __builtin_fma(ys, T4[64 + nibs], base);
+    const int nc = ((cmax > 1 && P1 * inv < u) ? 1 : 0) + ((cmax > 2 && P2 * inv < u) ? 1 : 0) +
+                   ((cmax > 3 && P3 * inv < u) ? 1 : 0);
+    const double Ph = (nc == 0) ? P1 : (nc == 1) ? P2 : (nc == 2) ? P3 : P4;
+    const double Pp = (nc == 0) ? base : (nc == 1) ? P1 : (nc == 2) ? P2 : P3;
+    const int w = w0 + 4 * gsel + nc;
+    const double t = u - Ph * inv, tprev = u - Pp * inv;
+    const double e = 2.0 * REL * fmin(Ph, S - Ph) * inv + ABS;
+    const double eprev = 2.0 * REL * fmin(Pp, S - Pp) * inv + ABS;
+    const bool prev_ok = (w == 0) || (tprev > eprev);
+    const bool here_ok = (w == L) || (t < -e);
+    if (prev_ok && here_ok) res = w;
+#ifdef SR_STAMPS
+    else atomicAdd((unsigned long long *)fbk + (prev_ok ? 2 : 1), 1ull);
+#endif
   }
   if (res < 0) {
 #ifdef SR_STAMPS
@@ -639,6 +684,7 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
 #endif
     return draw_exact(Pm, M, N, rev, o, L, u, K, tb, dt0, df0, dt1, df1);
   }
+  GSTAMP(3);
   const int POp = walk_prefix(Pm, M, N, NW, rev, res);
   if (res == o) { dt0 = df0 = dt1 = df1 = 0; }
   else if (res < o) { int O = POo - POp; int Z = (o - res) - O; dt0 = -Z; df0 = Z; dt1 = O; df1 = -O; }
@@ -780,11 +826,12 @@ __device__ __forceinline__ void build_hard_tables(const int *hp, int nh, int N, 
  * dt0 (zeros inside), dt1 (ones inside); the reference's df0 = -dt0 and df1 = -dt1 always
  * (mcmc.c:1175-1256 pi1, 1367-1436 pi2, 1568-1631 pi3).  hcnt/nhall: the wave's hard-site tables. */
 /* column bits at the hard positions, bit k = hard site k (input of the pi3 count change) */
-__device__ __forceinline__ uint32_t hard_bits_col(const uint32_t *Pm, int M, const int *hp, int nh)
+/* hl: lane k holds hard position k (loaded by the caller with every lane active) */
+__device__ __forceinline__ uint32_t hard_bits_col(const uint32_t *Pm, int M, int hl, int nh)
 {
   uint32_t hbm = 0;
   for (int k = 0; k < nh; ++k) {
-    const int h = __builtin_amdgcn_readfirstlane(hp[k]);
+    const int h = __builtin_amdgcn_readlane(hl, k);
     hbm |= ((Pm[(h >> 5) * M] >> (h & 31)) & 1u) << k;
   }
   return hbm;
@@ -867,13 +914,13 @@ __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, 
  * 1435, 1630 term order) compacted per 64-taxon chunk into cb, then summed sequentially in
  * ascending m by lane 0 of every wave.  Block-uniform call (contains a barrier). */
 __device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const int32_t *sab, const uint32_t *P, int M, int KT,
-                                              const int *hp, int nh, const int16_t *hcnt, const int16_t *nhall, double *cb, int *cc, double *xs,
+                                              int hl, int nh, const int16_t *hcnt, const int16_t *nhall, double *cb, int *cc, double *xs,
                                               int lane, int wave, int TB)
 {
   for (int m0 = wave * 64; m0 < KT * 64; m0 += TB) {
     const int ch = m0 >> 6, m = m0 + lane;
     int dt0 = 0, dt1 = 0;
-    if (m < M) taxon_dt(kind, q, sab[m], sab[M + m], P + m, M, kind == PK_PI3 ? hard_bits_col(P + m, M, hp, nh) : 0u,
+    if (m < M) taxon_dt(kind, q, sab[m], sab[M + m], P + m, M, kind == PK_PI3 ? hard_bits_col(P + m, M, hl, nh) : 0u,
                         hcnt, nhall, dt0, dt1);
     const double tv = (m < M) ? qval(dt0, -dt0, dt1, -dt1, K) : 0.0;
     const uint64_t msk = __ballot(tv != 0.0);
@@ -1030,6 +1077,9 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       }
       wsync();
 
+#ifdef SR_STAMP_GIBBS
+      STAMP(5);
+#endif
       /* ============ phase B: Gibbs update of own (a_m, b_m) (mcmc_sampleab) */
       rng_ensure(R, min(2 * M + SR_RNG_SLACK, (SR_RING - 1) * SR_MT_N - (SR_MT_N - 1)), tid, TB);
       {
@@ -1047,7 +1097,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             int d0, e0, d1, e1;
             const bool rev = pass != 0;
             const int res = draw_fast(Pm, M, N, NW, rev, rev ? N - b0 : a0, rev ? N - na : b0, rev ? ub : ua, K, tb,
-                                      vA, vB, rA, rB, T4w, ckb + tid, CKS, &misc[MS_FBK], d0, e0, d1, e1);
+                                      vA, vB, rA, rB, T4w, ckb + tid, CKS, &misc[MS_FBK], d0, e0, d1, e1 GSTAMP_PASS);
+            GSTAMP_K4();
             t0 += d0; f0 += e0; t1 += d1; f1 += e1;
             if (rev) nb = N - res; else na = res;
           }
@@ -1092,6 +1143,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         int p0 = 0;
         while (p0 < 16) {
           p0 = __builtin_amdgcn_readfirstlane(p0);   /* block-uniform: keep the control flow scalar */
+          const int hl = (lane < nh) ? hp[lane] : 0;  /* lane k: hard position k */
           /* ---- draws of proposals p0.. under the hypothesis: block-uniform scalar code; the
              record of proposal p lives in lane p of the v* registers */
           const uint32_t rblk = __builtin_amdgcn_readfirstlane(R.blk), roff = __builtin_amdgcn_readfirstlane(R.off);
@@ -1287,9 +1339,11 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           const bool one = M <= TB;
           int a1 = 0, b1 = 0;
           uint32_t hb1 = 0;
-          if (one && tid < M) { a1 = sab[tid]; b1 = sab[M + tid]; hb1 = hard_bits_col(P + tid, M, hp, nh); }
-#ifdef SR_STAMP_DRAWS
+          if (one && tid < M) { a1 = sab[tid]; b1 = sab[M + tid]; hb1 = hard_bits_col(P + tid, M, hl, nh); }
+#if defined(SR_STAMP_DRAWS)
           STAMP(5);
+#elif defined(SR_STAMP_GIBBS)
+          STAMP(6);
 #else
           STAMP(3);
 #endif
@@ -1341,7 +1395,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               const int m = m0 + lane;
               int dt0 = 0, dt1 = 0;
               if (m < M)
-                taxon_dt(kind, q, sab[m], sab[M + m], P + m, M, kind == PK_PI3 ? hard_bits_col(P + m, M, hp, nh) : 0u,
+                taxon_dt(kind, q, sab[m], sab[M + m], P + m, M, kind == PK_PI3 ? hard_bits_col(P + m, M, hl, nh) : 0u,
                          hcnt, nhall, dt0, dt1);
               x0 += dt0; x1 += dt1; y0 += abs(dt0); y1 += abs(dt1);
               nzc += __popcll(__ballot((dt0 | dt1) != 0));
@@ -1354,6 +1408,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             STAMP_K(kind);
           }
           __syncthreads();
+          STAMP_E(5);
 
           /* ---- lane-parallel certified decisions (lane p decides proposal p).  With
              X = sum dt, Y = sum |dt| (exact integers), S = X0 (cc - d) + X1 (dd - c) is the exact
@@ -1420,7 +1475,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               }
             }
             if (!decided || (accept && want_logl && !have_exact)) {   /* the exact sequential delta */
-              dl = sr_exact_delta(kind, q, K, sab, P, M, KT, hp, nh, hcnt, nhall, cbuf + xpar * KT * 64, ccnt + xpar * KT,
+              dl = sr_exact_delta(kind, q, K, sab, P, M, KT, hl, nh, hcnt, nhall, cbuf + xpar * KT * 64, ccnt + xpar * KT,
                                   xs, lane, wave, TB);
               xpar ^= 1;
               if (!decided) {
@@ -1435,7 +1490,11 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             used = udrawn ? __builtin_amdgcn_readlane(voff, p) : __builtin_amdgcn_readlane(vnd, p);
             break;
           }
+#ifdef SR_STAMP_DECIDE
+          STAMP(6);
+#else
           STAMP(7);
+#endif
           if (acc_p < 0) {   /* all of p0..pend-1 rejected or vetoed, as hypothesised */
             rng_skip(R, (uint32_t)__builtin_amdgcn_readlane(voff, pend - 1));
             p0 = pend;
@@ -1455,7 +1514,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             uint32_t *Pm = P + m;
             const int a = sab[m], b = sab[M + m];
             int dt0, dt1;
-            taxon_dt(kind, q, a, b, Pm, M, kind == PK_PI3 ? hard_bits_col(Pm, M, hp, nh) : 0u, hcnt, nhall, dt0, dt1);
+            taxon_dt(kind, q, a, b, Pm, M, kind == PK_PI3 ? hard_bits_col(Pm, M, hl, nh) : 0u, hcnt, nhall, dt0, dt1);
             scnt[m] += dt0; scnt[M + m] -= dt0; scnt[2 * M + m] += dt1; scnt[3 * M + m] -= dt1;
             if (kind == PK_PI1) {                                  /* mcmc.c:1266-1297 */
               if (i < j) {

@@ -530,7 +530,7 @@ __device__ __forceinline__ int walk_prefix(const uint32_t *Pm, int M, int N, int
 {
   int s = 0;
   const int full = w >> 5;
-  for (int k = 0; k < full; ++k) s += __popc(walk_word(Pm, M, N, NW, rev, k));
+    for (int k = 0; k < full; ++k) s += __popc(walk_word(Pm, M, N, NW, rev, k));
   if (w & 31) s += __popc(walk_word(Pm, M, N, NW, rev, full) & ((1u << (w & 31)) - 1u));
   return s;
 }
@@ -576,7 +576,7 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
   double qlo = 0.0;
   {
     int O = 0;   /* ones among walk entries [0, 32k) */
-    for (int k = 0; k < nk; ++k) {
+        for (int k = 0; k < nk; ++k) {
       const uint32_t ww = walk_word(Pm, M, N, NW, rev, k);
       const int nb = min(32, L + 1 - 32 * k);
       const uint32_t vm = (nb >= 32) ? 0xffffffffu : ((1u << nb) - 1u);
@@ -594,12 +594,23 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
     }
   }
   GSTAMP(1);
+#ifdef SR_STAMP_GIBBS
+  {   /* window statistics: words per draw, wave max, walk words */
+    const int wn = khi - klo + 1;
+    int wmax = wn;
+    for (int off_ = 32; off_ > 0; off_ >>= 1) wmax = max(wmax, __shfl_xor(wmax, off_));
+    atomicAdd((unsigned long long *)fbk + 26, (unsigned long long)wn);
+    if ((threadIdx.x & 63) == 0) atomicAdd((unsigned long long *)fbk + 27, (unsigned long long)wmax);
+    atomicAdd((unsigned long long *)fbk + 28, (unsigned long long)nk);
+    atomicAdd((unsigned long long *)fbk + 29, 1ull);
+  }
+#endif
   /* pass 1: S over the window, checkpoints */
   const double y0 = exp2_split(qlo);
   double S = 0.0;
   {
     double y = y0;
-    for (int k = klo; k <= khi; ++k) {
+        for (int k = klo; k <= khi; ++k) {
       const uint32_t ww = walk_word(Pm, M, N, NW, rev, k);
       const int nb = min(32, L + 1 - 32 * k);
       /* 4 entries per step: T4[c][nibble] = sum of the first c prefix products of the nibble's
@@ -622,9 +633,9 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
     const double REL = (double)(N + 1) * 0x1p-50;
     const double ABS = (double)(N + 1) * 0x1p-39;
     int j = klo;   /* first window word whose checkpoint reaches u (checkpoints ascend) */
-    for (int k = klo; k < khi; ++k) j += (ck[k * ckstride] * inv < u) ? 1 : 0;
+        for (int k = klo; k < khi; ++k) j += (ck[k * ckstride] * inv < u) ? 1 : 0;
     double y = y0;
-    for (int k = klo; k < j; ++k) {   /* words before j are full (only the walk's last word is partial) */
+        for (int k = klo; k < j; ++k) {   /* words before j are full (only the walk's last word is partial) */
       const uint32_t ww = walk_word(Pm, M, N, NW, rev, k);
 #pragma unroll
       for (int g = 0; g < 8; ++g) y = y * T4[80 + ((ww >> (4 * g)) & 15u)];
@@ -690,6 +701,175 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
   else if (res < o) { int O = POo - POp; int Z = (o - res) - O; dt0 = -Z; df0 = Z; dt1 = O; df1 = -O; }
   else { int O = POp - POo; int Z = (res - o) - O; dt0 = Z; df0 = -Z; dt1 = -O; df1 = O; }
   return res;
+}
+
+/* ---- static-size Gibbs draw (columns of <= NWM words held in registers) ----------------- */
+/* element idx of a register array, idx block-uniform but not a compile-time constant */
+template <int NWM, typename T>
+__device__ __forceinline__ T sel_u(const T (&a)[NWM], int idx)
+{
+  T v = a[0];
+#pragma unroll
+  for (int k = 1; k < NWM; ++k) v = (idx == k) ? a[k] : v;
+  return v;
+}
+
+/* ones among walk entries [0, w) of the walk words wk[] */
+template <int NWM>
+__device__ __forceinline__ int walk_prefix_s(const uint32_t (&wk)[NWM], int w)
+{
+  int s = 0;
+#pragma unroll
+  for (int k = 0; k < NWM; ++k) {
+    const int lo = 32 * k;
+    const uint32_t m = (w >= lo + 32) ? 0xffffffffu : ((w > lo) ? ((1u << (w - lo)) - 1u) : 0u);
+    s += __popc(wk[k] & m);
+  }
+  return s;
+}
+
+/* draw_fast with the walk words in registers, fully unrolled and branch-free (the measured cost
+ * of a loop trip with a taken branch on gfx950 is ~36 cycles, more than the work it guards).
+ * Same approximation and certification as draw_fast; fallback to draw_exact on failure. */
+template <int NWM>
+__device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint32_t *Pm, int M, int N, bool rev, int o,
+                                           int L, double u, const CD &K, const sr_mtab &tb, double vA, double vB,
+                                           const double *T4, uint64_t *fbk, int &dt0, int &df0, int &dt1, int &df1)
+{
+  const int POo = walk_prefix_s<NWM>(wk, o);
+  const int nk = (L >> 5) + 1;
+  /* pass 0: window of words that can hold mass above 2^-40 relative to entry o */
+  int klo = NWM, khi = -1;
+  double qlo = 0.0;
+  {
+    int O = 0;
+#pragma unroll
+    for (int k = 0; k < NWM; ++k) {
+      const int nb = min(32, L + 1 - 32 * k);
+      const uint32_t vm = (nb >= 32) ? 0xffffffffu : ((nb > 0) ? ((1u << nb) - 1u) : 0u);
+      const int w0 = 32 * k;
+      const double qs = (w0 <= o) ? ((double)((o - w0) - (POo - O)) * vA + (double)(POo - O) * vB)
+                                  : -((double)((w0 - o) - (O - POo)) * vA + (double)(O - POo) * vB);
+      const int ones = __popc(wk[k] & vm);
+      const double ub = qs - (double)(nb - ones) * vA;
+      const bool in = (k < nk) && ub > -SR_WIN_T;
+      const bool first = in && klo == NWM;
+      qlo = first ? qs : qlo;
+      klo = first ? k : klo;
+      khi = in ? k : khi;
+      O += __popc(wk[k]);
+    }
+  }
+  /* pass 1: S over the window; word-start y and end-of-word checkpoints kept in registers */
+  const double y0 = exp2_split(qlo);
+  double S = 0.0;
+  double ckr[NWM], yst[NWM];
+  {
+    double y = y0;
+#pragma unroll
+    for (int k = 0; k < NWM; ++k) {
+      const bool act = k >= klo && k <= khi;
+      const int nbe = act ? min(32, L + 1 - 32 * k) : 0;
+      yst[k] = y;
+      double yk = y;
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        const uint32_t nib = (wk[k] >> (4 * g)) & 15u;
+        const int c = min(max(nbe - 4 * g, 0), 4);
+        S = __builtin_fma(yk, T4[c * 16 + nib], S);
+        yk = yk * T4[80 + nib];
+      }
+      y = act ? yk : y;
+      ckr[k] = S;
+    }
+  }
+  /* pass 2: locate the word, then the group and entry where u falls; certify */
+  int res = -1;
+  if (S > 0.0 && S < 0x1p1000) {
+    const double inv = 1.0 / S;
+    const double REL = (double)(N + 1) * 0x1p-50;
+    const double ABS = (double)(N + 1) * 0x1p-39;
+    int j = klo;
+#pragma unroll
+    for (int k = 0; k < NWM; ++k) j += (k >= klo && k < khi && ckr[k] * inv < u) ? 1 : 0;
+    double Sp0 = 0.0, y = yst[0];
+    uint32_t ww = wk[0];
+#pragma unroll
+    for (int k = 0; k < NWM; ++k) {
+      if (k == j) { y = yst[k]; ww = wk[k]; }
+      if (k + 1 == j && j > klo) Sp0 = ckr[k];
+    }
+    const int w0 = 32 * j;
+    const int nb = min(32, L + 1 - w0);
+    const int nvg = (nb + 3) >> 2;
+    double gsum[8], gy[8];
+    int ng = 0;
+    {
+      double yy = y, acc = Sp0;
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        const uint32_t nib = (ww >> (4 * g)) & 15u;
+        const int c = min(max(nb - 4 * g, 0), 4);
+        gy[g] = yy;
+        acc = __builtin_fma(yy, T4[c * 16 + nib], acc);
+        gsum[g] = acc;
+        yy = yy * T4[80 + nib];
+      }
+#pragma unroll
+      for (int g = 0; g < 8; ++g) ng += (g < nvg && gsum[g] * inv < u) ? 1 : 0;
+    }
+    const int gsel = min(ng, nvg - 1);
+    double base = Sp0, ys = y;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      if (g == gsel) ys = gy[g];
+      if (g + 1 == gsel) base = gsum[g];
+    }
+    const uint32_t nibs = (ww >> (4 * gsel)) & 15u;
+    const int cmax = min(nb - 4 * gsel, 4);
+    const double P1 = __builtin_fma(ys, T4[16 + nibs], base), P2 = __builtin_fma(ys, T4[32 + nibs], base);
+    const double P3 = __builtin_fma(ys, T4[48 + nibs], base), P4 = __builtin_fma(ys, T4[64 + nibs], base);
+    const int nc = ((cmax > 1 && P1 * inv < u) ? 1 : 0) + ((cmax > 2 && P2 * inv < u) ? 1 : 0) +
+                   ((cmax > 3 && P3 * inv < u) ? 1 : 0);
+    const double Ph = (nc == 0) ? P1 : (nc == 1) ? P2 : (nc == 2) ? P3 : P4;
+    const double Pp = (nc == 0) ? base : (nc == 1) ? P1 : (nc == 2) ? P2 : P3;
+    const int w = w0 + 4 * gsel + nc;
+    const double t = u - Ph * inv, tprev = u - Pp * inv;
+    const double e = 2.0 * REL * fmin(Ph, S - Ph) * inv + ABS;
+    const double eprev = 2.0 * REL * fmin(Pp, S - Pp) * inv + ABS;
+    const bool prev_ok = (w == 0) || (tprev > eprev);
+    const bool here_ok = (w == L) || (t < -e);
+    if (prev_ok && here_ok) res = w;
+  }
+  if (res < 0) {
+#ifdef SR_STAMPS
+    atomicAdd((unsigned long long *)fbk, 1ull);
+#endif
+    return draw_exact(Pm, M, N, rev, o, L, u, K, tb, dt0, df0, dt1, df1);
+  }
+  const int POp = walk_prefix_s<NWM>(wk, res);
+  if (res == o) { dt0 = df0 = dt1 = df1 = 0; }
+  else if (res < o) { int O = POo - POp; int Z = (o - res) - O; dt0 = -Z; df0 = Z; dt1 = O; df1 = -O; }
+  else { int O = POp - POo; int Z = (res - o) - O; dt0 = Z; df0 = -Z; dt1 = -O; df1 = O; }
+  return res;
+}
+
+/* the forward and reversed walk words of column m (positions; positions N-1-w), NW <= NWM */
+template <int NWM>
+__device__ __forceinline__ void load_walks(const uint32_t *Pm, int M, int N, int NW, uint32_t (&fw)[NWM], uint32_t (&rw)[NWM])
+{
+#pragma unroll
+  for (int k = 0; k < NWM; ++k) fw[k] = (k < NW) ? Pm[min(k, NW - 1) * M] : 0u;
+  /* reversed word k = brev(column bits [s, s+32)), s = N - 32 - 32k = 32 (q - 1 - k) + r */
+  const int q = N >> 5, r = N & 31;
+#pragma unroll
+  for (int k = 0; k < NWM; ++k) {
+    const int wi = q - 1 - k;
+    const uint32_t lo = (wi >= 0) ? sel_u<NWM, uint32_t>(fw, wi) : 0u;
+    const uint32_t hi = (wi + 1 < NW && wi + 1 >= 0) ? sel_u<NWM, uint32_t>(fw, wi + 1) : 0u;
+    const uint32_t v = r ? ((lo >> r) | (hi << (32 - r))) : lo;
+    rw[k] = (k < NW) ? __brev(v) : 0u;
+  }
 }
 
 /* bits of positions [lo, hi] inside word w */
@@ -946,7 +1126,7 @@ __device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const i
  *   B  Gibbs (a_m, b_m) of own taxa (mcmc_sampleab); [barrier + logl on the last sweep]
  *   C  16 MH permutation proposals: draws, own taxa's count deltas and terms, per-wave
  *      partial sums -> one barrier -> certified decision -> apply to own taxa. */
-template <int TB>
+template <int TB, int NWM>
 __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1093,6 +1273,21 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           /* a_m over [0, b_m], then b_m over the reversed column with limit N - a_new: one
              inlined copy of the draw, two trips */
           int na = a0, nb = b0;
+          if constexpr (NWM > 0) {   /* column in registers, branch-free draws */
+            uint32_t fw[NWM], rw[NWM];
+            load_walks<NWM>(Pm, M, N, NW, fw, rw);
+            for (int pass = 0; pass < 2; ++pass) {
+              int d0, e0, d1, e1;
+              const bool rev = pass != 0;
+              uint32_t wk[NWM];
+#pragma unroll
+              for (int k = 0; k < NWM; ++k) wk[k] = rev ? rw[k] : fw[k];
+              const int res = draw_fast_s<NWM>(wk, Pm, M, N, rev, rev ? N - b0 : a0, rev ? N - na : b0, rev ? ub : ua, K,
+                                               tb, vA, vB, T4w, &misc[MS_FBK], d0, e0, d1, e1);
+              t0 += d0; f0 += e0; t1 += d1; f1 += e1;
+              if (rev) nb = N - res; else na = res;
+            }
+          } else
           for (int pass = 0; pass < 2; ++pass) {
             int d0, e0, d1, e1;
             const bool rev = pass != 0;
@@ -1621,7 +1816,12 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   STAMP_STORE(A.dbg);
 #ifdef SR_STAMPS
   if (tid == 0) { A.dbg[blockIdx.x * 17 * 8 + 0] += misc[MS_NEXACT]; for (int q_ = 0; q_ < 4; ++q_) A.dbg[blockIdx.x * 17 * 8 + 1 + q_] += misc[MS_FBK + q_];
-                  for (int q_ = 0; q_ < 3; ++q_) A.dbg[blockIdx.x * 17 * 8 + 5 + q_] += misc[40 + q_]; }
+                  for (int q_ = 0; q_ < 3; ++q_) A.dbg[blockIdx.x * 17 * 8 + 5 + q_] += misc[40 + q_];
+#ifdef SR_STAMP_GIBBS
+                  for (int q_ = 0; q_ < 3; ++q_) A.dbg[blockIdx.x * 17 * 8 + 5 + q_] = misc[MS_FBK + 26 + q_];
+                  A.dbg[blockIdx.x * 17 * 8 + 4] = misc[MS_FBK + 29];
+#endif
+                }
 #endif
   __syncthreads();
   uint32_t *oP = A.P + (size_t)chain * NW * M;
@@ -1666,11 +1866,15 @@ struct srk_dev {
 
 typedef void (*sr_kfn)(KArgs);
 
-static sr_kfn sr_pick_kernel(int TB)
+/* NWM: walks of <= 9 / 17 words (N + 1 entries: N <= 287 / 543) use the register-resident
+ * Gibbs draw, longer ones the LDS walk */
+static int sr_nwm(int N) { const int nk = (N >> 5) + 1; return nk <= 9 ? 9 : (nk <= 17 ? 17 : 0); }
+static sr_kfn sr_pick_kernel(int TB, int N)
 {
-  if (TB == 256) return (sr_kfn)sr_sweep_kernel<256>;
-  if (TB == 512) return (sr_kfn)sr_sweep_kernel<512>;
-  if (TB == 1024) return (sr_kfn)sr_sweep_kernel<1024>;
+  const int nwm = sr_nwm(N);
+  if (TB == 256) return nwm == 9 ? (sr_kfn)sr_sweep_kernel<256, 9> : nwm == 17 ? (sr_kfn)sr_sweep_kernel<256, 17> : (sr_kfn)sr_sweep_kernel<256, 0>;
+  if (TB == 512) return nwm == 9 ? (sr_kfn)sr_sweep_kernel<512, 9> : nwm == 17 ? (sr_kfn)sr_sweep_kernel<512, 17> : (sr_kfn)sr_sweep_kernel<512, 0>;
+  if (TB == 1024) return (sr_kfn)sr_sweep_kernel<1024, 0>;
   return nullptr;
 }
 
@@ -1703,7 +1907,7 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
   d->device = device; d->N = st->N; d->M = st->M; d->NW = st->NW; d->nh = st->nh; d->nchains = st->nchains;
   int TB = block_threads;
   if (TB <= 0) { TB = 256; while (TB < st->M && TB < 1024) TB *= 2; }
-  if (!sr_pick_kernel(TB)) { delete d; return -6; }
+  if (!sr_pick_kernel(TB, st->N)) { delete d; return -6; }
   d->TB = TB; d->TPT = 1;
   Lay L = sr_layout(st->N, st->M, st->NW, TB);
   d->lds = L.total;
@@ -1727,7 +1931,7 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
   rc |= dev_alloc_copy(d, &A.rec_cdl, (const double *)nullptr, C * d->rec_cap * 3);
   rc |= dev_alloc_copy(d, &A.dbg, (const unsigned long long *)nullptr, C * 17 * 8);
   if (rc) { srk_destroy(d); return -5; }
-  sr_kfn k = sr_pick_kernel(TB);
+  sr_kfn k = sr_pick_kernel(TB, st->N);
   if (hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d->lds) != hipSuccess) {
     srk_destroy(d);
     return -5;
@@ -1754,7 +1958,7 @@ extern "C" int srk_run(srk_dev *d, int calls, int spc, int save, int rec_base)
   HIPCHK(hipSetDevice(d->device));
   KArgs A = d->args;
   A.calls = calls; A.spc = spc; A.save = save; A.rec_base = rec_base;
-  sr_kfn k = sr_pick_kernel(d->TB);
+  sr_kfn k = sr_pick_kernel(d->TB, d->N);
   if (d->have_events) HIPCHK(hipEventRecord(d->ev0, d->stream));
   hipLaunchKernelGGL(k, dim3(d->nchains), dim3(d->TB), d->lds, d->stream, A);
   HIPCHK(hipGetLastError());

@@ -44,3 +44,8 @@ print("  sampleab fallback reasons/sweep: prev %.3f here %.3f S0 %.3f (rest = no
 ev = out[:, 0, 5:8].astype(np.float64).mean(0) / 2 / sweeps
 print("  term evaluations/sweep: pi1 %.2f pi2/swap %.2f pi3 %.2f" % tuple(ev))
 print("  cycles per evaluation (wave-mean): pi1 %.0f pi2/swap %.0f pi3 %.0f" % tuple(per[:, :, 4 + k].mean() / max(ev[k], 1e-9) for k in range(3)))
+if os.environ.get("SR_GIBBS_STATS"):
+    h = out[:, 0, :].astype(np.float64).sum(0)
+    nd = max(h[4], 1)
+    print("  gibbs draws %d: window words/draw %.2f, wave-max window/draw %.2f, walk words/draw %.2f" % (
+        h[4], h[5] / nd, h[6] / (nd / 64), h[7] / nd))

@@ -43,7 +43,7 @@ __constant__ double c_log_lhi[128] = SR_LOG_LHI_INIT;
 __constant__ double c_log_llo[128] = SR_LOG_LLO_INIT;
 
 #ifndef SR_EXP
-#define SR_EXP 0   /* timing experiments only (breaks the sampler): 1 skip proposals, 2 skip Gibbs */
+#define SR_EXP 0   /* timing experiments only (break the sampler): 1 skip proposals, 2 skip Gibbs, 4/8/16 skip pi3/pi2/pi1 terms */
 #endif
 #define SR_ZIGR 3.44428647676
 
@@ -62,7 +62,7 @@ struct KArgs {
 
 /* ---------------------------------------------------------------- LDS carve */
 struct Lay {
-  size_t tab, cbuf, lbuf, mt, P, rpi0, rpi1, ht, ck, ccnt, sab, scnt, hpw, t4, part, tot, xs, misc, total;
+  size_t tab, cbuf, lbuf, mt, P, rpi0, rpi1, ht, ck, ccnt, sab, scnt, hpw, t4, pre, part, tot, xs, misc, total;
 };
 __host__ __device__ static inline size_t sr_al16(size_t x) { return (x + 15) & ~(size_t)15; }
 /* Gibbs checkpoint slots per word: one per thread that owns a taxon */
@@ -86,6 +86,7 @@ __host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB)
   L.scnt = o;  o = sr_al16(o + (size_t)4 * M * 4);
   L.hpw = o;   o = sr_al16(o + (size_t)NWV * SR_NHMAX * 4);           /* per wave: hard positions */
   L.t4 = o;    o = sr_al16(o + (size_t)NWV * 96 * 8);                 /* per wave: 4-entry step tables */
+  L.pre = o;   o = sr_al16(o + (size_t)(NW + 1) * M * 2);             /* column prefix ones per word boundary */
   L.part = o;  o = sr_al16(o + (size_t)2 * 16 * NWV * 8 * 4);         /* [2][proposal][wave] count sums */
   L.tot = o;   o = sr_al16(o + (size_t)2 * NWV * 4 * 4);               /* [2][wave] t0, f0, t1, f1 */
   L.xs = o;    o = sr_al16(o + (size_t)NWV * sizeof(double));          /* per-wave broadcast slot */
@@ -895,6 +896,22 @@ __device__ __forceinline__ void ones_split(const uint32_t *Pm, int M, int lo, in
   }
 }
 
+/* ones of column m at positions [0, x) from the per-word prefix table (pre: column m's entries,
+ * stride M; row k = ones in [0, 32k)) and one partial word */
+__device__ __forceinline__ int col_pre(const uint16_t *prem, const uint32_t *Pm, int M, int x)
+{
+  const int w = x >> 5, bits = x & 31;
+  const uint32_t word = bits ? Pm[w * M] : 0u;
+  return (int)prem[w * M] + __popc(word & ((1u << bits) - 1u));
+}
+/* recompute column m's prefix table (rows 0..NW) */
+__device__ __forceinline__ void col_pre_build(uint16_t *prem, const uint32_t *Pm, int M, int NW)
+{
+  int s = 0;
+  for (int k = 0; k < NW; ++k) { prem[k * M] = (uint16_t)s; s += __popc(Pm[k * M]); }
+  prem[NW * M] = (uint16_t)s;
+}
+
 __device__ __forceinline__ int ininterval(int i, int a, int b, int inc1, int inc2)   /* mcmc.c:1097-1124 */
 {
   int r;
@@ -1017,8 +1034,8 @@ __device__ __forceinline__ uint32_t hard_bits_col(const uint32_t *Pm, int M, int
   return hbm;
 }
 
-__device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, const uint32_t *Pm, int M,
-                                         uint32_t hbm, const int16_t *hcnt, const int16_t *nhall, int &dt0, int &dt1)
+__device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, const uint32_t *Pm, const uint16_t *prem,
+                                         int M, uint32_t hbm, const int16_t *hcnt, const int16_t *nhall, int &dt0, int &dt1)
 {
   const int i = q.i, j = q.j;
   dt0 = 0; dt1 = 0;
@@ -1039,8 +1056,8 @@ __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, 
     const int bin = ininterval(b, i, j + 1, q.inc1, q.inc2);
     if (ain != bin) {
       const int sp = ain ? a : b;
-      int O1, O2;
-      ones_split(Pm, M, i, sp, j + 1, O1, O2);
+      const int c0 = col_pre(prem, Pm, M, i), c1 = col_pre(prem, Pm, M, sp), c2 = col_pre(prem, Pm, M, j + 1);
+      const int O1 = c1 - c0, O2 = c2 - c1;
       const int Z1 = (sp - i) - O1, Z2 = (j + 1 - sp) - O2;
       if (ain) { dt1 = O1 - O2; dt0 = Z2 - Z1; }
       else { dt1 = O2 - O1; dt0 = Z1 - Z2; }
@@ -1069,13 +1086,13 @@ __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, 
     };
     const int wlo = max(a, i), whi = min(b - 1, j);
     const int sizeW = max(0, whi - wlo + 1);
-    const int onesW = ones_range(Pm, M, wlo, whi + 1);
+    const int onesW = (whi >= wlo) ? col_pre(prem, Pm, M, whi + 1) - col_pre(prem, Pm, M, wlo) : 0;
     int onesI = 0, sizeI = 0;
     if (s_lo < s_hi) {
       const int pl = nhall[ri + q.Kn - s_hi], ph = nhall[ri + q.Kn - s_lo - 1];
       int hc;
       const int ho = hard_ones(pl, ph, hc);
-      onesI = ones_range(Pm, M, pl, ph + 1) - ho;
+      onesI = col_pre(prem, Pm, M, ph + 1) - col_pre(prem, Pm, M, pl) - ho;
       sizeI = s_hi - s_lo;
     }
     {
@@ -1093,14 +1110,15 @@ __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, 
 /* The exact delta of one proposal: the reference's per-taxon terms (qval, mcmc.c:1214,
  * 1435, 1630 term order) compacted per 64-taxon chunk into cb, then summed sequentially in
  * ascending m by lane 0 of every wave.  Block-uniform call (contains a barrier). */
-__device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const int32_t *sab, const uint32_t *P, int M, int KT,
+__device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const int32_t *sab, const uint32_t *P, const uint16_t *pre,
+                                              int M, int KT,
                                               int hl, int nh, const int16_t *hcnt, const int16_t *nhall, double *cb, int *cc, double *xs,
                                               int lane, int wave, int TB)
 {
   for (int m0 = wave * 64; m0 < KT * 64; m0 += TB) {
     const int ch = m0 >> 6, m = m0 + lane;
     int dt0 = 0, dt1 = 0;
-    if (m < M) taxon_dt(kind, q, sab[m], sab[M + m], P + m, M, kind == PK_PI3 ? hard_bits_col(P + m, M, hl, nh) : 0u,
+    if (m < M) taxon_dt(kind, q, sab[m], sab[M + m], P + m, pre + m, M, kind == PK_PI3 ? hard_bits_col(P + m, M, hl, nh) : 0u,
                         hcnt, nhall, dt0, dt1);
     const double tv = (m < M) ? qval(dt0, -dt0, dt1, -dt1, K) : 0.0;
     const uint64_t msk = __ballot(tv != 0.0);
@@ -1143,6 +1161,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   uint32_t *P = (uint32_t *)(smem + L.P);
   int32_t *rpiA = (int32_t *)(smem + L.rpi0);
   int32_t *rpiB = (int32_t *)(smem + L.rpi1);
+  uint16_t *pre = (uint16_t *)(smem + L.pre);                        /* column prefix ones */
   int16_t *hcnt = (int16_t *)(smem + L.ht) + wave * (2 * N + 2);    /* this wave's hard-site tables */
   int16_t *nhall = hcnt + N + 1;
   const int CKS = sr_ckstride(M, TB);
@@ -1203,6 +1222,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   __syncthreads();
 
   build_hard_tables(hp, nh, N, hcnt, nhall, lane);
+  for (int m = tid; m < M; m += TB) col_pre_build(pre + m, P + m, M, NW);   /* own columns */
   const double ec = sr_exp_m(SR_LOGEPSILON, &tb);
   const uint32_t nhard = (uint32_t)nh;
   const UDivM mdN = make_udivm((uint32_t)N), mdN1 = make_udivm((uint32_t)(N - 1)), md2 = make_udivm(2u);
@@ -1554,7 +1574,10 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               if (sI >= p0 && sI < pend && !(fl & 4)) {
                 const Prop q = load_prop(sI);
                 int dt0 = 0, dt1 = 0;
-                if (tid < M) taxon_dt(prop_kind(sI), q, a1, b1, P + tid, M, hb1, hcnt, nhall, dt0, dt1);
+                const int kx = prop_kind(sI);
+                const bool skip = ((SR_EXP & 4) && kx == PK_PI3) || ((SR_EXP & 8) && (kx == PK_PI2 || kx == PK_SWAP)) ||
+                                  ((SR_EXP & 16) && kx == PK_PI1);
+                if (tid < M && !skip) taxon_dt(prop_kind(sI), q, a1, b1, P + tid, pre + tid, M, hb1, hcnt, nhall, dt0, dt1);
                 d0s[sI] = dt0; d1s[sI] = dt1;
                 nzs[sI] = __popcll(__ballot((dt0 | dt1) != 0));
               }
@@ -1590,7 +1613,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               const int m = m0 + lane;
               int dt0 = 0, dt1 = 0;
               if (m < M)
-                taxon_dt(kind, q, sab[m], sab[M + m], P + m, M, kind == PK_PI3 ? hard_bits_col(P + m, M, hl, nh) : 0u,
+                taxon_dt(kind, q, sab[m], sab[M + m], P + m, pre + m, M, kind == PK_PI3 ? hard_bits_col(P + m, M, hl, nh) : 0u,
                          hcnt, nhall, dt0, dt1);
               x0 += dt0; x1 += dt1; y0 += abs(dt0); y1 += abs(dt1);
               nzc += __popcll(__ballot((dt0 | dt1) != 0));
@@ -1670,7 +1693,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               }
             }
             if (!decided || (accept && want_logl && !have_exact)) {   /* the exact sequential delta */
-              dl = sr_exact_delta(kind, q, K, sab, P, M, KT, hl, nh, hcnt, nhall, cbuf + xpar * KT * 64, ccnt + xpar * KT,
+              dl = sr_exact_delta(kind, q, K, sab, P, pre, M, KT, hl, nh, hcnt, nhall, cbuf + xpar * KT * 64, ccnt + xpar * KT,
                                   xs, lane, wave, TB);
               xpar ^= 1;
               if (!decided) {
@@ -1709,7 +1732,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             uint32_t *Pm = P + m;
             const int a = sab[m], b = sab[M + m];
             int dt0, dt1;
-            taxon_dt(kind, q, a, b, Pm, M, kind == PK_PI3 ? hard_bits_col(Pm, M, hl, nh) : 0u, hcnt, nhall, dt0, dt1);
+            taxon_dt(kind, q, a, b, Pm, pre + m, M, kind == PK_PI3 ? hard_bits_col(Pm, M, hl, nh) : 0u, hcnt, nhall, dt0, dt1);
             scnt[m] += dt0; scnt[M + m] -= dt0; scnt[2 * M + m] += dt1; scnt[3 * M + m] -= dt1;
             if (kind == PK_PI1) {                                  /* mcmc.c:1266-1297 */
               if (i < j) {
@@ -1759,6 +1782,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 }
               }
             }
+            col_pre_build(pre + m, Pm, M, NW);   /* the column moved: refresh its prefix table */
           }
           /* rpi (double-buffered full permutation, read only at save time) and hard positions */
           {

@@ -62,7 +62,7 @@ struct KArgs {
 
 /* ---------------------------------------------------------------- LDS carve */
 struct Lay {
-  size_t tab, cbuf, lbuf, mt, P, rpi0, rpi1, ht, ck, ccnt, sab, scnt, hpw, t4, pre, part, tot, xs, misc, total;
+  size_t tab, cbuf, lbuf, mt, P, rpi0, rpi1, ht, ck, ccnt, sab, scnt, hpw, hbw, t4, pre, part, tot, xs, misc, total;
 };
 __host__ __device__ static inline size_t sr_al16(size_t x) { return (x + 15) & ~(size_t)15; }
 /* Gibbs checkpoint slots per word: one per thread that owns a taxon */
@@ -85,6 +85,7 @@ __host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB)
   L.sab = o;   o = sr_al16(o + (size_t)2 * M * 4);
   L.scnt = o;  o = sr_al16(o + (size_t)4 * M * 4);
   L.hpw = o;   o = sr_al16(o + (size_t)NWV * SR_NHMAX * 4);           /* per wave: hard positions */
+  L.hbw = o;   o = sr_al16(o + (size_t)NWV * NW * 4);                 /* per wave: hard bitmap */
   L.t4 = o;    o = sr_al16(o + (size_t)NWV * 96 * 8);                 /* per wave: 4-entry step tables */
   L.pre = o;   o = sr_al16(o + (size_t)(NW + 1) * M * 2);             /* column prefix ones per word boundary */
   L.part = o;  o = sr_al16(o + (size_t)2 * 16 * NWV * 8 * 4);         /* [2][proposal][wave] count sums */
@@ -908,7 +909,16 @@ __device__ __forceinline__ int col_pre(const uint16_t *prem, const uint32_t *Pm,
 __device__ __forceinline__ void col_pre_build(uint16_t *prem, const uint32_t *Pm, int M, int NW)
 {
   int s = 0;
-  for (int k = 0; k < NW; ++k) { prem[k * M] = (uint16_t)s; s += __popc(Pm[k * M]); }
+  for (int k0 = 0; k0 < NW; k0 += 8) {   /* 8 independent loads per round */
+    uint32_t wv[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) wv[t] = Pm[min(k0 + t, NW - 1) * M];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      if (k0 + t < NW) prem[(k0 + t) * M] = (uint16_t)s;
+      s += (k0 + t < NW) ? __popc(wv[t]) : 0;
+    }
+  }
   prem[NW * M] = (uint16_t)s;
 }
 
@@ -1003,13 +1013,18 @@ struct Prop { int i, j, ii, jj, inc1, inc2, Kn, r0; };   /* r0: non-hard rank of
 
 /* Per-wave hard-site tables (hard positions hp[] ascending): hcnt[x] = #hard positions < x
  * (x = 0..N), nhall[r] = position of the r-th non-hard position.  Rebuilt whenever hp moves. */
-__device__ __forceinline__ void build_hard_tables(const int *hp, int nh, int N, int16_t *hcnt, int16_t *nhall, int lane)
+__device__ __forceinline__ void build_hard_tables(const int *hp, int nh, int N, int NW, uint32_t *hbw, int16_t *hcnt,
+                                                  int16_t *nhall, int lane)
 {
+  /* hard bitmap (hbw: this wave's NW words, NW <= 64), then ranks by ballot over positions */
+  if (lane < NW) hbw[lane] = 0u;
+  wsync();
+  if (lane < nh) { const int h = hp[lane]; atomicOr(&hbw[h >> 5], 1u << (h & 31)); }
+  wsync();
   int base = 0;
   for (int x0 = 0; x0 <= N; x0 += 64) {
     const int x = x0 + lane;
-    bool h = false;
-    for (int k = 0; k < nh; ++k) h |= (hp[k] == x);
+    const bool h = (x < N) && ((hbw[min(x, N - 1) >> 5] >> (x & 31)) & 1u);
     const uint64_t msk = __ballot(h && x < N);
     const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
     if (x <= N) hcnt[x] = (int16_t)(base + below);
@@ -1027,9 +1042,17 @@ __device__ __forceinline__ void build_hard_tables(const int *hp, int nh, int N, 
 __device__ __forceinline__ uint32_t hard_bits_col(const uint32_t *Pm, int M, int hl, int nh)
 {
   uint32_t hbm = 0;
-  for (int k = 0; k < nh; ++k) {
-    const int h = __builtin_amdgcn_readlane(hl, k);
-    hbm |= ((Pm[(h >> 5) * M] >> (h & 31)) & 1u) << k;
+  if (nh > 0) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {   /* independent loads, one round trip */
+      const int h = __builtin_amdgcn_readlane(hl, min(k, nh - 1));
+      const uint32_t bit = (Pm[(h >> 5) * M] >> (h & 31)) & 1u;
+      hbm |= (k < nh ? bit : 0u) << k;
+    }
+    for (int k = 16; k < nh; ++k) {
+      const int h = __builtin_amdgcn_readlane(hl, k);
+      hbm |= ((Pm[(h >> 5) * M] >> (h & 31)) & 1u) << k;
+    }
   }
   return hbm;
 }
@@ -1170,6 +1193,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   int32_t *sab = (int32_t *)(smem + L.sab);     /* a[M], b[M] */
   int32_t *scnt = (int32_t *)(smem + L.scnt);   /* t0[M], f0[M], t1[M], f1[M] */
   int *hp = (int *)(smem + L.hpw) + wave * SR_NHMAX;   /* this wave's copy of the hard positions */
+  uint32_t *hbw = (uint32_t *)(smem + L.hbw) + wave * NW;   /* this wave's hard bitmap */
   double *T4w = (double *)(smem + L.t4) + wave * 96;     /* this wave's 4-step tables */
   int *part = (int *)(smem + L.part);
   int *tot = (int *)(smem + L.tot);
@@ -1221,7 +1245,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   int xpar = 0;     /* parity of the double-buffered exact-delta term lists */
   __syncthreads();
 
-  build_hard_tables(hp, nh, N, hcnt, nhall, lane);
+  build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane);
   for (int m = tid; m < M; m += TB) col_pre_build(pre + m, P + m, M, NW);   /* own columns */
   const double ec = sr_exp_m(SR_LOGEPSILON, &tb);
   const uint32_t nhard = (uint32_t)nh;
@@ -1811,7 +1835,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             }
             rcur ^= 1;
           }
-          if (kind != PK_PI3) { wsync(); build_hard_tables(hp, nh, N, hcnt, nhall, lane); }   /* hard sites may have moved */
+          if (kind != PK_PI3) { wsync(); build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane); }   /* hard sites may have moved */
           wsync();
           STAMP(7);
         } /* batches */

@@ -174,12 +174,13 @@ class Session:
 
 
 def run_chains(dataset, seeds, burnin_calls=1000, sample_calls=1000, sweeps_per_call=10, device=0,
-               chain_ids=None, keep_records=False, calls_per_launch=0):
+               chain_ids=None, keep_records=False, calls_per_launch=0, block_threads=0):
     """sr_run_chains: returns (summaries list of dicts, records or None).
     records = (ab_pi int32 [n, ts, 2M+N], cdl [n, ts, 3]) when keep_records."""
     n = len(seeds)
     specs = make_specs(seeds, chain_ids)
-    opts = make_opts(burnin_calls, sample_calls, sweeps_per_call, device, calls_per_launch=calls_per_launch)
+    opts = make_opts(burnin_calls, sample_calls, sweeps_per_call, device, block_threads=block_threads,
+                     calls_per_launch=calls_per_launch)
     out = (L.sr_chain_summary * n)()
     N, M = dataset.N, dataset.M
     recs = None

@@ -38,6 +38,29 @@ def algorithmic_bytes_per_iter(N, M):
     return N * M + 192 * M
 
 
+def measured_traffic(N, M, chains, sweeps_per_step):
+    """HBM bytes per sweep-kernel launch from the newest PMC summary in profiles/ whose workload
+    matches (tools/pmc_summary.py: 2*FETCH_SIZE + WRITE_SIZE from separate rocprofv3 --pmc passes
+    over this bench).  None when no matching PMC pass exists."""
+    import glob
+    best = None
+    for p in glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")):
+        try:
+            with open(p) as fh:
+                t = json.load(fh)
+            w = t.get("workload") or {}
+            if (w.get("sites"), w.get("taxa"), w.get("chains_per_gpu"), w.get("sweeps_per_step")) != \
+                    (N, M, chains, sweeps_per_step) or "traffic_bytes_per_launch" not in t:
+                continue
+            if best is None or os.path.getmtime(p) > best[0]:
+                best = (os.path.getmtime(p), p, t)
+        except (OSError, ValueError):
+            continue
+    if best is None:
+        return None, None
+    return best[2]["traffic_bytes_per_launch"], os.path.relpath(best[1], ROOT)
+
+
 def _cpu_worker(args):
     text, seed, calls = args
     import oracle_ref
@@ -75,6 +98,10 @@ def main():
     ap.add_argument("--chains-per-gpu", type=int, default=100)
     ap.add_argument("--calls-per-step", type=int, default=10)
     ap.add_argument("--dataset", default=SYNTH)
+    ap.add_argument("--sites", type=int, default=0, help="synthetic N x M instead of --dataset "
+                    "(seed 20261015 for 256x512, 20261016 otherwise: SURVEY.md 8(d) configs 3 and 5)")
+    ap.add_argument("--taxa", type=int, default=0)
+    ap.add_argument("--columns", default="auto", choices=("auto", "lds", "hbm"))
     ap.add_argument("--cpu-calls", type=int, default=800)
     ap.add_argument("--cpu-workers", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -85,7 +112,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
-    if not os.path.exists(args.dataset):
+    if args.sites and args.taxa:
+        import tempfile
+        import gen_synthetic
+        seed = 20261015 if (args.sites, args.taxa) == (256, 512) else 20261016
+        args.dataset = os.path.join(tempfile.gettempdir(), "sr_synth_%dx%d_%d.txt" % (args.sites, args.taxa, seed))
+        if not os.path.exists(args.dataset):
+            gen_synthetic.write(args.sites, args.taxa, seed, args.dataset)
+    elif not os.path.exists(args.dataset):
         import gen_synthetic
         gen_synthetic.write(256, 512, 20261015, args.dataset)
 
@@ -108,13 +142,13 @@ def main():
     else:
         torch.cuda.set_device(local_rank)
 
-    ds = sa.Dataset.load(args.dataset)
+    ds = sa.Dataset.load(args.dataset, maxs=0)
     C = args.chains_per_gpu
     # weak scaling: C chains per rank, rank r owns chains [r*C, (r+1)*C) (sd.shard), seed = id + 1
     chain_ids = list(sd.shard(C * world, world, rank))
     seeds = [i + 1 for i in chain_ids]
     sess = sa.Session(ds, seeds, device=local_rank, calls_per_launch=args.calls_per_step,
-                      block_threads=args.block_threads, chain_ids=chain_ids)
+                      block_threads=args.block_threads, chain_ids=chain_ids, columns=args.columns)
     stream = torch.cuda.current_stream()
     sess.set_stream(stream.cuda_stream)
     cps = args.calls_per_step
@@ -161,6 +195,7 @@ def main():
     B = algorithmic_bytes_per_iter(ds.N, ds.M)
     launch_bytes = C * sweeps_per_step * B
     achieved = launch_bytes / (kernel_ms / 1e3) / 1e9
+    traffic, traffic_src = measured_traffic(ds.N, ds.M, C, sweeps_per_step)
     out = {
         "metric": "chain-iterations/sec (100 chains, 256x512 matrix) at 1/2/4/8 MI355X",
         "value": value,
@@ -175,11 +210,14 @@ def main():
         "dtype": "f64",
         "data": "synthetic",
         "config": {
-            "workload": "synthetic %dx%d (tools/gen_synthetic.py seed 20261015), %d chains per GPU, "
+            "workload": "%s %dx%d, %d chains per GPU, "
                         "%d mcmc_sample calls (%d sweeps) per chain per step, one saved record per call"
-                        % (ds.N, ds.M, C, cps, sweeps_per_step),
+                        % ("synthetic (tools/gen_synthetic.py seed %d)" % (20261015 if (ds.N, ds.M) == (256, 512)
+                                                                          else 20261016)
+                           if args.dataset == SYNTH or args.sites else os.path.basename(args.dataset),
+                           ds.N, ds.M, C, cps, sweeps_per_step),
             "sites": ds.N, "taxa": ds.M, "chains": total_chains, "chains_per_gpu": C,
-            "sweeps_per_step": sweeps_per_step, "block_threads": sess.block_threads,
+            "sweeps_per_step": sweeps_per_step, "block_threads": sess.block_threads, "columns": sess.variant,
             "parallelism": "chains sharded over %d GPU(s), RCCL all-gather at end" % world,
         },
         "roofline": {
@@ -188,7 +226,9 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_unit": "bytes per launch (HBM, PMC)",
+            "traffic_source": traffic_src,
             "kernel": "sr_sweep_kernel",
             "kernel_ms": kernel_ms,
             "bytes_per_chain_iteration": B,

@@ -64,6 +64,8 @@ typedef struct {
   int32_t flags;             /* SR_F_* */
 } sr_run_opts;
 #define SR_F_NO_CHECK 1      /* skip the closing mcmc_consistent check */
+#define SR_F_HBM_COLUMNS 2   /* force the HBM-column kernel variant (default: only when LDS is too small) */
+#define SR_F_LDS_COLUMNS 4   /* force the LDS-column variant (SR_EUNSUPPORTED if it does not fit) */
 
 typedef struct {
   int32_t chain_id;
@@ -116,6 +118,9 @@ int sr_session_accept_counts(sr_session *s, int32_t chain, int64_t *acc7);
 /* Device time of the last sr_session_run (ms, HIP events on the session stream; syncs). */
 double sr_session_last_kernel_ms(sr_session *s);
 int32_t sr_session_block_threads(const sr_session *s);
+/* Kernel variant the session runs: 0 = occurrence columns in LDS, 1 = columns in HBM
+ * (chosen when the LDS layout exceeds 160 KB, e.g. 1024 sites x 2048 taxa). */
+int32_t sr_session_variant(const sr_session *s);
 void sr_session_destroy(sr_session *s);
 
 const char *sr_strerror(int code);

@@ -58,6 +58,8 @@ struct KArgs {
   int16_t *rec_abpi;
   double *rec_cdl;
   unsigned long long *dbg;   /* SR_STAMPS builds: [chain][16] cycles per phase */
+  uint16_t *gpre;            /* gm variant scratch, per chain: column prefix tables */
+  double *gck, *glbuf, *gcbuf;   /* gm variant scratch: Gibbs checkpoints, logl terms, exact-delta terms */
 };
 
 /* ---------------------------------------------------------------- LDS carve */
@@ -67,27 +69,31 @@ struct Lay {
 __host__ __device__ static inline size_t sr_al16(size_t x) { return (x + 15) & ~(size_t)15; }
 /* Gibbs checkpoint slots per word: one per thread that owns a taxon */
 __host__ __device__ static inline int sr_ckstride(int M, int TB) { return M >= TB ? TB : ((M + 63) & ~63); }
-__host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB)
+/* gm: the global-memory variant (columns too large for LDS, e.g. 1024 x 2048): the per-taxon
+ * arrays (P, pre, ck, a/b, counts, logl terms, exact-delta terms) live in HBM (chain-private,
+ * owner-thread access, L2/MALL-resident) and get no LDS slot */
+__host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB, bool gm)
 {
   Lay L;
   size_t o = 0;
   const int KT = (M + 63) / 64, NWV = TB / 64;
+  const size_t g = gm ? 0 : 1;
   L.tab = o;   o = sr_al16(o + 640 * sizeof(double));
-  L.cbuf = o;  o = sr_al16(o + (size_t)2 * KT * 64 * sizeof(double));   /* [2][KT*64] by proposal parity */
-  L.lbuf = o;  o = sr_al16(o + (size_t)M * sizeof(double));
+  L.cbuf = o;  o = sr_al16(o + g * 2 * KT * 64 * sizeof(double));       /* [2][KT*64] by proposal parity */
+  L.lbuf = o;  o = sr_al16(o + g * M * sizeof(double));
   L.mt = o;    o = sr_al16(o + (size_t)SR_RING * SR_MT_N * 4);
-  L.P = o;     o = sr_al16(o + (size_t)NW * M * 4);
+  L.P = o;     o = sr_al16(o + g * NW * M * 4);
   L.rpi0 = o;  o = sr_al16(o + (size_t)N * 4);
   L.rpi1 = o;  o = sr_al16(o + (size_t)N * 4);
   L.ht = o;    o = sr_al16(o + (size_t)NWV * (2 * N + 2) * 2);           /* per wave: hcnt[N+1], nhall[N] (int16) */
-  L.ck = o;    o = sr_al16(o + (size_t)((N >> 5) + 1) * sr_ckstride(M, TB) * sizeof(double));
+  L.ck = o;    o = sr_al16(o + g * ((N >> 5) + 1) * sr_ckstride(M, TB) * sizeof(double));
   L.ccnt = o;  o = sr_al16(o + (size_t)2 * KT * 4);
-  L.sab = o;   o = sr_al16(o + (size_t)2 * M * 4);
-  L.scnt = o;  o = sr_al16(o + (size_t)4 * M * 4);
+  L.sab = o;   o = sr_al16(o + g * 2 * M * 4);
+  L.scnt = o;  o = sr_al16(o + g * 4 * M * 4);
   L.hpw = o;   o = sr_al16(o + (size_t)NWV * SR_NHMAX * 4);           /* per wave: hard positions */
   L.hbw = o;   o = sr_al16(o + (size_t)NWV * NW * 4);                 /* per wave: hard bitmap */
   L.t4 = o;    o = sr_al16(o + (size_t)NWV * 96 * 8);                 /* per wave: 4-entry step tables */
-  L.pre = o;   o = sr_al16(o + (size_t)(NW + 1) * M * 2);             /* column prefix ones per word boundary */
+  L.pre = o;   o = sr_al16(o + g * (NW + 1) * M * 2);                 /* column prefix ones per word boundary */
   L.part = o;  o = sr_al16(o + (size_t)2 * 16 * NWV * 8 * 4);         /* [2][proposal][wave] count sums */
   L.tot = o;   o = sr_al16(o + (size_t)2 * NWV * 4 * 4);               /* [2][wave] t0, f0, t1, f1 */
   L.xs = o;    o = sr_al16(o + (size_t)NWV * sizeof(double));          /* per-wave broadcast slot */
@@ -95,6 +101,10 @@ __host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB)
   L.total = o;
   return L;
 }
+/* per-chain HBM scratch of the gm variant (elements): pre u16, ck f64, lbuf f64, cbuf f64 */
+__host__ __device__ static inline size_t sr_gm_pre(int M, int NW) { return (size_t)(NW + 1) * M; }
+__host__ __device__ static inline size_t sr_gm_ck(int N, int M, int TB) { return (size_t)((N >> 5) + 1) * sr_ckstride(M, TB); }
+__host__ __device__ static inline size_t sr_gm_cbuf(int M) { return (size_t)2 * ((M + 63) / 64) * 64; }
 /* misc slots (8-byte words) */
 #define MS_TOT 0      /* 4 ints in 2 words */
 #define MS_DELTA 2
@@ -1167,7 +1177,7 @@ __device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const i
  *   B  Gibbs (a_m, b_m) of own taxa (mcmc_sampleab); [barrier + logl on the last sweep]
  *   C  16 MH permutation proposals: draws, own taxa's count deltas and terms, per-wave
  *      partial sums -> one barrier -> certified decision -> apply to own taxa. */
-template <int TB, int NWM>
+template <int TB, int NWM, bool GM>
 __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1176,22 +1186,24 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   const int chain = blockIdx.x;
   const int N = A.N, M = A.M, NW = A.NW, nh = A.nh;
   const int KT = (M + 63) >> 6;
-  const Lay L = sr_layout(N, M, NW, TB);
+  const Lay L = sr_layout(N, M, NW, TB, GM);
   double *tabs = (double *)(smem + L.tab);
-  double *cbuf = (double *)(smem + L.cbuf);
-  double *lbuf = (double *)(smem + L.lbuf);
+  /* GM: the per-taxon arrays are the chain's HBM state itself (P, a/b, counts: updated in
+     place) or its HBM scratch; otherwise LDS copies loaded here and stored at the end */
+  double *cbuf = GM ? A.gcbuf + (size_t)chain * sr_gm_cbuf(M) : (double *)(smem + L.cbuf);
+  double *lbuf = GM ? A.glbuf + (size_t)chain * M : (double *)(smem + L.lbuf);
   uint32_t *ring = (uint32_t *)(smem + L.mt);
-  uint32_t *P = (uint32_t *)(smem + L.P);
+  uint32_t *P = GM ? A.P + (size_t)chain * NW * M : (uint32_t *)(smem + L.P);
   int32_t *rpiA = (int32_t *)(smem + L.rpi0);
   int32_t *rpiB = (int32_t *)(smem + L.rpi1);
-  uint16_t *pre = (uint16_t *)(smem + L.pre);                        /* column prefix ones */
+  uint16_t *pre = GM ? A.gpre + (size_t)chain * sr_gm_pre(M, NW) : (uint16_t *)(smem + L.pre);   /* column prefix ones */
   int16_t *hcnt = (int16_t *)(smem + L.ht) + wave * (2 * N + 2);    /* this wave's hard-site tables */
   int16_t *nhall = hcnt + N + 1;
   const int CKS = sr_ckstride(M, TB);
-  double *ckb = (double *)(smem + L.ck);
+  double *ckb = GM ? A.gck + (size_t)chain * sr_gm_ck(N, M, TB) : (double *)(smem + L.ck);
   int *ccnt = (int *)(smem + L.ccnt);
-  int32_t *sab = (int32_t *)(smem + L.sab);     /* a[M], b[M] */
-  int32_t *scnt = (int32_t *)(smem + L.scnt);   /* t0[M], f0[M], t1[M], f1[M] */
+  int32_t *sab = GM ? A.ab + (size_t)chain * 2 * M : (int32_t *)(smem + L.sab);     /* a[M], b[M] */
+  int32_t *scnt = GM ? A.cnt + (size_t)chain * 4 * M : (int32_t *)(smem + L.scnt);  /* t0[M], f0[M], t1[M], f1[M] */
   int *hp = (int *)(smem + L.hpw) + wave * SR_NHMAX;   /* this wave's copy of the hard positions */
   uint32_t *hbw = (uint32_t *)(smem + L.hbw) + wave * NW;   /* this wave's hard bitmap */
   double *T4w = (double *)(smem + L.t4) + wave * 96;     /* this wave's 4-step tables */
@@ -1212,15 +1224,15 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   tb.exp_thi = tabs; tb.exp_tlo = tabs + 128; tb.log_invc = tabs + 256; tb.log_lhi = tabs + 384; tb.log_llo = tabs + 512;
   {
     const uint32_t *gP = A.P + (size_t)chain * NW * M;
-    for (int i = tid; i < NW * M; i += TB) P[i] = gP[i];
+    if (!GM) for (int i = tid; i < NW * M; i += TB) P[i] = gP[i];
     const int32_t *grpi = A.rpi + (size_t)chain * N;
     for (int i = tid; i < N; i += TB) rpiA[i] = grpi[i];
     const uint32_t *gmt = A.mt + (size_t)chain * SR_RING * SR_MT_N;
     for (int i = tid; i < SR_RING * SR_MT_N; i += TB) ring[i] = gmt[i];
     const int32_t *gab = A.ab + (size_t)chain * 2 * M;
-    for (int i = tid; i < 2 * M; i += TB) sab[i] = gab[i];
+    if (!GM) for (int i = tid; i < 2 * M; i += TB) sab[i] = gab[i];
     const int32_t *gcnt = A.cnt + (size_t)chain * 4 * M;
-    for (int i = tid; i < 4 * M; i += TB) scnt[i] = gcnt[i];
+    if (!GM) for (int i = tid; i < 4 * M; i += TB) scnt[i] = gcnt[i];
   }
   if (tid == 0) for (int q = MS_CAB; q < 64; ++q) misc[q] = 0;
 
@@ -1305,13 +1317,21 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       STAMP(5);
 #endif
       /* ============ phase B: Gibbs update of own (a_m, b_m) (mcmc_sampleab) */
-      rng_ensure(R, min(2 * M + SR_RNG_SLACK, (SR_RING - 1) * SR_MT_N - (SR_MT_N - 1)), tid, TB);
+      /* taxa in rounds of TB (round r: m = r*TB + tid, words 2(m - r*TB), +1 from the round's
+         cursor), each round's 2*TB words made resident first: the ring holds < 2M words when
+         M > ~1870 (1024 x 2048) */
       {
         unsigned long long nchg = 0;
-        for (int m = tid; m < M && !(SR_EXP & 2); m += TB) {
+        const int rcap = (SR_RING - 1) * SR_MT_N - (SR_MT_N - 1);
+        const int nround = (2 * M + SR_RNG_SLACK <= rcap) ? 1 : (M + TB - 1) / TB;
+        for (int rd = 0; rd < nround; ++rd) {
+        const int mlo = (nround == 1) ? 0 : rd * TB, mhi = (nround == 1) ? M : min(M, mlo + TB);
+        if (rd > 0) __syncthreads();   /* every thread is done with the previous round's words */
+        rng_ensure(R, min(2 * (mhi - mlo) + SR_RNG_SLACK, rcap), tid, TB);
+        for (int m = mlo + tid; m < mhi && !(SR_EXP & 2); m += TB) {
           const uint32_t *Pm = P + m;
-          const double ua = rng_peek(R, 2 * m) / 4294967296.0;
-          const double ub = rng_peek(R, 2 * m + 1) / 4294967296.0;
+          const double ua = rng_peek(R, 2 * (m - mlo)) / 4294967296.0;
+          const double ub = rng_peek(R, 2 * (m - mlo) + 1) / 4294967296.0;
           const int a0 = sab[m], b0 = sab[M + m];
           int t0 = scnt[m], f0 = scnt[M + m], t1 = scnt[2 * M + m], f1 = scnt[3 * M + m];
           /* a_m over [0, b_m], then b_m over the reversed column with limit N - a_new: one
@@ -1347,10 +1367,11 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           if (want_logl)   /* mcmc_logl term (mcmc.c:643-644) */
             lbuf[m] = (double)t0 * K.cc + (double)f0 * K.d + (double)t1 * K.dd + (double)f1 * K.c;
         }
+        rng_skip(R, 2 * (mhi - mlo));
+        }
         const int nw = wave_sum_i32((int)nchg);
         if (lane == 0 && nw) atomicAdd((unsigned long long *)&misc[MS_CAB], (unsigned long long)nw);
       }
-      rng_skip(R, 2 * M);
       STAMP(1);
       if (want_logl) {   /* mcmc_logl (mcmc.c:639-645), sequential over m, lane 0 of every wave */
         __syncthreads();
@@ -1873,16 +1894,16 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 #endif
   __syncthreads();
   uint32_t *oP = A.P + (size_t)chain * NW * M;
-  for (int i = tid; i < NW * M; i += TB) oP[i] = P[i];
+  if (!GM) for (int i = tid; i < NW * M; i += TB) oP[i] = P[i];
   const int32_t *rc = rcur ? rpiB : rpiA;
   int32_t *orpi = A.rpi + (size_t)chain * N;
   for (int i = tid; i < N; i += TB) orpi[i] = rc[i];
   uint32_t *omt = A.mt + (size_t)chain * SR_RING * SR_MT_N;
   for (int i = tid; i < SR_RING * SR_MT_N; i += TB) omt[i] = ring[i];
   int32_t *oab = A.ab + (size_t)chain * 2 * M;
-  for (int i = tid; i < 2 * M; i += TB) oab[i] = sab[i];
+  if (!GM) for (int i = tid; i < 2 * M; i += TB) oab[i] = sab[i];
   int32_t *ocnt = A.cnt + (size_t)chain * 4 * M;
-  for (int i = tid; i < 4 * M; i += TB) ocnt[i] = scnt[i];
+  if (!GM) for (int i = tid; i < 4 * M; i += TB) ocnt[i] = scnt[i];
   if (tid == 0) {
     for (int k = 0; k < nh; ++k) A.hp[(size_t)chain * SR_NHMAX + k] = hp[k];
     A.cdl[(size_t)chain * 4 + 0] = c;
@@ -1901,28 +1922,34 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   fprintf(stderr, "seriation: HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); return -5; } } while (0)
 
 struct srk_dev {
-  int device, N, M, NW, nh, nchains, TB, TPT, rec_cap;
+  int device, N, M, NW, nh, nchains, TB, TPT, rec_cap, gm;
   size_t lds;
   hipStream_t stream;
   int own_stream;
   hipEvent_t ev0, ev1;
   int have_events;
   KArgs args;
-  void *bufs[16];
+  void *bufs[24];
   int nbufs;
 };
 
 typedef void (*sr_kfn)(KArgs);
 
 /* NWM: walks of <= 9 / 17 words (N + 1 entries: N <= 287 / 543) use the register-resident
- * Gibbs draw, longer ones the LDS walk */
+ * Gibbs draw, longer ones the LDS walk.  gm: the HBM-column variant (sr_layout) */
 static int sr_nwm(int N) { const int nk = (N >> 5) + 1; return nk <= 9 ? 9 : (nk <= 17 ? 17 : 0); }
-static sr_kfn sr_pick_kernel(int TB, int N)
+static sr_kfn sr_pick_kernel(int TB, int N, bool gm)
 {
+  if (gm) {
+    if (TB == 256) return (sr_kfn)sr_sweep_kernel<256, 0, true>;
+    if (TB == 512) return (sr_kfn)sr_sweep_kernel<512, 0, true>;
+    if (TB == 1024) return (sr_kfn)sr_sweep_kernel<1024, 0, true>;
+    return nullptr;
+  }
   const int nwm = sr_nwm(N);
-  if (TB == 256) return nwm == 9 ? (sr_kfn)sr_sweep_kernel<256, 9> : nwm == 17 ? (sr_kfn)sr_sweep_kernel<256, 17> : (sr_kfn)sr_sweep_kernel<256, 0>;
-  if (TB == 512) return nwm == 9 ? (sr_kfn)sr_sweep_kernel<512, 9> : nwm == 17 ? (sr_kfn)sr_sweep_kernel<512, 17> : (sr_kfn)sr_sweep_kernel<512, 0>;
-  if (TB == 1024) return (sr_kfn)sr_sweep_kernel<1024, 0>;
+  if (TB == 256) return nwm == 9 ? (sr_kfn)sr_sweep_kernel<256, 9, false> : nwm == 17 ? (sr_kfn)sr_sweep_kernel<256, 17, false> : (sr_kfn)sr_sweep_kernel<256, 0, false>;
+  if (TB == 512) return nwm == 9 ? (sr_kfn)sr_sweep_kernel<512, 9, false> : nwm == 17 ? (sr_kfn)sr_sweep_kernel<512, 17, false> : (sr_kfn)sr_sweep_kernel<512, 0, false>;
+  if (TB == 1024) return (sr_kfn)sr_sweep_kernel<1024, 0, false>;
   return nullptr;
 }
 
@@ -1945,7 +1972,8 @@ static int dev_alloc_copy(srk_dev *d, T **dst, const T *src, size_t n)
   return 0;
 }
 
-extern "C" int srk_create(const sr_state_host *st, int device, int block_threads, int rec_cap_calls, srk_dev **out)
+extern "C" int srk_create(const sr_state_host *st, int device, int block_threads, int rec_cap_calls, int gm_force,
+                          srk_dev **out)
 {
   int ndev = srk_device_count();
   if (ndev <= 0 || device < 0 || device >= ndev) return -5;
@@ -1955,11 +1983,17 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
   d->device = device; d->N = st->N; d->M = st->M; d->NW = st->NW; d->nh = st->nh; d->nchains = st->nchains;
   int TB = block_threads;
   if (TB <= 0) { TB = 256; while (TB < st->M && TB < 1024) TB *= 2; }
-  if (!sr_pick_kernel(TB, st->N)) { delete d; return -6; }
   d->TB = TB; d->TPT = 1;
-  Lay L = sr_layout(st->N, st->M, st->NW, TB);
+  /* columns in LDS when the whole layout fits, else the HBM-column variant */
+  d->gm = 0;
+  Lay L = sr_layout(st->N, st->M, st->NW, TB, false);
+  if (L.total > 160 * 1024) { d->gm = 1; L = sr_layout(st->N, st->M, st->NW, TB, true); }
+  if (gm_force >= 0 && gm_force != d->gm) {   /* explicit variant request (tests) */
+    d->gm = gm_force;
+    L = sr_layout(st->N, st->M, st->NW, TB, d->gm != 0);
+  }
   d->lds = L.total;
-  if (d->lds > 160 * 1024) { delete d; return -6; }
+  if (!sr_pick_kernel(TB, st->N, d->gm != 0) || d->lds > 160 * 1024) { delete d; return -6; }
   d->rec_cap = rec_cap_calls > 0 ? rec_cap_calls : 1;
   const size_t C = st->nchains;
   KArgs &A = d->args;
@@ -1978,8 +2012,14 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
   rc |= dev_alloc_copy(d, &A.rec_abpi, (const int16_t *)nullptr, C * d->rec_cap * (2 * st->M + st->N));
   rc |= dev_alloc_copy(d, &A.rec_cdl, (const double *)nullptr, C * d->rec_cap * 3);
   rc |= dev_alloc_copy(d, &A.dbg, (const unsigned long long *)nullptr, C * 17 * 8);
+  if (d->gm) {
+    rc |= dev_alloc_copy(d, &A.gpre, (const uint16_t *)nullptr, C * sr_gm_pre(st->M, st->NW));
+    rc |= dev_alloc_copy(d, &A.gck, (const double *)nullptr, C * sr_gm_ck(st->N, st->M, TB));
+    rc |= dev_alloc_copy(d, &A.glbuf, (const double *)nullptr, C * st->M);
+    rc |= dev_alloc_copy(d, &A.gcbuf, (const double *)nullptr, C * sr_gm_cbuf(st->M));
+  }
   if (rc) { srk_destroy(d); return -5; }
-  sr_kfn k = sr_pick_kernel(TB, st->N);
+  sr_kfn k = sr_pick_kernel(TB, st->N, d->gm != 0);
   if (hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d->lds) != hipSuccess) {
     srk_destroy(d);
     return -5;
@@ -2006,7 +2046,7 @@ extern "C" int srk_run(srk_dev *d, int calls, int spc, int save, int rec_base)
   HIPCHK(hipSetDevice(d->device));
   KArgs A = d->args;
   A.calls = calls; A.spc = spc; A.save = save; A.rec_base = rec_base;
-  sr_kfn k = sr_pick_kernel(d->TB, d->N);
+  sr_kfn k = sr_pick_kernel(d->TB, d->N, d->gm != 0);
   if (d->have_events) HIPCHK(hipEventRecord(d->ev0, d->stream));
   hipLaunchKernelGGL(k, dim3(d->nchains), dim3(d->TB), d->lds, d->stream, A);
   HIPCHK(hipGetLastError());
@@ -2031,6 +2071,7 @@ extern "C" double srk_last_ms(srk_dev *d)
 }
 
 extern "C" int srk_block_threads(const srk_dev *d) { return d->TB; }
+extern "C" int srk_variant(const srk_dev *d) { return d->gm; }
 
 extern "C" int srk_fetch_dbg(srk_dev *d, unsigned long long *out)
 {

@@ -355,7 +355,8 @@ SR_API int sr_session_create(const sr_dataset *ds, const sr_chain_spec *specs, i
   for (int c = 0; c < n_chains && rc == SR_OK; c++) rc = init_chain(ds, specs[c].seed, &st, c);
   if (rc) { state_free(&st); sr_session_destroy(s); return rc; }
   s->rec_cap = auto_calls_per_launch(&o);
-  rc = srk_create(&st, o.device, o.block_threads, s->rec_cap, &s->dev);
+  const int gm_force = (o.flags & SR_F_HBM_COLUMNS) ? 1 : ((o.flags & SR_F_LDS_COLUMNS) ? 0 : -1);
+  rc = srk_create(&st, o.device, o.block_threads, s->rec_cap, gm_force, &s->dev);
   state_free(&st);
   if (rc) { sr_session_destroy(s); return rc == -6 ? SR_EUNSUPPORTED : SR_EDEVICE; }
   *out = s;
@@ -382,6 +383,7 @@ SR_API int sr_session_sync(sr_session *s) { return (!s) ? SR_EINVAL : (srk_sync(
 SR_API int32_t sr_session_records(const sr_session *s) { return s ? s->nrec : 0; }
 SR_API int32_t sr_session_record_capacity(const sr_session *s) { return s ? s->rec_cap : 0; }
 SR_API int32_t sr_session_block_threads(const sr_session *s) { return s ? srk_block_threads(s->dev) : 0; }
+SR_API int32_t sr_session_variant(const sr_session *s) { return s ? srk_variant(s->dev) : -1; }
 SR_API double sr_session_last_kernel_ms(sr_session *s) { return s ? srk_last_ms(s->dev) : -1.0; }
 
 SR_API int sr_session_fetch_records(sr_session *s, int32_t first, int32_t count, int16_t *ab_pi, double *cdl)

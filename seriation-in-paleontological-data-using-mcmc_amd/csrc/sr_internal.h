@@ -35,13 +35,15 @@ extern "C" {
 #endif
 
 int srk_device_count(void);
-int srk_create(const sr_state_host *st, int device, int block_threads, int rec_cap_calls, srk_dev **out);
+/* gm_force: -1 auto (LDS columns when they fit, else HBM columns), 0 LDS, 1 HBM */
+int srk_create(const sr_state_host *st, int device, int block_threads, int rec_cap_calls, int gm_force, srk_dev **out);
 int srk_set_stream(srk_dev *d, void *stream);
 /* calls*spc sweeps for all chains; save -> records appended at slot rec_base.. */
 int srk_run(srk_dev *d, int calls, int spc, int save, int rec_base);
 int srk_sync(srk_dev *d);
 double srk_last_ms(srk_dev *d);
 int srk_block_threads(const srk_dev *d);
+int srk_variant(const srk_dev *d);   /* 0 LDS columns, 1 HBM columns */
 int srk_fetch_dbg(srk_dev *d, unsigned long long *out);
 int srk_fetch_records(srk_dev *d, int first, int count, int16_t *ab_pi, double *cdl);
 int srk_download_state(srk_dev *d, sr_state_host *st);

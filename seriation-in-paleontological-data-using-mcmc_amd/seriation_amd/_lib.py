@@ -21,6 +21,8 @@ SR_EIO = -7
 SR_EINCONSISTENT = -8
 SR_MAXS = 2000
 SR_F_NO_CHECK = 1
+SR_F_HBM_COLUMNS = 2
+SR_F_LDS_COLUMNS = 4
 
 
 class SrError(RuntimeError):
@@ -67,7 +69,7 @@ PUBLIC_SYMBOLS = [
     "sr_run_chains", "sr_run_to_dirs", "sr_session_create", "sr_session_set_stream",
     "sr_session_run", "sr_session_sync", "sr_session_records", "sr_session_record_capacity",
     "sr_session_fetch_records", "sr_session_reset_records", "sr_session_state",
-    "sr_session_accept_counts", "sr_session_last_kernel_ms", "sr_session_block_threads",
+    "sr_session_accept_counts", "sr_session_last_kernel_ms", "sr_session_block_threads", "sr_session_variant",
     "sr_session_destroy", "sr_strerror", "sr_device_count", "sr_version",
 ]
 
@@ -104,6 +106,7 @@ def _lib():
         "sr_session_accept_counts": (c_int, [c_void_p, c_i32, P(ctypes.c_int64)]),
         "sr_session_last_kernel_ms": (c_double, [c_void_p]),
         "sr_session_block_threads": (c_i32, [c_void_p]),
+        "sr_session_variant": (c_i32, [c_void_p]),
         "sr_session_destroy": (None, [c_void_p]),
         "sr_strerror": (ctypes.c_char_p, [c_int]),
         "sr_device_count": (c_int, []),

@@ -63,7 +63,8 @@ class Dataset:
 
 
 def make_opts(burnin_calls=1000, sample_calls=1000, sweeps_per_call=10, device=0, block_threads=0,
-              calls_per_launch=0, check=True):
+              calls_per_launch=0, check=True, columns="auto"):
+    """columns: "auto" (LDS when the layout fits, else HBM), "lds" or "hbm" (SR_F_*_COLUMNS)."""
     o = L.sr_run_opts()
     L.lib().sr_default_opts(ctypes.byref(o))
     o.burnin_calls = burnin_calls
@@ -72,7 +73,8 @@ def make_opts(burnin_calls=1000, sample_calls=1000, sweeps_per_call=10, device=0
     o.device = device
     o.block_threads = block_threads
     o.calls_per_launch = calls_per_launch
-    o.flags = 0 if check else L.SR_F_NO_CHECK
+    o.flags = (0 if check else L.SR_F_NO_CHECK) | {"auto": 0, "lds": L.SR_F_LDS_COLUMNS,
+                                                   "hbm": L.SR_F_HBM_COLUMNS}[columns]
     return o
 
 
@@ -90,12 +92,12 @@ class Session:
     ``calls`` mcmc_sample calls (mcmc.c:214-258) for every chain."""
 
     def __init__(self, dataset, seeds, device=0, sweeps_per_call=10, calls_per_launch=0, block_threads=0,
-                 chain_ids=None):
+                 chain_ids=None, columns="auto"):
         self.ds = dataset
         self.n = len(seeds)
         self.specs = make_specs(seeds, chain_ids)
         self.opts = make_opts(sweeps_per_call=sweeps_per_call, device=device, block_threads=block_threads,
-                              calls_per_launch=calls_per_launch)
+                              calls_per_launch=calls_per_launch, columns=columns)
         h = ctypes.c_void_p()
         _check(L.lib().sr_session_create(ctypes.byref(dataset.c), self.specs, self.n, ctypes.byref(self.opts),
                                          ctypes.byref(h)), "sr_session_create")
@@ -108,6 +110,11 @@ class Session:
     @property
     def block_threads(self):
         return L.lib().sr_session_block_threads(self.h)
+
+    @property
+    def variant(self):
+        """Kernel variant: "lds" (occurrence columns in LDS) or "hbm" (columns in HBM)."""
+        return "hbm" if L.lib().sr_session_variant(self.h) == 1 else "lds"
 
     def set_stream(self, stream_handle):
         _check(L.lib().sr_session_set_stream(self.h, ctypes.c_void_p(stream_handle)), "set_stream")
@@ -174,13 +181,13 @@ class Session:
 
 
 def run_chains(dataset, seeds, burnin_calls=1000, sample_calls=1000, sweeps_per_call=10, device=0,
-               chain_ids=None, keep_records=False, calls_per_launch=0, block_threads=0):
+               chain_ids=None, keep_records=False, calls_per_launch=0, block_threads=0, columns="auto"):
     """sr_run_chains: returns (summaries list of dicts, records or None).
     records = (ab_pi int32 [n, ts, 2M+N], cdl [n, ts, 3]) when keep_records."""
     n = len(seeds)
     specs = make_specs(seeds, chain_ids)
     opts = make_opts(burnin_calls, sample_calls, sweeps_per_call, device, block_threads=block_threads,
-                     calls_per_launch=calls_per_launch)
+                     calls_per_launch=calls_per_launch, columns=columns)
     out = (L.sr_chain_summary * n)()
     N, M = dataset.N, dataset.M
     recs = None

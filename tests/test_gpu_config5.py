@@ -1,0 +1,41 @@
+"""BASELINE.json configs[4]: synthetic 1024 sites x 2048 taxa (tools/gen_synthetic.py, seed
+20261016, 12 hard sites).  The bit columns (256 KB per chain) exceed the 160 KB LDS, so the
+session runs the HBM-column kernel variant; every saved sample must equal the CPU oracle bit for
+bit.  The reference parser cannot read its 4096-char lines (MAXS = 2000, mcmc.h:25), so the
+dataset is parsed with maxs = 0 on both sides and the oracle is the only reference here."""
+import numpy as np
+import pytest
+
+import gen_synthetic
+import oracle_ref
+import seriation_amd as sa
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def config5():
+    X, hard = gen_synthetic.make(1024, 2048, 20261016)
+    text = gen_synthetic.to_text(X, hard)
+    return text if isinstance(text, bytes) else text.encode()
+
+
+def test_config5_variant_is_hbm(config5):
+    ds = sa.Dataset.parse(config5, maxs=0)
+    assert (ds.N, ds.M) == (1024, 2048)
+    with sa.Session(ds, [1]) as s:
+        assert s.variant == "hbm"
+    with pytest.raises(sa.SrError):
+        sa.Session(ds, [1], columns="lds")
+
+
+def test_config5_parity(config5):
+    ds = sa.Dataset.parse(config5, maxs=0)
+    seeds = [1, 2]
+    summ, (ri, rd) = sa.run_chains(ds, seeds, burnin_calls=1, sample_calls=2, keep_records=True)
+    for k, s in enumerate(seeds):
+        o = oracle_ref.run_chain(config5, s, 1, 2, maxs=0)
+        assert o["rc"] == 0
+        np.testing.assert_array_equal(ri[k], o["rec_int"], err_msg="seed %d" % s)
+        assert np.array_equal(rd[k].view(np.uint64), o["rec_dbl"].view(np.uint64)), s
+        assert summ[k]["consistent"] == 0

@@ -61,3 +61,26 @@ def test_edge_parity(name, N, M, nh, tb):
         np.testing.assert_array_equal(ri[k], o["rec_int"], err_msg="%s seed %d" % (name, s))
         assert np.array_equal(rd[k].view(np.uint64), o["rec_dbl"].view(np.uint64)), (name, s)
         assert summ[k]["consistent"] == 0
+
+
+# The HBM-column variant (columns, prefix tables, a/b, counts in HBM; chosen automatically when
+# the LDS layout exceeds 160 KB) forced on small cases: same bits as the oracle.
+HBM_CASES = [c for c in CASES if c[0] in ("tiny", "many-hard", "walk17", "lds-walk", "tb256-2-per-thread",
+                                          "3-per-thread")]
+
+
+@pytest.mark.parametrize("name,N,M,nh,tb", HBM_CASES, ids=["hbm-" + c[0] for c in HBM_CASES])
+def test_edge_parity_hbm_columns(name, N, M, nh, tb):
+    text = make_text(N, M, nh, seed=N * 1000 + M)
+    ds = sa.Dataset.parse(text, maxs=0)
+    seeds = [3, 11]
+    with sa.Session(ds, seeds, block_threads=tb, columns="hbm") as s:
+        assert s.variant == "hbm"
+    summ, (ri, rd) = sa.run_chains(ds, seeds, burnin_calls=2, sample_calls=3, keep_records=True, block_threads=tb,
+                                   columns="hbm")
+    for k, s in enumerate(seeds):
+        o = oracle_ref.run_chain(text, s, 2, 3, maxs=0)
+        assert o["rc"] == 0
+        np.testing.assert_array_equal(ri[k], o["rec_int"], err_msg="%s seed %d" % (name, s))
+        assert np.array_equal(rd[k].view(np.uint64), o["rec_dbl"].view(np.uint64)), (name, s)
+        assert summ[k]["consistent"] == 0

@@ -1,0 +1,110 @@
+#!/usr/bin/env python3
+"""Summarise one gpu_round.sh pass (rocprofv3 CSV output) into the per-round profile files.
+
+    python tools/pmc_summary.py gpurun_out/<run> profiles/<round> --warmup 3 [--config-json bench.json]
+
+Writes
+  <prefix>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (as produced)
+  <prefix>_traffic.json       HBM bytes per sr_sweep_kernel launch from the PMC passes, plus the
+                              SQ/LDS counters and the kernel-trace duration of the timed launches
+
+HBM traffic follows MI355X_MICROARCH.md (HBM section): FETCH_SIZE and WRITE_SIZE are collected
+in separate --pmc passes (FETCH_SIZE uses 3 of the 4 TCC slots, WRITE_SIZE 2); rocprofv3 reports
+both in KiB; on gfx950 FETCH_SIZE counts half the bytes of a coalesced streaming read, so the
+fetch figure is doubled.  The kernel's loads are dword-per-lane (coalesced 256 B per wave), a
+width the guide lists as uncalibrated -- the raw values are kept next to the corrected ones.
+bench.py reads <prefix>_traffic.json for its roofline.traffic field when the workload matches.
+"""
+import argparse
+import csv
+import json
+import os
+import shutil
+import statistics
+import sys
+
+KERNEL = "sr_sweep_kernel"
+
+
+def per_dispatch(path):
+    """{counter: [value per sr_sweep_kernel dispatch in dispatch order]} and the kernel name"""
+    rows = [r for r in csv.DictReader(open(path)) if KERNEL in r["Kernel_Name"]]
+    out, name = {}, None
+    by_disp = {}
+    for r in rows:
+        name = r["Kernel_Name"]
+        key = (int(r["Dispatch_Id"]), r["Counter_Name"])
+        by_disp[key] = by_disp.get(key, 0.0) + float(r["Counter_Value"])
+    for (d, c), v in sorted(by_disp.items()):
+        out.setdefault(c, []).append(v)
+    return out, name
+
+
+def find(d, suffix):
+    for root, _, files in os.walk(d):
+        for f in files:
+            if f.endswith(suffix):
+                return os.path.join(root, f)
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("run")
+    ap.add_argument("prefix")
+    ap.add_argument("--warmup", type=int, default=1, help="untimed launches at the start of each PMC pass")
+    ap.add_argument("--trace-warmup", type=int, default=3, help="untimed launches in the kernel-trace run")
+    args = ap.parse_args()
+
+    res = {"kernel": None, "source": args.run,
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over bench.py; "
+                     "KiB -> bytes; FETCH_SIZE doubled (gfx950 correction, MI355X_MICROARCH.md HBM); "
+                     "traffic = 2*FETCH + WRITE per sr_sweep_kernel launch, warm-up launches dropped"}
+    stats = find(os.path.join(args.run, "prof"), "kernel_stats.csv")
+    if stats:
+        shutil.copy(stats, args.prefix + "_kernel_stats.csv")
+    trace = find(os.path.join(args.run, "prof"), "kernel_trace.csv")
+    if trace:
+        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(trace))
+                if KERNEL in r["Kernel_Name"]]
+        timed = durs[args.trace_warmup:]
+        res["trace"] = {"launches": len(durs), "timed_launches": len(timed),
+                        "avg_ns_timed": statistics.mean(timed) if timed else None,
+                        "avg_ns_all": statistics.mean(durs) if durs else None}
+    fetch = find(os.path.join(args.run, "pmc_fetch"), "counter_collection.csv")
+    write = find(os.path.join(args.run, "pmc_write"), "counter_collection.csv")
+    if fetch and write:
+        f, name = per_dispatch(fetch)
+        w, _ = per_dispatch(write)
+        fk = f["FETCH_SIZE"][args.warmup:]
+        wk = w["WRITE_SIZE"][args.warmup:]
+        res["kernel"] = name
+        fb = statistics.mean(fk) * 1024.0
+        wb = statistics.mean(wk) * 1024.0
+        res["fetch_bytes_raw"] = fb
+        res["fetch_bytes"] = 2.0 * fb
+        res["write_bytes"] = wb
+        res["traffic_bytes_per_launch"] = 2.0 * fb + wb
+        res["launches"] = len(fk)
+    sq = find(os.path.join(args.run, "pmc_sq"), "counter_collection.csv")
+    if sq:
+        s, _ = per_dispatch(sq)
+        res["sq"] = {k: statistics.mean(v[args.warmup:]) for k, v in s.items()}
+        if "SQ_INSTS_LDS" in res["sq"] and res["sq"]["SQ_INSTS_LDS"]:
+            res["sq"]["lds_bank_conflict_cycles_per_lds_inst"] = (res["sq"].get("SQ_LDS_BANK_CONFLICT", 0.0) /
+                                                                   res["sq"]["SQ_INSTS_LDS"])
+    bench = os.path.join(args.run, "bench.json")
+    if os.path.exists(bench):
+        try:
+            b = json.loads(open(bench).read().strip().splitlines()[-1])
+            res["workload"] = {k: b["config"][k] for k in ("sites", "taxa", "chains_per_gpu", "sweeps_per_step")}
+        except Exception:
+            pass
+    with open(args.prefix + "_traffic.json", "w") as fh:
+        json.dump(res, fh, indent=1)
+    json.dump(res, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == "__main__":
+    main()

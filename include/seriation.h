@@ -123,6 +123,30 @@ int32_t sr_session_block_threads(const sr_session *s);
 int32_t sr_session_variant(const sr_session *s);
 void sr_session_destroy(sr_session *s);
 
+/* ---- posterior summaries over saved samples, on the GPU ----
+ * Replace the per-sample loops of the reference's analysis script (script.py):
+ *   pair_order  [N][N]  compute_pair_order_matrix / generate_po_matrix   script.py:155-189
+ *   alive       [N][M]  X_sum of plot_taxa_occurence_probability_matrix  script.py:306-333
+ *   false_alive [N][M]  X_sum of plot_false_taxa_occurence_probability   script.py:350-377
+ *   false_ones  [N][M]  X_sum of plot_false_ones_probability             script.py:392-417
+ *   exp_pi      [N]     compute_exp_pi                                   script.py:230-251
+ *   exp_a       [M]     compute_exp_a                                    script.py:254-275
+ * bit for bit, quirks included (per-chain accumulators never reset, the fixed /1000, the
+ * [site][taxon] loops comparing the site index with the limits); the argsort reorderings that
+ * follow in the script are left to the caller.  NULL outputs are skipped; kernel_ms receives
+ * the summed device time.  Samples are mcmc_save_chain rows (a, b, pi with pi[site] = position). */
+typedef struct {
+  double *pair_order, *alive, *false_alive, *false_ones, *exp_pi, *exp_a;
+  double kernel_ms;
+} sr_posterior_out;
+/* ab_pi: [n_sel][count][2M+N] int16 host rows, chains in selection order; ds supplies N, M, X. */
+int sr_posterior(const sr_dataset *ds, const int16_t *ab_pi, int32_t n_sel, int32_t count,
+                 int32_t chains_selected, int32_t device, sr_posterior_out *out);
+/* The session's own records in HBM (no host round trip): chains[n_sel] are session chain
+ * indices in selection order, samples [first, first + count) of its record buffer. */
+int sr_session_posterior(sr_session *s, const int32_t *chains, int32_t n_sel, int32_t first, int32_t count,
+                         int32_t chains_selected, sr_posterior_out *out);
+
 const char *sr_strerror(int code);
 int sr_device_count(void);
 const char *sr_version(void);

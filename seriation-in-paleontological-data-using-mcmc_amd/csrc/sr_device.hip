@@ -2098,6 +2098,17 @@ extern "C" int srk_fetch_records(srk_dev *d, int first, int count, int16_t *ab_p
   return 0;
 }
 
+extern "C" int srk_records_device(srk_dev *d, const int16_t **rec, int *rec_cap, int *device, void **stream)
+{
+  HIPCHK(hipSetDevice(d->device));
+  HIPCHK(hipStreamSynchronize(d->stream));
+  *rec = d->args.rec_abpi;
+  *rec_cap = d->rec_cap;
+  *device = d->device;
+  *stream = (void *)d->stream;
+  return 0;
+}
+
 extern "C" int srk_download_state(srk_dev *d, sr_state_host *st)
 {
   HIPCHK(hipSetDevice(d->device));

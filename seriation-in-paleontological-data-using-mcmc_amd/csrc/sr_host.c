@@ -435,6 +435,66 @@ SR_API int sr_session_accept_counts(sr_session *s, int32_t chain, int64_t *acc7)
   return SR_OK;
 }
 
+/* ---- posterior summaries on the GPU (script.py:155-189, 230-275, 306-417) ---- */
+static const int post_kinds[6] = {SRP_PAIR_ORDER, SRP_ALIVE, SRP_FALSE_ALIVE, SRP_FALSE_ONES, SRP_EXP_PI, SRP_EXP_A};
+
+static double *post_slot(sr_posterior_out *o, int k)
+{
+  switch (k) {
+    case 0: return o->pair_order;
+    case 1: return o->alive;
+    case 2: return o->false_alive;
+    case 3: return o->false_ones;
+    case 4: return o->exp_pi;
+    default: return o->exp_a;
+  }
+}
+
+static int post_rc(int rc) { return rc == 0 ? SR_OK : (rc == -1 ? SR_EINVAL : (rc == -4 ? SR_ENOMEM : SR_EDEVICE)); }
+
+SR_API int sr_posterior(const sr_dataset *ds, const int16_t *ab_pi, int32_t n_sel, int32_t count,
+                        int32_t chains_selected, int32_t device, sr_posterior_out *out)
+{
+  if (!ds || !ab_pi || !out || n_sel <= 0 || count < 0 || chains_selected == 0) return SR_EINVAL;
+  for (int k = 0; k < 6; k++) {
+    double *dst = post_slot(out, k);
+    if (!dst) continue;
+    float ms = 0.0f;
+    int rc = srp_posterior_host(device, post_kinds[k], ab_pi, n_sel, count, ds->N, ds->M, ds->X, chains_selected, dst, &ms);
+    if (rc) return post_rc(rc);
+    out->kernel_ms += ms;
+  }
+  return SR_OK;
+}
+
+SR_API int sr_session_posterior(sr_session *s, const int32_t *chains, int32_t n_sel, int32_t first, int32_t count,
+                                int32_t chains_selected, sr_posterior_out *out)
+{
+  if (!s || !chains || !out || n_sel <= 0 || first < 0 || count < 0 || first + count > s->nrec || chains_selected == 0)
+    return SR_EINVAL;
+  for (int k = 0; k < n_sel; k++)
+    if (chains[k] < 0 || chains[k] >= s->nchains) return SR_EINVAL;
+  const int16_t *rec;
+  int cap, dev;
+  void *stream;
+  if (srk_records_device(s->dev, &rec, &cap, &dev, &stream)) return SR_EDEVICE;
+  const long long W = 2LL * s->ds.M + s->ds.N;
+  long long *off = (long long *)malloc(sizeof(long long) * n_sel);
+  if (!off) return SR_ENOMEM;
+  for (int k = 0; k < n_sel; k++) off[k] = ((long long)chains[k] * cap + first) * W;
+  int rc = 0;
+  for (int k = 0; k < 6 && !rc; k++) {
+    double *dst = post_slot(out, k);
+    if (!dst) continue;
+    float ms = 0.0f;
+    rc = srp_posterior_dev(dev, stream, post_kinds[k], rec, off, n_sel, count, W, s->ds.N, s->ds.M, s->ds.X,
+                           chains_selected, dst, &ms);
+    out->kernel_ms += ms;
+  }
+  free(off);
+  return post_rc(rc);
+}
+
 SR_API void sr_session_destroy(sr_session *s)
 {
   if (!s) return;

@@ -47,6 +47,21 @@ int srk_variant(const srk_dev *d);   /* 0 LDS columns, 1 HBM columns */
 int srk_fetch_dbg(srk_dev *d, unsigned long long *out);
 int srk_fetch_records(srk_dev *d, int first, int count, int16_t *ab_pi, double *cdl);
 int srk_download_state(srk_dev *d, sr_state_host *st);
+/* the session's record buffer in HBM: [nchains][rec_cap][2M+N] int16 */
+int srk_records_device(srk_dev *d, const int16_t **rec, int *rec_cap, int *device, void **stream);
+
+/* posterior summaries (sr_post.hip); kinds = SR_POST_* bit positions */
+#define SRP_PAIR_ORDER 0
+#define SRP_ALIVE 1
+#define SRP_FALSE_ALIVE 2
+#define SRP_FALSE_ONES 3
+#define SRP_EXP_PI 4
+#define SRP_EXP_A 5
+int srp_posterior_dev(int device, void *stream, int kind, const int16_t *d_rec, const long long *chain_off, int n_sel,
+                      int count, long long row_stride, int N, int M, const uint8_t *X_host, int chains_selected,
+                      double *out_host, float *ms);
+int srp_posterior_host(int device, int kind, const int16_t *ab_pi, int n_sel, int count, int N, int M,
+                       const uint8_t *X_host, int chains_selected, double *out_host, float *ms);
 void srk_destroy(srk_dev *d);
 
 #ifdef __cplusplus

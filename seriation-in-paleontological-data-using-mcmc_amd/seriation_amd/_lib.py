@@ -60,6 +60,13 @@ class sr_record(ctypes.Structure):
                 ("c", ctypes.c_double), ("d", ctypes.c_double), ("loglik", ctypes.c_double)]
 
 
+class sr_posterior_out(ctypes.Structure):
+    _fields_ = [("pair_order", ctypes.POINTER(ctypes.c_double)), ("alive", ctypes.POINTER(ctypes.c_double)),
+                ("false_alive", ctypes.POINTER(ctypes.c_double)), ("false_ones", ctypes.POINTER(ctypes.c_double)),
+                ("exp_pi", ctypes.POINTER(ctypes.c_double)), ("exp_a", ctypes.POINTER(ctypes.c_double)),
+                ("kernel_ms", ctypes.c_double)]
+
+
 SINK_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
                            ctypes.POINTER(sr_record))
 
@@ -70,7 +77,7 @@ PUBLIC_SYMBOLS = [
     "sr_session_run", "sr_session_sync", "sr_session_records", "sr_session_record_capacity",
     "sr_session_fetch_records", "sr_session_reset_records", "sr_session_state",
     "sr_session_accept_counts", "sr_session_last_kernel_ms", "sr_session_block_threads", "sr_session_variant",
-    "sr_session_destroy", "sr_strerror", "sr_device_count", "sr_version",
+    "sr_session_destroy", "sr_posterior", "sr_session_posterior", "sr_strerror", "sr_device_count", "sr_version",
 ]
 
 _LIB = None
@@ -108,6 +115,8 @@ def _lib():
         "sr_session_block_threads": (c_i32, [c_void_p]),
         "sr_session_variant": (c_i32, [c_void_p]),
         "sr_session_destroy": (None, [c_void_p]),
+        "sr_posterior": (c_int, [P(sr_dataset), P(ctypes.c_int16), c_i32, c_i32, c_i32, c_i32, P(sr_posterior_out)]),
+        "sr_session_posterior": (c_int, [c_void_p, P(c_i32), c_i32, c_i32, c_i32, c_i32, P(sr_posterior_out)]),
         "sr_strerror": (ctypes.c_char_p, [c_int]),
         "sr_device_count": (c_int, []),
         "sr_version": (ctypes.c_char_p, []),

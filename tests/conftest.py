@@ -5,7 +5,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "seriation-in-paleontological-data-using-mcmc_amd")
-for p in (ROOT, PKG, os.path.join(ROOT, "tests"), os.path.join(ROOT, "tools")):
+for p in (ROOT, PKG, os.path.join(ROOT, "tests"), os.path.join(ROOT, "tools"), os.path.join(ROOT, "oracle")):
     if p not in sys.path:
         sys.path.insert(0, p)
 

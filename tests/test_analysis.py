@@ -6,6 +6,7 @@ import subprocess
 import numpy as np
 
 import oracle_ref
+import om_script
 from seriation_amd import analysis
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -41,7 +42,8 @@ def test_file_and_record_forms_agree(tmp_path):
     r = analysis.compute_exp_ages(chains, 3, N, root=str(tmp_path))
     r2 = analysis.corr_mn_from_records([recs[k]["rec_int"][:, 2 * M:] for k in chains])
     assert abs(r - r2) < 1e-12
-    # literal pair-order restatement (script.py:155-189 with generate_po_matrix's loops)
+    # the oracle's vectorised pair-order (checker of the GPU kernel) equals the script's literal
+    # loops (script.py:155-189 with generate_po_matrix), read back from the chain files
     po_ref = np.zeros((N, N))
     po_chain = np.zeros((N, N))
     for k in chains:
@@ -52,5 +54,10 @@ def test_file_and_record_forms_agree(tmp_path):
         po_chain /= 1000
         po_ref += po_chain
     po_ref /= 3
-    np.testing.assert_allclose(analysis.compute_pair_order_matrix(chains, 3, N, root=str(tmp_path)), po_ref,
-                               rtol=0, atol=1e-15)
+    rows = [om_script.read_chain_rows(os.path.join(str(tmp_path), "Chains", "chain_%02d" % k, "chain_data.csv"), N, M)
+            for k in chains]
+    assert np.array_equal(om_script.pair_order_matrix(rows, 3, N, M).view(np.uint64), po_ref.view(np.uint64))
+    # the product's chain-file reader gives the same rows
+    prod = analysis.read_chain_rows(str(tmp_path), chains, N, M)
+    for k in range(3):
+        assert np.array_equal(prod[k], rows[k])

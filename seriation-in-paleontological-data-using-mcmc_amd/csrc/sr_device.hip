@@ -2098,6 +2098,65 @@ extern "C" int srk_fetch_records(srk_dev *d, int first, int count, int16_t *ab_p
   return 0;
 }
 
+/* Sampling with the host work overlapped: launch j (k_j calls, records into half j&1 of the record
+ * buffer) is followed on the stream by an async copy of its records into pinned host half j&1; the
+ * host then waits only for launch j-1's copy and hands it to `consume` while launch j runs.  Needs
+ * rec_cap >= 2 * cpl.  consume(ctx, first_call, count, ab_pi [nchains][count][2M+N], cdl
+ * [nchains][count][3]) returns nonzero to stop. */
+extern "C" int srk_run_pipelined(srk_dev *d, int total_calls, int cpl, int spc,
+                                 int (*consume)(void *, int, int, const int16_t *, const double *), void *ctx)
+{
+  if (total_calls <= 0) return 0;
+  if (cpl <= 0 || 2 * cpl > d->rec_cap) return -1;
+  HIPCHK(hipSetDevice(d->device));
+  const size_t W = 2 * (size_t)d->M + d->N, C = d->nchains;
+  int16_t *hab[2] = {nullptr, nullptr};
+  double *hcd[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  int cnt[2] = {0, 0}, first[2] = {0, 0};
+  int rc = 0;
+  for (int h = 0; h < 2 && !rc; ++h) {
+    if (hipHostMalloc((void **)&hab[h], C * cpl * W * sizeof(int16_t), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void **)&hcd[h], C * cpl * 3 * sizeof(double), hipHostMallocDefault) != hipSuccess ||
+        hipEventCreateWithFlags(&ev[h], hipEventDisableTiming) != hipSuccess)
+      rc = -5;
+  }
+  int done = 0, j = 0;
+  while (!rc && done < total_calls) {
+    const int h = j & 1, k = (total_calls - done < cpl) ? total_calls - done : cpl;
+    rc = srk_run(d, k, spc, 1, h * cpl);
+    if (rc) break;
+    /* strided: chain c's k records at [c][h*cpl .. h*cpl+k) -> pinned [c][0..k) */
+    if (hipMemcpy2DAsync(hab[h], k * W * sizeof(int16_t), d->args.rec_abpi + (size_t)h * cpl * W,
+                         d->rec_cap * W * sizeof(int16_t), k * W * sizeof(int16_t), C, hipMemcpyDeviceToHost,
+                         d->stream) != hipSuccess ||
+        hipMemcpy2DAsync(hcd[h], k * 3 * sizeof(double), d->args.rec_cdl + (size_t)h * cpl * 3,
+                         d->rec_cap * 3 * sizeof(double), k * 3 * sizeof(double), C, hipMemcpyDeviceToHost,
+                         d->stream) != hipSuccess ||
+        hipEventRecord(ev[h], d->stream) != hipSuccess) { rc = -5; break; }
+    cnt[h] = k; first[h] = done;
+    if (j > 0) {   /* the previous launch's records, while this launch runs */
+      const int p = h ^ 1;
+      if (hipEventSynchronize(ev[p]) != hipSuccess) { rc = -5; break; }
+      if (consume(ctx, first[p], cnt[p], hab[p], hcd[p])) { rc = -1; break; }
+    }
+    done += k;
+    ++j;
+  }
+  if (!rc && j > 0) {
+    const int p = (j - 1) & 1;
+    if (hipEventSynchronize(ev[p]) != hipSuccess) rc = -5;
+    else if (consume(ctx, first[p], cnt[p], hab[p], hcd[p])) rc = -1;
+  }
+  (void)hipStreamSynchronize(d->stream);
+  for (int h = 0; h < 2; ++h) {
+    if (hab[h]) (void)hipHostFree(hab[h]);
+    if (hcd[h]) (void)hipHostFree(hcd[h]);
+    if (ev[h]) (void)hipEventDestroy(ev[h]);
+  }
+  return rc;
+}
+
 extern "C" int srk_records_device(srk_dev *d, const int16_t **rec, int *rec_cap, int *device, void **stream)
 {
   HIPCHK(hipSetDevice(d->device));

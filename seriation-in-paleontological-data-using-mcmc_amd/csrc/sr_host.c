@@ -21,12 +21,15 @@
 #include <errno.h>
 #include <sys/stat.h>
 #include <sys/types.h>
+#include <pthread.h>
+#include <unistd.h>
 #include "seriation.h"
 #include "sr_internal.h"
 #include "sr_math.h"
 #include "sr_rng.h"
 
 #define SR_API __attribute__((visibility("default")))
+#define SR_MAX_WRITERS 64   /* chain_data.csv formatting threads (SR_WRITER_THREADS, default = online CPUs) */
 
 static const sr_mtab SR_HOST_TAB = {sr_exp_thi, sr_exp_tlo, sr_log_invc, sr_log_lhi, sr_log_llo};
 static double h_exp(double x) { return sr_exp_m(x, &SR_HOST_TAB); }
@@ -552,64 +555,170 @@ typedef struct {
   double ls, cs, ds;
 } sr_sums;
 
+typedef struct {
+  FILE **f;     /* chain_data.csv per chain */
+  int M;
+} dir_ctx;
+
+/* one mcmc_save_chain line (mcmc.c:69-92) into *buf; c and d are shared by all taxa
+ * (manycd=0), so their "%.14f " text is formatted once and replicated.  Returns the length. */
+static char *put_int(char *p, int v);
+static long format_line(char **buf, size_t *cap, int N, int M, const int16_t *ab_pi, const double *cdl)
+{
+  char cbuf[64], dbuf[64];
+  const int cl = snprintf(cbuf, sizeof cbuf, "%.14f ", exp(cdl[0]));
+  const int dl = snprintf(dbuf, sizeof dbuf, "%.14f ", exp(cdl[1]));
+  const size_t need = (size_t)(2 * M + N) * 12 + (size_t)M * (cl + dl) + 128;
+  if (need > *cap) {
+    char *nl = (char *)realloc(*buf, need);
+    if (!nl) return -1;
+    *buf = nl; *cap = need;
+  }
+  char *p = *buf;
+  for (int i = 0; i < M; i++) { p = put_int(p, ab_pi[i]); *p++ = ' '; }
+  *p++ = ',';
+  for (int i = 0; i < M; i++) { p = put_int(p, ab_pi[M + i]); *p++ = ' '; }
+  *p++ = ',';
+  for (int i = 0; i < N; i++) { p = put_int(p, ab_pi[2 * M + i]); *p++ = ' '; }
+  *p++ = ',';
+  for (int i = 0; i < M; i++) { memcpy(p, cbuf, cl); p += cl; }
+  *p++ = ',';
+  for (int i = 0; i < M; i++) { memcpy(p, dbuf, dl); p += dl; }
+  p += sprintf(p, ",%.14f\n", cdl[2]);
+  return (long)(p - *buf);
+}
+
+/* per-launch consumer of the pipelined sampler (srk_run_pipelined): running sums of
+ * compute_exp_data (mcmc.c:53-58) and either the caller's sink (sequential, per chain in sample
+ * order) or the chain_data.csv writers (chains formatted in parallel by nthr threads, each chain
+ * by one thread in sample order; the GPU runs the next launch meanwhile). */
+typedef struct {
+  int n, N, M;
+  sr_sums *sums;
+  sr_sample_sink_fn sink;
+  void *ctx;
+  int32_t *ra;
+  dir_ctx *dir;
+  int nthr;
+  /* current batch (for the writer threads) */
+  int first, count;
+  const int16_t *ab;
+  const double *cd;
+  int err;
+} run_ctx;
+
+typedef struct { run_ctx *r; int t; char *line; size_t cap; } writer_arg;
+
+static void chain_sums(run_ctx *r, int c)
+{
+  for (int t = 0; t < r->count; t++) {
+    const double *cd = r->cd + ((size_t)c * r->count + t) * 3;
+    r->sums[c].ls += -(cd[2]);
+    r->sums[c].cs += exp(cd[0]);
+    r->sums[c].ds += exp(cd[1]);
+  }
+}
+
+static void *writer_main(void *va)
+{
+  writer_arg *w = (writer_arg *)va;
+  run_ctx *r = w->r;
+  const size_t W = 2 * (size_t)r->M + r->N;
+  for (int c = w->t; c < r->n; c += r->nthr) {
+    chain_sums(r, c);
+    for (int t = 0; t < r->count; t++) {
+      const long len = format_line(&w->line, &w->cap, r->N, r->M, r->ab + ((size_t)c * r->count + t) * W,
+                                   r->cd + ((size_t)c * r->count + t) * 3);
+      if (len < 0 || fwrite(w->line, 1, (size_t)len, r->dir->f[c]) != (size_t)len) { r->err = 1; return NULL; }
+    }
+  }
+  return NULL;
+}
+
+static int consume_batch(void *vctx, int first, int count, const int16_t *ab, const double *cd)
+{
+  run_ctx *r = (run_ctx *)vctx;
+  r->first = first; r->count = count; r->ab = ab; r->cd = cd;
+  const int N = r->N, M = r->M, W = 2 * M + N;
+  if (r->dir) {
+    writer_arg wa[SR_MAX_WRITERS];
+    pthread_t th[SR_MAX_WRITERS];
+    int started = 0;
+    for (int t = 0; t < r->nthr; t++) { wa[t].r = r; wa[t].t = t; wa[t].line = NULL; wa[t].cap = 0; }
+    for (int t = 1; t < r->nthr; t++) {
+      if (pthread_create(&th[t], NULL, writer_main, &wa[t]) != 0) { r->err = 1; break; }
+      started = t;
+    }
+    writer_main(&wa[0]);
+    for (int t = 1; t <= started; t++) pthread_join(th[t], NULL);
+    for (int t = 0; t < r->nthr; t++) free(wa[t].line);
+    return r->err;
+  }
+  for (int c = 0; c < r->n; c++) {
+    chain_sums(r, c);
+    if (!r->sink) continue;
+    for (int t = 0; t < count; t++) {
+      const int16_t *src = ab + ((size_t)c * count + t) * W;
+      const double *cdl = cd + ((size_t)c * count + t) * 3;
+      for (int q = 0; q < W; q++) r->ra[q] = src[q];
+      sr_record rec = {N, M, r->ra, r->ra + M, r->ra + 2 * M, cdl[0], cdl[1], cdl[2]};
+      if (r->sink(r->ctx, c, first + t, &rec)) return 1;
+    }
+  }
+  return 0;
+}
+
+static int writer_threads(int n)
+{
+  const char *e = getenv("SR_WRITER_THREADS");
+  long t = e ? strtol(e, NULL, 10) : sysconf(_SC_NPROCESSORS_ONLN);
+  if (t < 1) t = 1;
+  if (t > SR_MAX_WRITERS) t = SR_MAX_WRITERS;
+  if (t > n) t = n;
+  return (int)t;
+}
+
 static int run_common(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n, const sr_run_opts *opts,
-                      sr_sample_sink_fn sink, void *ctx, sr_chain_summary *out, sr_state_host *final_state)
+                      sr_sample_sink_fn sink, void *ctx, dir_ctx *dir, sr_chain_summary *out, sr_state_host *final_state)
 {
   sr_run_opts o;
   if (opts) o = *opts; else sr_default_opts(&o);
   if (o.burnin_calls < 0 || o.sample_calls < 0) return SR_EINVAL;
+  const int cpl = auto_calls_per_launch(&o);
+  sr_run_opts o2 = o;
+  o2.calls_per_launch = 2 * cpl;   /* two record halves: one being written, one being consumed */
   sr_session *s = NULL;
-  int rc = sr_session_create(ds, specs, n, &o, &s);
+  int rc = sr_session_create(ds, specs, n, &o2, &s);
   if (rc) return rc;
-  const int cpl = s->rec_cap;
   for (int done = 0; done < o.burnin_calls;) {
     int k = o.burnin_calls - done < cpl ? o.burnin_calls - done : cpl;
     if ((rc = sr_session_run(s, k, 0))) goto fail;
     done += k;
   }
   const int N = ds->N, M = ds->M, W = 2 * M + N;
-  sr_sums *sums = (sr_sums *)calloc(n, sizeof(sr_sums));
-  int16_t *rab = (int16_t *)malloc((size_t)n * cpl * W * sizeof(int16_t));
-  double *rcd = (double *)malloc((size_t)n * cpl * 3 * sizeof(double));
-  int32_t *ra = (int32_t *)malloc((size_t)W * 4);
-  if (!sums || !rab || !rcd || !ra) { free(sums); free(rab); free(rcd); free(ra); rc = SR_ENOMEM; goto fail; }
-  for (int done = 0; done < o.sample_calls;) {
-    int k = o.sample_calls - done < cpl ? o.sample_calls - done : cpl;
-    sr_session_reset_records(s);
-    if ((rc = sr_session_run(s, k, 1))) break;
-    if ((rc = sr_session_fetch_records(s, 0, k, rab, rcd))) break;
-    for (int c = 0; c < n && !rc; c++) {
-      for (int t = 0; t < k; t++) {
-        const int16_t *src = rab + ((size_t)c * k + t) * W;
-        const double *cd = rcd + ((size_t)c * k + t) * 3;
-        sums[c].ls += -(cd[2]);                 /* compute_exp_data, mcmc.c:53-58 */
-        sums[c].cs += exp(cd[0]);
-        sums[c].ds += exp(cd[1]);
-        if (sink) {
-          for (int q = 0; q < W; q++) ra[q] = src[q];
-          sr_record rec = {N, M, ra, ra + M, ra + 2 * M, cd[0], cd[1], cd[2]};
-          if (sink(ctx, c, done + t, &rec)) { rc = SR_EINVAL; break; }
-        }
-      }
-    }
-    if (rc) break;
-    done += k;
-  }
-  free(rab); free(rcd); free(ra);
-  if (rc) { free(sums); goto fail; }
+  run_ctx r;
+  memset(&r, 0, sizeof r);
+  r.n = n; r.N = N; r.M = M; r.sink = sink; r.ctx = ctx; r.dir = dir;
+  r.nthr = dir ? writer_threads(n) : 1;
+  r.sums = (sr_sums *)calloc(n, sizeof(sr_sums));
+  r.ra = (int32_t *)malloc((size_t)W * 4);
+  if (!r.sums || !r.ra) { free(r.sums); free(r.ra); rc = SR_ENOMEM; goto fail; }
+  rc = srk_run_pipelined(s->dev, o.sample_calls, cpl, o.sweeps_per_call, consume_batch, &r);
+  free(r.ra);
+  if (rc) { free(r.sums); rc = (rc == -1) ? (dir ? SR_EIO : SR_EINVAL) : SR_EDEVICE; goto fail; }
   sr_state_host st;
   rc = download(s, &st);
-  if (rc) { free(sums); goto fail; }
+  if (rc) { free(r.sums); goto fail; }
   for (int c = 0; c < n; c++) {
     if (out) {
       out[c].chain_id = specs[c].chain_id;
-      out[c].exp_loglik = sums[c].ls / 1000;      /* print_exp_data divides by 1000 (mcmc.c:62-64) */
-      out[c].exp_c = sums[c].cs / 1000;
-      out[c].exp_d = sums[c].ds / 1000;
+      out[c].exp_loglik = r.sums[c].ls / 1000;      /* print_exp_data divides by 1000 (mcmc.c:62-64) */
+      out[c].exp_c = r.sums[c].cs / 1000;
+      out[c].exp_d = r.sums[c].ds / 1000;
       out[c].consistent = (o.flags & SR_F_NO_CHECK) ? 0 : check_chain(ds, &st, c);
     }
   }
-  free(sums);
+  free(r.sums);
   if (final_state) *final_state = st; else state_free(&st);
   sr_session_destroy(s);
   if (out && !(o.flags & SR_F_NO_CHECK))
@@ -624,7 +733,7 @@ SR_API int sr_run_chains(const sr_dataset *ds, const sr_chain_spec *specs, int32
                          sr_sample_sink_fn sink, void *sink_ctx, sr_chain_summary *out)
 {
   if (!ds || !specs || n_chains <= 0) return SR_EINVAL;
-  return run_common(ds, specs, n_chains, opts, sink, sink_ctx, out, NULL);
+  return run_common(ds, specs, n_chains, opts, sink, sink_ctx, NULL, out, NULL);
 }
 
 /* ------------------------------------------------------------ file output */
@@ -637,42 +746,6 @@ static char *put_int(char *p, int v)
   do { tmp[n++] = (char)('0' + u % 10); u /= 10; } while (u);
   while (n) *p++ = tmp[--n];
   return p;
-}
-
-typedef struct {
-  FILE **f;
-  char *line;
-  size_t cap;
-  int M;
-} dir_ctx;
-
-/* one mcmc_save_chain line (mcmc.c:69-92); c and d are shared by all taxa (manycd=0),
- * so their "%.14f " text is formatted once and replicated. */
-static int dir_sink(void *vctx, int32_t ci, int32_t si, const sr_record *r)
-{
-  (void)si;
-  dir_ctx *x = (dir_ctx *)vctx;
-  char cbuf[64], dbuf[64];
-  int cl = snprintf(cbuf, sizeof cbuf, "%.14f ", exp(r->c));
-  int dl = snprintf(dbuf, sizeof dbuf, "%.14f ", exp(r->d));
-  size_t need = (size_t)(2 * r->M + r->N) * 12 + (size_t)r->M * (cl + dl) + 128;
-  if (need > x->cap) {
-    char *nl = (char *)realloc(x->line, need);
-    if (!nl) return 1;
-    x->line = nl; x->cap = need;
-  }
-  char *p = x->line;
-  for (int i = 0; i < r->M; i++) { p = put_int(p, r->a[i]); *p++ = ' '; }
-  *p++ = ',';
-  for (int i = 0; i < r->M; i++) { p = put_int(p, r->b[i]); *p++ = ' '; }
-  *p++ = ',';
-  for (int i = 0; i < r->N; i++) { p = put_int(p, r->pi[i]); *p++ = ' '; }
-  *p++ = ',';
-  for (int i = 0; i < r->M; i++) { memcpy(p, cbuf, cl); p += cl; }
-  *p++ = ',';
-  for (int i = 0; i < r->M; i++) { memcpy(p, dbuf, dl); p += dl; }
-  p += sprintf(p, ",%.14f\n", r->loglik);
-  return fwrite(x->line, 1, (size_t)(p - x->line), x->f[ci]) == (size_t)(p - x->line) ? 0 : 1;
 }
 
 static void chain_dir(char *buf, size_t n, const char *root, int id)
@@ -692,7 +765,6 @@ SR_API int sr_run_to_dirs(const sr_dataset *ds, const sr_chain_spec *specs, int3
   snprintf(dir, sizeof dir, "%s/Chains", root);
   mkdir(dir, 0777);
   dir_ctx x;
-  memset(&x, 0, sizeof x);
   x.M = ds->M;
   x.f = (FILE **)calloc(n, sizeof(FILE *));
   sr_chain_summary *sum = out ? out : (sr_chain_summary *)calloc(n, sizeof(sr_chain_summary));
@@ -707,10 +779,9 @@ SR_API int sr_run_to_dirs(const sr_dataset *ds, const sr_chain_spec *specs, int3
   }
   sr_state_host st;
   memset(&st, 0, sizeof st);
-  if (!rc) rc = run_common(ds, specs, n, opts, dir_sink, &x, sum, &st);
+  if (!rc) rc = run_common(ds, specs, n, opts, NULL, NULL, &x, sum, &st);
   for (int c = 0; c < n; c++) if (x.f[c]) fclose(x.f[c]);
   free(x.f);
-  free(x.line);
   if (rc && rc != SR_EINCONSISTENT) { if (!out) free(sum); state_free(&st); return rc; }
   const int N = ds->N, M = ds->M;
   for (int c = 0; c < n && st.ab; c++) {

@@ -46,6 +46,18 @@ __constant__ double c_log_llo[128] = SR_LOG_LLO_INIT;
 #define SR_EXP 0   /* timing experiments only (break the sampler): 1 skip proposals, 2 skip Gibbs, 4/8/16 skip pi3/pi2/pi1 terms */
 #endif
 #define SR_ZIGR 3.44428647676
+#ifndef SR_ZIG_UNIFORM
+#define SR_ZIG_UNIFORM 1
+#endif
+#ifndef SR_HALF_DRAWS
+#define SR_HALF_DRAWS 1
+#endif
+#ifndef SR_CD_FAST
+#define SR_CD_FAST 1
+#endif
+#ifndef SR_SWAP_ALONE
+#define SR_SWAP_ALONE 1
+#endif
 
 struct KArgs {
   int N, M, NW, nh, nchains;
@@ -138,13 +150,24 @@ __device__ __forceinline__ void gsync()
 
 /* ---------------------------------------------------------------- stamps */
 #ifdef SR_STAMPS
-#define STAMP_DECL unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long st_t = __builtin_amdgcn_s_memtime();
-#define STAMP(ph) do { unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[ph] += t_ - st_t; st_t = t_; } while (0)
-#define STAMP_STORE(dst) do { if ((threadIdx.x & 63) == 0 && (dst)) for (int q_ = 0; q_ < 8; ++q_) \
-  (dst)[(blockIdx.x * 17 + 1 + (threadIdx.x >> 6)) * 8 + q_] += st_acc[q_]; } while (0)
+#define STAMP_DECL unsigned long long st_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; \
+  unsigned long long st_t = __builtin_amdgcn_s_memtime();
+#define STAMP_RAW(ph) do { unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[ph] += t_ - st_t; st_t = t_; } while (0)
+#ifdef SR_STAMP_FINE   /* exact attribution: drain outstanding memory ops before each stamp (slows the kernel) */
+#define STAMP(ph) do { } while (0)
+#define FST(ph) do { __builtin_amdgcn_s_waitcnt(0); STAMP_RAW(ph); } while (0)
+#else
+#define STAMP(ph) STAMP_RAW(ph)
+#define FST(ph) do { } while (0)
+#endif
+/* slots 0-7 in row 1 + wave, slots 8-15 (SR_STAMP_FINE, TB <= 512) in row 9 + wave */
+#define STAMP_STORE(dst) do { if ((threadIdx.x & 63) == 0 && (dst)) for (int q_ = 0; q_ < 16; ++q_) \
+  if (q_ < 8 || (threadIdx.x >> 6) < 8) \
+    (dst)[(blockIdx.x * 17 + 1 + (threadIdx.x >> 6) + (q_ >= 8 ? 8 : 0)) * 8 + (q_ & 7)] += st_acc[q_]; } while (0)
 #else
 #define STAMP_DECL
 #define STAMP(ph) do { } while (0)
+#define FST(ph) do { } while (0)
 #define STAMP_STORE(dst) do { } while (0)
 #endif
 #ifdef SR_STAMP_GIBBS   /* phase B split: slots 1 prefix+pass0, 2 pass1, 3 pass2, 4 tail */
@@ -336,7 +359,13 @@ template <bool WAVE>
 __device__ __forceinline__ double d_gauss_zig(DRng &r, int lane, int nthr, const sr_mtab &tb)
 {
   for (;;) {
+#if SR_ZIG_UNIFORM
+    /* the word is block-uniform: keep it (and the table index) in SGPRs so the ziggurat table
+       lookups are scalar constant-cache loads */
+    uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)rng_get<WAVE>(r, lane, nthr));
+#else
     uint32_t k = rng_get<WAVE>(r, lane, nthr);
+#endif
     uint32_t i = k & 0xFF;
     uint32_t j = (k >> 8) & 0xFFFFFF;
     int sign = (i & 0x80) ? +1 : -1;
@@ -398,6 +427,68 @@ __device__ __forceinline__ double d_samplebeta(DRng &r, double x, double a, doub
     if (low <= y && y <= high) x = y;
   }
   return x;
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int l)
+{
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+/* mcmc_samplec + mcmc_sampled (mcmc.c:751-825) with the four gammas evaluated lane-parallel.
+ * Speculation: each gamma takes exactly two words (one ziggurat word inside the box, one
+ * uniform_pos word accepted by the squeeze or the log test), so gamma g reads words 2g, 2g+1 from
+ * the cursor.  Lanes 0..3 evaluate gamma(1+f1), gamma(1+t0), gamma(1+f0), gamma(1+t1) with the
+ * expressions of d_gauss_zig / d_gamma verbatim; lanes 0, 1 then form the two betas.  Valid iff all
+ * four gammas took their two-word path and the 8 words are resident -- otherwise returns false
+ * and the caller runs the sequential draws from the same cursor.  Wave-level: every wave of the
+ * block computes it identically (no block synchronisation). */
+__device__ __forceinline__ bool draw_cd_fast(DRng &r, double &c, double &d, int f1, int t0, int f0, int t1,
+                                             const sr_mtab &tb, int lane)
+{
+  if (r.blk + (r.off + 7) / SR_MT_N >= r.gen) return false;
+  const uint32_t base = (r.blk & (SR_RING - 1)) * SR_MT_N + r.off;
+  const int g = lane & 3;
+  uint32_t i0 = base + 2 * g, i1 = base + 2 * g + 1;
+  i0 = (i0 >= SR_RING * SR_MT_N) ? i0 - SR_RING * SR_MT_N : i0;
+  i1 = (i1 >= SR_RING * SR_MT_N) ? i1 - SR_RING * SR_MT_N : i1;
+  const uint32_t k = sr_mt_temper(r.ring[i0]), w1 = sr_mt_temper(r.ring[i1]);
+  const int cnt = (g == 0) ? f1 : (g == 1) ? t0 : (g == 2) ? f0 : t1;
+  const double a = 1. + (double)cnt;                   /* d_samplebeta: gamma(1. + a) */
+  const double dd = a - 1.0 / 3.0;
+  const double cc = (1.0 / 3.0) / __builtin_sqrt(dd);
+  uint32_t i = k & 0xFF;
+  const uint32_t j = (k >> 8) & 0xFFFFFF;
+  const int sign = (i & 0x80) ? +1 : -1;
+  i &= 0x7f;
+  double x = j * c_zig_w[i];
+  bool ok = j < c_zig_k[i];
+  x = sign * 1.0 * x;
+  double v = 1.0 + cc * x;
+  ok = ok && v > 0 && w1 != 0u;
+  v = v * v * v;
+  const double u = w1 / 4294967296.0;
+  bool acc = u < 1 - 0.0331 * x * x * x * x;
+  if (ok && !acc) acc = sr_log_m(u, &tb) < 0.5 * x * x + dd * (1 - v + sr_log_m(v, &tb));
+  ok = ok && acc;
+  const double gv = 1.0 * dd * v;
+  if ((__ballot(ok) & 0xFull) != 0xFull) return false;
+  /* betas: lane 0 -> c (gammas 0, 1), lane 1 -> d (gammas 2, 3) */
+  const double x1 = readlane_f64(gv, 0), x2 = readlane_f64(gv, 1), x3 = readlane_f64(gv, 2), x4 = readlane_f64(gv, 3);
+  const bool isd = (lane & 1) != 0;
+  const double ga = isd ? x3 : x1, gb = isd ? x4 : x2;
+  double res = isd ? d : c;
+  double y = ga / (ga + gb);
+  if (y > 0.) {
+    y = sr_log_m(y, &tb);
+    if ((isd ? SR_MIND : SR_MINC) <= y && y <= (isd ? SR_MAXD : SR_MAXC)) res = y;
+  }
+  c = readlane_f64(res, 0);
+  d = readlane_f64(res, 1);
+  rng_skip(r, 8);
+  return true;
 }
 
 /* ---------------------------------------------------------------- helpers */
@@ -976,13 +1067,6 @@ __device__ __forceinline__ int wave_sum_i32(int x)
   return __builtin_amdgcn_readlane(x, 63);
 }
 
-__device__ __forceinline__ double readlane_f64(double v, int l)
-{
-  const uint64_t b = __builtin_bit_cast(uint64_t, v);
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
-  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-}
 
 /* Exact delta: the reference's sequential `delta += term` over ascending m (mcmc.c:1214,
  * 1435, 1630), computed by lane 0 of the calling wave and broadcast through its slot.
@@ -1252,6 +1336,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   }
   if (tid == 0) for (int k = 0; k < 7; ++k) misc[MS_ACC + k] = 0;
   int rcur = 0;     /* current rpi buffer */
+  uint32_t hbc = 0;       /* own taxon's column bits at the hard positions (one-taxon kernels), */
+  bool hb_dirty = true;   /* recomputed after an accepted pi1 / pi2 (block-uniform flag) */
   int par = 0;      /* parity of the double-buffered totals */
   int bpar = 0;     /* parity of the double-buffered proposal count sums */
   int xpar = 0;     /* parity of the double-buffered exact-delta term lists */
@@ -1278,7 +1364,9 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         if (lane == 0) { tw[0] = s0; tw[1] = s1; tw[2] = s2; tw[3] = s3; }
       }
       STAMP(0);
+      FST(11);
       __syncthreads();
+      FST(13);
       {
         int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
 #pragma unroll
@@ -1287,12 +1375,15 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           s0 += tw[0]; s1 += tw[1]; s2 += tw[2]; s3 += tw[3];
         }
         /* mcmc_samplec then mcmc_sampled: Beta(1 + f1, 1 + t0), Beta(1 + f0, 1 + t1) */
-        double cd2[2] = {c, d};
-        for (int k = 0; k < 2; ++k)
-          cd2[k] = d_samplebeta<false>(R, cd2[k], (double)(k ? s1 : s3), (double)(k ? s2 : s0), k ? SR_MIND : SR_MINC,
-                                       k ? SR_MAXD : SR_MAXC, tid, TB, tb);
-        c = cd2[0];
-        d = cd2[1];
+        if (!(SR_CD_FAST && draw_cd_fast(R, c, d, s3, s0, s1, s2, tb, lane))) {
+          double cd2[2] = {c, d};
+          for (int k = 0; k < 2; ++k)
+            cd2[k] = d_samplebeta<false>(R, cd2[k], (double)(k ? s1 : s3), (double)(k ? s2 : s0), k ? SR_MIND : SR_MINC,
+                                         k ? SR_MAXD : SR_MAXC, tid, TB, tb);
+          c = cd2[0];
+          d = cd2[1];
+        }
+        FST(12);
         if (tid == 0) { misc[MS_ACC + 0]++; misc[MS_ACC + 1]++; }
       }
       CD K;
@@ -1316,6 +1407,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 #ifdef SR_STAMP_GIBBS
       STAMP(5);
 #endif
+      FST(0);
       /* ============ phase B: Gibbs update of own (a_m, b_m) (mcmc_sampleab) */
       /* taxa in rounds of TB (round r: m = r*TB + tid, words 2(m - r*TB), +1 from the round's
          cursor), each round's 2*TB words made resident first: the ring holds < 2M words when
@@ -1327,7 +1419,9 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         for (int rd = 0; rd < nround; ++rd) {
         const int mlo = (nround == 1) ? 0 : rd * TB, mhi = (nround == 1) ? M : min(M, mlo + TB);
         if (rd > 0) __syncthreads();   /* every thread is done with the previous round's words */
+        FST(1);
         rng_ensure(R, min(2 * (mhi - mlo) + SR_RNG_SLACK, rcap), tid, TB);
+        FST(8);
         for (int m = mlo + tid; m < mhi && !(SR_EXP & 2); m += TB) {
           const uint32_t *Pm = P + m;
           const double ua = rng_peek(R, 2 * (m - mlo)) / 4294967296.0;
@@ -1372,6 +1466,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         const int nw = wave_sum_i32((int)nchg);
         if (lane == 0 && nw) atomicAdd((unsigned long long *)&misc[MS_CAB], (unsigned long long)nw);
       }
+      FST(1);
       STAMP(1);
       if (want_logl) {   /* mcmc_logl (mcmc.c:639-645), sequential over m, lane 0 of every wave */
         __syncthreads();
@@ -1390,6 +1485,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         wsync();
       }
       STAMP(2);
+      FST(10);
 
       /* ============ phase C: the permutation proposals (mcmc.c:237-243), speculatively batched.
          Hypothesis: every remaining proposal is rejected.  A rejected non-vetoed proposal has
@@ -1420,16 +1516,91 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             vw0 = sr_mt_temper(ring[i0]);
             vw1 = sr_mt_temper(ring[i1]);
           }
+          FST(14);
           STAMP_D(3);
           int off = 0, pend = p0;
-          if (p0 > 0) {
+          /* one proposal drawn by block-uniform scalar code at word offset `off` (false: not enough
+             resident words) */
+          auto scalar_one = [&](int p) -> bool {
+              const int kind = prop_kind(p);
+              bool bad = false;
+              auto word = [&](void) -> uint32_t {
+                if (off >= avail) { bad = true; return 0u; }
+                const int k = off++;
+                return (uint32_t)__builtin_amdgcn_readlane((int)(k < 64 ? vw0 : vw1), k & 63);
+              };
+              auto uint_draw = [&](const UDivM &u) -> int {   /* gsl_rng_uniform_int */
+                uint32_t k;
+                do { k = udivm(word(), u); } while (!bad && k >= u.n);
+                return (int)k;
+              };
+              auto hc = [&](int x) -> int { return __builtin_amdgcn_readfirstlane((int)hcnt[x]); };
+              int i = 0, j = 0, inc1 = 0, inc2 = 0, Kn = 0, r0 = 0;
+              bool veto = false;
+              if (kind == PK_PI1) {                                  /* mcmc.c:1133-1160 */
+                i = uint_draw(mdN);
+                j = uint_draw(mdN1);
+                if (j >= i) j++;
+                if (!bad && hc(i + 1) != hc(i) && hc(max(i, j) + 1) - hc(min(i, j)) > 1) veto = true;
+              } else if (kind == PK_PI2 || kind == PK_SWAP) {        /* mcmc.c:1317-1364 */
+                if (kind == PK_PI2) {
+                  i = uint_draw(mdN);
+                  j = uint_draw(mdN1);
+                  if (j >= i) j++;
+                  else { const int t = i; i = j; j = t; }
+                } else {
+                  i = uint_draw(mdN1);
+                  j = i + 1;
+                }
+                if (!bad && hc(j + 1) - hc(i) > 1) veto = true;
+                if (!veto) { inc1 = uint_draw(md2); inc2 = uint_draw(md2); }
+              } else {                                               /* mcmc.c:1495-1565 */
+                if ((uint32_t)N - nhard < 2) veto = true;
+                else {
+                  const int n0 = uint_draw(mdH), m0 = uint_draw(mdH1);
+                  inc1 = uint_draw(md2);
+                  inc2 = uint_draw(md2);
+                  /* non-hard ranks -> positions (mcmc.c:1505-1533) */
+                  int ri, rj;
+                  if (n0 <= m0) { ri = n0; rj = m0 + 1; } else { ri = m0; rj = n0; }
+                  if (!bad) {
+                    i = __builtin_amdgcn_readfirstlane((int)nhall[ri]);
+                    j = __builtin_amdgcn_readfirstlane((int)nhall[rj]);
+                  }
+                  Kn = rj - ri + 1;
+                  r0 = ri;
+                }
+              }
+              const int nd = off;
+              uint32_t uw = 0;
+              if (!veto) { do { uw = word(); } while (!bad && uw == 0u); }   /* gsl_rng_uniform_pos */
+              if (bad) return false;
+              vi = (lane == p) ? (i) : vi;
+              vj = (lane == p) ? (j) : vj;
+              vfl = (lane == p) ? (inc1 | (inc2 << 1) | (veto ? 4 : 0)) : vfl;
+              vkn = (lane == p) ? (Kn) : vkn;
+              vuw = (lane == p) ? ((int)uw) : vuw;
+              vnd = (lane == p) ? (nd) : vnd;
+              voff = (lane == p) ? (off) : voff;
+              vr0 = (lane == p) ? (r0) : vr0;
+              pend = p + 1;
+              return true;
+          };
+          /* the swap (accepted ~44 %) is drawn first; with SR_SWAP_ALONE it forms its own batch,
+             otherwise proposals 1.. join its batch */
+          if (p0 == 0) (void)scalar_one(0);
+          if (p0 > 0 || (!SR_SWAP_ALONE && pend == 1)) {
             /* Lane-parallel draws: lane l evaluates "a pi1 / pi2 / pi3 proposal starting at word
                offset o" for o = l and o = l + 64 (words o..o+4); the scan below then walks the
                batch's actual offsets reading those results.  ok = no GSL rejection and a nonzero
                uniform_pos word (else the scalar path below takes over at that proposal). */
-            uint32_t rA1[2], rA2[2], rA3[2], rB3[2], rU1[2], rU2[2];
+            uint32_t rA1[2] = {0u, 0u}, rA2[2] = {0u, 0u}, rA3[2] = {0u, 0u}, rB3[2] = {0u, 0u}, rU1[2] = {0u, 0u},
+                     rU2[2] = {0u, 0u};
+            /* the second 64 offsets only when the batch's proposals can reach them (<= 5 words each) */
+            const int nh2 = (SR_HALF_DRAWS && 5 * (16 - p0) + 5 <= 64) ? 1 : 2;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
+              if (h >= nh2) break;
               const int o = lane + 64 * h;
               uint32_t w[5];
 #pragma unroll
@@ -1476,6 +1647,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 rB3[h] = (uint32_t)ri | ((uint32_t)(rj - ri + 1) << 16);
               }
             }
+            FST(15);
             /* scan: the batch's proposals at their actual offsets (all-rejected hypothesis) */
 #pragma unroll
             for (int sI = 1; sI < 16; ++sI) {
@@ -1508,73 +1680,13 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               pend = sI + 1;
             }
           }
-          for (int p = pend; p < 16; ++p) {   /* scalar path: the swap batch, and after a fast-path stop */
-            if (p0 == 0 && p == 1) break;     /* the swap (accepted ~40 %) forms its own batch */
+          for (int p = pend; p < 16; ++p) {   /* scalar path: the batch's first proposal after a fast-path stop */
+            if (p0 == 0 && p == 1) break;     /* the swap batch (SR_SWAP_ALONE) */
             if (p > p0) break;                /* only the batch's first proposal goes scalar */
-            const int kind = prop_kind(p);
-            bool bad = false;
-            auto word = [&](void) -> uint32_t {
-              if (off >= avail) { bad = true; return 0u; }
-              const int k = off++;
-              return (uint32_t)__builtin_amdgcn_readlane((int)(k < 64 ? vw0 : vw1), k & 63);
-            };
-            auto uint_draw = [&](const UDivM &u) -> int {   /* gsl_rng_uniform_int */
-              uint32_t k;
-              do { k = udivm(word(), u); } while (!bad && k >= u.n);
-              return (int)k;
-            };
-            auto hc = [&](int x) -> int { return __builtin_amdgcn_readfirstlane((int)hcnt[x]); };
-            int i = 0, j = 0, inc1 = 0, inc2 = 0, Kn = 0, r0 = 0;
-            bool veto = false;
-            if (kind == PK_PI1) {                                  /* mcmc.c:1133-1160 */
-              i = uint_draw(mdN);
-              j = uint_draw(mdN1);
-              if (j >= i) j++;
-              if (!bad && hc(i + 1) != hc(i) && hc(max(i, j) + 1) - hc(min(i, j)) > 1) veto = true;
-            } else if (kind == PK_PI2 || kind == PK_SWAP) {        /* mcmc.c:1317-1364 */
-              if (kind == PK_PI2) {
-                i = uint_draw(mdN);
-                j = uint_draw(mdN1);
-                if (j >= i) j++;
-                else { const int t = i; i = j; j = t; }
-              } else {
-                i = uint_draw(mdN1);
-                j = i + 1;
-              }
-              if (!bad && hc(j + 1) - hc(i) > 1) veto = true;
-              if (!veto) { inc1 = uint_draw(md2); inc2 = uint_draw(md2); }
-            } else {                                               /* mcmc.c:1495-1565 */
-              if ((uint32_t)N - nhard < 2) veto = true;
-              else {
-                const int n0 = uint_draw(mdH), m0 = uint_draw(mdH1);
-                inc1 = uint_draw(md2);
-                inc2 = uint_draw(md2);
-                /* non-hard ranks -> positions (mcmc.c:1505-1533) */
-                int ri, rj;
-                if (n0 <= m0) { ri = n0; rj = m0 + 1; } else { ri = m0; rj = n0; }
-                if (!bad) {
-                  i = __builtin_amdgcn_readfirstlane((int)nhall[ri]);
-                  j = __builtin_amdgcn_readfirstlane((int)nhall[rj]);
-                }
-                Kn = rj - ri + 1;
-                r0 = ri;
-              }
-            }
-            const int nd = off;
-            uint32_t uw = 0;
-            if (!veto) { do { uw = word(); } while (!bad && uw == 0u); }   /* gsl_rng_uniform_pos */
-            if (bad) break;
-            vi = (lane == p) ? (i) : vi;
-            vj = (lane == p) ? (j) : vj;
-            vfl = (lane == p) ? (inc1 | (inc2 << 1) | (veto ? 4 : 0)) : vfl;
-            vkn = (lane == p) ? (Kn) : vkn;
-            vuw = (lane == p) ? ((int)uw) : vuw;
-            vnd = (lane == p) ? (nd) : vnd;
-            voff = (lane == p) ? (off) : voff;
-            vr0 = (lane == p) ? (r0) : vr0;
-            pend = p + 1;
+            if (!scalar_one(p)) break;
           }
           pend = __builtin_amdgcn_readfirstlane(pend);
+          FST(2);
           STAMP_D(4);
           if (pend == p0) {   /* not enough resident words for one proposal: make more, retry */
             rng_ensure(R, min(avail + 256, (SR_RING - 1) * SR_MT_N - (SR_MT_N - 1)), tid, TB);
@@ -1598,8 +1710,10 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           /* own taxon's limits and hard-site bits, fixed for the batch (one taxon per thread) */
           const bool one = M <= TB;
           int a1 = 0, b1 = 0;
-          uint32_t hb1 = 0;
-          if (one && tid < M) { a1 = sab[tid]; b1 = sab[M + tid]; hb1 = hard_bits_col(P + tid, M, hl, nh); }
+          if (hb_dirty && one) { if (tid < M) hbc = hard_bits_col(P + tid, M, hl, nh); hb_dirty = false; }
+          const uint32_t hb1 = hbc;
+          if (one && tid < M) { a1 = sab[tid]; b1 = sab[M + tid]; }
+          FST(7);
 #if defined(SR_STAMP_DRAWS)
           STAMP(5);
 #elif defined(SR_STAMP_GIBBS)
@@ -1627,6 +1741,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 nzs[sI] = __popcll(__ballot((dt0 | dt1) != 0));
               }
             }
+            FST(3);
 #pragma unroll
             for (int sI = 0; sI < 16; ++sI) {
               const int fl = __builtin_amdgcn_readlane(vfl, sI);
@@ -1670,8 +1785,10 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             }
             STAMP_K(kind);
           }
+          FST(4);
           __syncthreads();
           STAMP_E(5);
+          FST(5);
 
           /* ---- lane-parallel certified decisions (lane p decides proposal p).  With
              X = sum dt, Y = sum |dt| (exact integers), S = X0 (cc - d) + X1 (dd - c) is the exact
@@ -1758,6 +1875,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 #else
           STAMP(7);
 #endif
+          FST(6);
           if (acc_p < 0) {   /* all of p0..pend-1 rejected or vetoed, as hypothesised */
             rng_skip(R, (uint32_t)__builtin_amdgcn_readlane(voff, pend - 1));
             p0 = pend;
@@ -1830,6 +1948,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             col_pre_build(pre + m, Pm, M, NW);   /* the column moved: refresh its prefix table */
           }
           /* rpi (double-buffered full permutation, read only at save time) and hard positions */
+          bool hmoved = false;   /* wave-uniform */
           {
             const int32_t *ro = rcur ? rpiB : rpiA;
             int32_t *rn = rcur ? rpiA : rpiB;
@@ -1840,15 +1959,23 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 else { if (n > j && n <= i) src = n - 1; else if (n == j) src = i; }
                 rn[n] = ro[src];
               }
-              if (lane < nh) {
-                const int h = hp[lane];
-                if (h == i) hp[lane] = j;
-                else if (i < j && h > i && h <= j) hp[lane] = h - 1;
-                else if (i > j && h >= j && h < i) hp[lane] = h + 1;
+              {
+                const int h = (lane < nh) ? hp[lane] : -1;
+                int hn = h;
+                if (h == i) hn = j;
+                else if (i < j && h > i && h <= j) hn = h - 1;
+                else if (i > j && h >= j && h < i) hn = h + 1;
+                hmoved = __ballot(lane < nh && hn != h) != 0;
+                if (lane < nh) hp[lane] = hn;
               }
             } else if (kind != PK_PI3) {
               for (int n = tid; n < N; n += TB) rn[n] = ro[(n >= i && n <= j) ? (i + j - n) : n];
-              if (lane < nh && hp[lane] >= i && hp[lane] <= j) hp[lane] = i + j - hp[lane];
+              {
+                const int h = (lane < nh) ? hp[lane] : -1;
+                const bool mv = lane < nh && h >= i && h <= j && i + j - h != h;
+                hmoved = __ballot(mv) != 0;
+                if (mv) hp[lane] = i + j - h;
+              }
             } else {
               for (int n = tid; n < N; n += TB)
                 if (n < i || n > j || hcnt[n + 1] != hcnt[n]) rn[n] = ro[n];
@@ -1856,13 +1983,20 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             }
             rcur ^= 1;
           }
-          if (kind != PK_PI3) { wsync(); build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane); }   /* hard sites may have moved */
+          FST(7);
+          /* the hard tables only when a hard site moved; the columns' hard-site bits after any
+             pi1 / pi2 (the bits at the hard positions move with the sites) */
+          if (hmoved) { wsync(); build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane); }
+          if (kind != PK_PI3) hb_dirty = true;
+          FST(9);
           wsync();
           STAMP(7);
         } /* batches */
       }
       STAMP(7);
+      FST(0);
       __syncthreads();
+      FST(13);
     } /* sweeps */
 
     /* ---------------- saved sample (mcmc_save_chain, mcmc.c:69-92) */

@@ -14,6 +14,10 @@ import numpy as np  # noqa: E402
 import seriation_amd as sa  # noqa: E402
 
 PH = ["totals+c,d", "sampleab", "logl", "prop draws", "terms pi1", "terms pi2/swap", "terms pi3", "decide/apply/tail"]
+if os.environ.get("SR_FINE"):   # SR_STAMP_FINE builds (tools/build_variant.sh fine "-DSR_STAMPS -DSR_STAMP_FINE")
+    PH = ["misc (K, T4, tail)", "sampleab", "C scan+scalar", "C terms", "C dpp sums", "C barrier", "C decide", "C apply + hard bits",
+          "rng generation", "hard tables", "logl", "A totals", "A c,d draws", "sweep barriers", "C ring words",
+          "C lane-par draws"]
 path = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "tests/golden/datasets/synth_256x512.txt")
 C = int(sys.argv[2]) if len(sys.argv) > 2 else 100
 calls = int(sys.argv[3]) if len(sys.argv) > 3 else 10
@@ -31,6 +35,8 @@ sa.lib().sr_session_debug_counters(s.h, out.ctypes.data_as(ctypes.POINTER(ctypes
 sweeps = calls * 10
 nw = s.block_threads // 64
 per = out[:, 1:1 + nw, :].astype(np.float64) / 2.0 / sweeps   # [chain, wave, phase] cycles per sweep
+if os.environ.get("SR_FINE") and nw <= 8:
+    per = np.concatenate([per, out[:, 9:9 + nw, :].astype(np.float64) / 2.0 / sweeps], axis=2)[:, :, :len(PH)]
 print("dataset %s  chains %d  TB %d  launch wall %.2f ms  (%.1f us/sweep)" % (os.path.basename(path), C, s.block_threads,
                                                                           wall * 1e3, wall * 1e6 / sweeps))
 print("  %-24s %12s %12s %12s" % ("phase (cycles/sweep)", "wave0", "mean wave", "max wave"))

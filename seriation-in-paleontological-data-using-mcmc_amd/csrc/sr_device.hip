@@ -52,6 +52,9 @@ __constant__ double c_log_llo[128] = SR_LOG_LLO_INIT;
 #ifndef SR_HALF_DRAWS
 #define SR_HALF_DRAWS 1
 #endif
+#ifndef SR_GATHER_SCAN
+#define SR_GATHER_SCAN 1
+#endif
 #ifndef SR_CD_FAST
 #define SR_CD_FAST 1
 #endif
@@ -1648,6 +1651,63 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               }
             }
             FST(15);
+#if SR_GATHER_SCAN
+            /* scan, two steps.  (1) the offset chain: proposal p starts where p-1 ended; a 5-bit
+               entry per offset (lane l: offset l in bits 0-15, l + 64 in bits 16-31) holds, per kind,
+               whether the fast path applies there and how many words it consumes (pi1 2 / 3,
+               pi2 2 / 5, pi3 5), so each step is one readlane and a few scalar ops.  (2) lane p
+               gathers its own proposal's record from the tables at its start offset. */
+            uint32_t lent = 0;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const uint32_t e = ((rA1[h] >> 23) & 1u) | ((((rA1[h] >> 22) & 1u) ^ 1u) << 1) | (((rA2[h] >> 23) & 1u) << 2) |
+                                 (((rA2[h] >> 22) & 1u) << 3) | (((rA3[h] >> 23) & 1u) << 4);
+              lent |= e << (16 * h);
+            }
+            const int sstart = pend;
+            int vstart = 0;
+#pragma unroll
+            for (int sI = 1; sI < 16; ++sI) {
+              if (sI < p0 || pend != sI || off + 5 > 128) continue;
+              const int kind = prop_kind(sI);
+              const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)lent, off & 63) >> (16 * (off >> 6));
+              bool ok;
+              int adv;
+              if (kind == PK_PI1) { ok = e & 1u; adv = (e & 2u) ? 3 : 2; }
+              else if (kind == PK_PI2) { ok = (e >> 2) & 1u; adv = (e & 8u) ? 2 : 5; }
+              else { ok = (e >> 4) & 1u; adv = 5; }
+              if (!ok) continue;   /* rejection or zero word: scalar path */
+              vstart = (lane == sI) ? off : vstart;
+              off += adv;
+              pend = sI + 1;
+            }
+            {
+              const int o = vstart, src = o & 63;
+              const bool hi = o >= 64;
+              const int kind = prop_kind(lane & 15);
+              auto g = [&](const uint32_t (&t)[2]) -> uint32_t {
+                const uint32_t a = (uint32_t)__shfl((int)t[0], src), b = (uint32_t)__shfl((int)t[1], src);
+                return hi ? b : a;
+              };
+              const uint32_t g1 = g(rA1), g2 = g(rA2), g3 = g(rA3), gb = g(rB3), gu1 = g(rU1), gu2 = g(rU2);
+              const uint32_t ra = (kind == PK_PI1) ? g1 : (kind == PK_PI2) ? g2 : g3;
+              const uint32_t rb = (kind == PK_PI3) ? gb : 0u;
+              const uint32_t ru = (kind == PK_PI1) ? gu1 : gu2;
+              const bool veto = (ra >> 22) & 1u;
+              const int nd = o + (kind == PK_PI1 ? 2 : (kind == PK_PI2 ? (veto ? 2 : 4) : 4));
+              if (lane >= sstart && lane < pend) {
+                vi = (int)(ra & 2047u);
+                vj = (int)((ra >> 11) & 2047u);
+                vfl = (int)((ra >> 24) & 3u) | (veto ? 4 : 0);
+                vkn = (int)(rb >> 16);
+                vr0 = (int)(rb & 0xffffu);
+                vuw = (int)ru;
+                vnd = nd;
+                voff = nd + (veto ? 0 : 1);
+              }
+            }
+          }
+#else
             /* scan: the batch's proposals at their actual offsets (all-rejected hypothesis) */
 #pragma unroll
             for (int sI = 1; sI < 16; ++sI) {
@@ -1680,6 +1740,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               pend = sI + 1;
             }
           }
+#endif
           for (int p = pend; p < 16; ++p) {   /* scalar path: the batch's first proposal after a fast-path stop */
             if (p0 == 0 && p == 1) break;     /* the swap batch (SR_SWAP_ALONE) */
             if (p > p0) break;                /* only the batch's first proposal goes scalar */

@@ -866,6 +866,17 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
       O += __popc(wk[k]);
     }
   }
+#ifdef SR_STAMP_FINE
+  {   /* window statistics: words per draw, wave max, walk words */
+    const int wn = khi - klo + 1;
+    int wmax = wn;
+    for (int off_ = 32; off_ > 0; off_ >>= 1) wmax = max(wmax, __shfl_xor(wmax, off_));
+    atomicAdd((unsigned long long *)fbk + 26, (unsigned long long)wn);
+    if ((threadIdx.x & 63) == 0) atomicAdd((unsigned long long *)fbk + 27, (unsigned long long)wmax);
+    atomicAdd((unsigned long long *)fbk + 28, (unsigned long long)nk);
+    atomicAdd((unsigned long long *)fbk + 29, 1ull);
+  }
+#endif
   /* pass 1: S over the window; word-start y and end-of-word checkpoints kept in registers */
   const double y0 = exp2_split(qlo);
   double S = 0.0;
@@ -966,16 +977,10 @@ __device__ __forceinline__ void load_walks(const uint32_t *Pm, int M, int N, int
 {
 #pragma unroll
   for (int k = 0; k < NWM; ++k) fw[k] = (k < NW) ? Pm[min(k, NW - 1) * M] : 0u;
-  /* reversed word k = brev(column bits [s, s+32)), s = N - 32 - 32k = 32 (q - 1 - k) + r */
-  const int q = N >> 5, r = N & 31;
+  /* reversed word k = brev(column bits [s, s+32)), s = N - 32 - 32k, read again from LDS (a
+     select over fw[] at the runtime index N/32 - 1 - k made the compiler spill fw to scratch) */
 #pragma unroll
-  for (int k = 0; k < NWM; ++k) {
-    const int wi = q - 1 - k;
-    const uint32_t lo = (wi >= 0) ? sel_u<NWM, uint32_t>(fw, wi) : 0u;
-    const uint32_t hi = (wi + 1 < NW && wi + 1 >= 0) ? sel_u<NWM, uint32_t>(fw, wi + 1) : 0u;
-    const uint32_t v = r ? ((lo >> r) | (hi << (32 - r))) : lo;
-    rw[k] = (k < NW) ? __brev(v) : 0u;
-  }
+  for (int k = 0; k < NWM; ++k) rw[k] = (k < NW) ? walk_word(Pm, M, N, NW, true, k) : 0u;
 }
 
 /* bits of positions [lo, hi] inside word w */
@@ -1369,7 +1374,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       STAMP(0);
       FST(11);
       __syncthreads();
-      FST(13);
+      FST(11);
       {
         int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
 #pragma unroll
@@ -1488,7 +1493,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         wsync();
       }
       STAMP(2);
-      FST(10);
+      FST(0);
 
       /* ============ phase C: the permutation proposals (mcmc.c:237-243), speculatively batched.
          Hypothesis: every remaining proposal is rejected.  A rejected non-vetoed proposal has
@@ -1774,7 +1779,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           if (hb_dirty && one) { if (tid < M) hbc = hard_bits_col(P + tid, M, hl, nh); hb_dirty = false; }
           const uint32_t hb1 = hbc;
           if (one && tid < M) { a1 = sab[tid]; b1 = sab[M + tid]; }
-          FST(7);
+          FST(13);
 #if defined(SR_STAMP_DRAWS)
           STAMP(5);
 #elif defined(SR_STAMP_GIBBS)
@@ -2008,6 +2013,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             }
             col_pre_build(pre + m, Pm, M, NW);   /* the column moved: refresh its prefix table */
           }
+          FST(7);
           /* rpi (double-buffered full permutation, read only at save time) and hard positions */
           bool hmoved = false;   /* wave-uniform */
           {
@@ -2044,7 +2050,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             }
             rcur ^= 1;
           }
-          FST(7);
+          FST(10);
           /* the hard tables only when a hard site moved; the columns' hard-site bits after any
              pi1 / pi2 (the bits at the hard positions move with the sites) */
           if (hmoved) { wsync(); build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane); }
@@ -2057,7 +2063,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       STAMP(7);
       FST(0);
       __syncthreads();
-      FST(13);
+      FST(11);
     } /* sweeps */
 
     /* ---------------- saved sample (mcmc_save_chain, mcmc.c:69-92) */
@@ -2081,7 +2087,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 #ifdef SR_STAMPS
   if (tid == 0) { A.dbg[blockIdx.x * 17 * 8 + 0] += misc[MS_NEXACT]; for (int q_ = 0; q_ < 4; ++q_) A.dbg[blockIdx.x * 17 * 8 + 1 + q_] += misc[MS_FBK + q_];
                   for (int q_ = 0; q_ < 3; ++q_) A.dbg[blockIdx.x * 17 * 8 + 5 + q_] += misc[40 + q_];
-#ifdef SR_STAMP_GIBBS
+#if defined(SR_STAMP_GIBBS) || defined(SR_STAMP_FINE)
                   for (int q_ = 0; q_ < 3; ++q_) A.dbg[blockIdx.x * 17 * 8 + 5 + q_] = misc[MS_FBK + 26 + q_];
                   A.dbg[blockIdx.x * 17 * 8 + 4] = misc[MS_FBK + 29];
 #endif

@@ -15,9 +15,9 @@ import seriation_amd as sa  # noqa: E402
 
 PH = ["totals+c,d", "sampleab", "logl", "prop draws", "terms pi1", "terms pi2/swap", "terms pi3", "decide/apply/tail"]
 if os.environ.get("SR_FINE"):   # SR_STAMP_FINE builds (tools/build_variant.sh fine "-DSR_STAMPS -DSR_STAMP_FINE")
-    PH = ["misc (K, T4, tail)", "sampleab", "C scan+scalar", "C terms", "C dpp sums", "C barrier", "C decide", "C apply + hard bits",
-          "rng generation", "hard tables", "logl", "A totals", "A c,d draws", "sweep barriers", "C ring words",
-          "C lane-par draws"]
+    PH = ["misc (K, T4, logl, tail)", "sampleab", "C scan+scalar", "C terms", "C dpp sums", "C barrier", "C decide",
+          "C apply taxa", "rng generation", "hard tables", "C apply rpi/hp", "A totals + sweep barriers",
+          "A c,d draws", "C setup + hard bits", "C ring words", "C lane-par draws"]
 path = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "tests/golden/datasets/synth_256x512.txt")
 C = int(sys.argv[2]) if len(sys.argv) > 2 else 100
 calls = int(sys.argv[3]) if len(sys.argv) > 3 else 10

@@ -47,6 +47,10 @@ typedef struct {
 int sr_parse_dataset(const char *text, size_t len, int32_t maxs, sr_dataset *out);
 int sr_load_dataset(const char *path, int32_t maxs, sr_dataset *out);
 void sr_free_dataset(sr_dataset *ds);
+/* Binary bit-packed form ("SRBX" header, N hard bytes, N rows of ceil(M/8) bytes; SURVEY §8f-4,
+ * an extension: the reference reads text only).  sr_load_dataset also accepts it (by magic). */
+int sr_save_dataset_bin(const sr_dataset *ds, const char *path);
+int sr_load_dataset_bin(const char *path, sr_dataset *out);
 
 typedef struct {
   int32_t chain_id;   /* names the output directory Chains/chain_NN */

@@ -72,7 +72,8 @@ SINK_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, ctypes
 
 # every symbol include/seriation.h declares (tests/test_abi.py checks the export list)
 PUBLIC_SYMBOLS = [
-    "sr_parse_dataset", "sr_load_dataset", "sr_free_dataset", "sr_default_opts",
+    "sr_parse_dataset", "sr_load_dataset", "sr_free_dataset", "sr_save_dataset_bin", "sr_load_dataset_bin",
+    "sr_default_opts",
     "sr_run_chains", "sr_run_to_dirs", "sr_session_create", "sr_session_set_stream",
     "sr_session_run", "sr_session_sync", "sr_session_records", "sr_session_record_capacity",
     "sr_session_fetch_records", "sr_session_reset_records", "sr_session_state",
@@ -96,6 +97,8 @@ def _lib():
         "sr_parse_dataset": (c_int, [ctypes.c_char_p, ctypes.c_size_t, c_i32, P(sr_dataset)]),
         "sr_load_dataset": (c_int, [ctypes.c_char_p, c_i32, P(sr_dataset)]),
         "sr_free_dataset": (None, [P(sr_dataset)]),
+        "sr_save_dataset_bin": (c_int, [P(sr_dataset), ctypes.c_char_p]),
+        "sr_load_dataset_bin": (c_int, [ctypes.c_char_p, P(sr_dataset)]),
         "sr_default_opts": (None, [P(sr_run_opts)]),
         "sr_run_chains": (c_int, [P(sr_dataset), P(sr_chain_spec), c_i32, P(sr_run_opts), SINK_FN,
                                   c_void_p, P(sr_chain_summary)]),

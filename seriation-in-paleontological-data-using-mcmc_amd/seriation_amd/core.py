@@ -57,6 +57,16 @@ class Dataset:
         _check(L.lib().sr_load_dataset(os.fsencode(path), maxs, ctypes.byref(ds)), "load %s" % path)
         return cls._adopt(ds)
 
+    def save_bin(self, path):
+        """Write the bit-packed binary form (sr_save_dataset_bin)."""
+        _check(L.lib().sr_save_dataset_bin(ctypes.byref(self._c), os.fsencode(path)), "save_bin %s" % path)
+
+    @classmethod
+    def load_bin(cls, path):
+        ds = L.sr_dataset()
+        _check(L.lib().sr_load_dataset_bin(os.fsencode(path), ctypes.byref(ds)), "load_bin %s" % path)
+        return cls._adopt(ds)
+
     @property
     def c(self):
         return self._c

@@ -106,6 +106,8 @@ def main():
     ap.add_argument("--cpu-workers", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--block-threads", type=int, default=0)
+    ap.add_argument("--no-save", action="store_true", help="sample without saving records (SURVEY.md 8(d) "
+                    "asks for both; the default saves one record per call, as the reference's sampling phase)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -155,7 +157,7 @@ def main():
 
     def step():
         sess.reset_records()
-        sess.run(cps, save=True)
+        sess.run(cps, save=not args.no_save)
 
     for _ in range(args.warmup):
         step()
@@ -170,6 +172,9 @@ def main():
         evs[k][1].record(stream)
     # the one collective: every rank's per-chain summary record (exp_data payload of the
     # last step's saved samples) all-gathered, then the one-sigma selection on every rank
+    if args.no_save:   # summaries from the final state (c, d, loglik) when no records were kept
+        sess.reset_records()
+        sess.run(1, save=True)
     _, cdl = sess.fetch_records()
     rows = sd.summaries_from_records(chain_ids, cdl)
     if dist:
@@ -210,8 +215,9 @@ def main():
         "dtype": "f64",
         "data": "synthetic",
         "config": {
-            "workload": "%s %dx%d, %d chains per GPU, "
-                        "%d mcmc_sample calls (%d sweeps) per chain per step, one saved record per call"
+            "workload": ("%s %dx%d, %d chains per GPU, "
+                         "%d mcmc_sample calls (%d sweeps) per chain per step, " +
+                         ("no records saved" if args.no_save else "one saved record per call"))
                         % ("synthetic (tools/gen_synthetic.py seed %d)" % (20261015 if (ds.N, ds.M) == (256, 512)
                                                                           else 20261016)
                            if args.dataset == SYNTH or args.sites else os.path.basename(args.dataset),

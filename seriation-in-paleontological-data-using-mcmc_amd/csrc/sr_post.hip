@@ -33,6 +33,7 @@
 
 #define TR 16   /* output rows per block (4 waves x 4 rows) */
 #define TCOL 64 /* output columns per block (lanes) */
+#define SU 8    /* samples whose operands are loaded together */
 
 struct PostArgs {
   const int16_t *rec;
@@ -63,27 +64,39 @@ __global__ __launch_bounds__(256) void sr_post_kernel(PostArgs P)
   double acc[4] = {0.0, 0.0, 0.0, 0.0}, tot[4] = {0.0, 0.0, 0.0, 0.0};
   for (int ch = 0; ch < P.n_sel; ++ch) {
     const int16_t *base = P.rec + P.chain_off[ch];
-    for (int s = 0; s < P.count; ++s) {
-      const int16_t *row = base + (long long)s * P.row_stride;
-      const int x = row[coff];
-      const int y = (KIND == SRP_ALIVE || KIND == SRP_FALSE_ALIVE || KIND == SRP_FALSE_ONES) ? row[M + cc] : 0;
+    /* samples in blocks of SU: the block's operand loads are issued together, then the
+       accumulation runs over them in sample order (the sum order is unchanged) */
+    for (int s0 = 0; s0 < P.count; s0 += SU) {
+      int xs[SU], ys[SU], prs[SU][4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int r = r0 + k;   /* output row: PAIR_ORDER site i; ALIVE.. site index j; EXP_* 0 */
-        int v;
-        if (KIND == SRP_PAIR_ORDER) {
-          const int pr = row[2 * M + min(r, N - 1)];   /* wave-uniform */
-          v = (r == col) ? -1 : (pr < x ? 1 : 0);      /* generate_po_matrix, script.py:183-188 */
-        } else if (KIND == SRP_ALIVE) {
-          v = (r >= x && r <= y) ? 1 : 0;              /* script.py:326 */
-        } else if (KIND == SRP_FALSE_ALIVE) {
-          v = (r < x || r > y) ? 1 : 0;                /* script.py:370 */
-        } else if (KIND == SRP_FALSE_ONES) {
-          v = (xo[k] == 1 && !(r >= x && r <= y)) ? 1 : 0;   /* script.py:408-413 */
-        } else {
-          v = x;                                       /* EXP_PI: pi[site]; EXP_A: a[taxon] */
+      for (int u = 0; u < SU; ++u) {
+        const int16_t *row = base + (long long)min(s0 + u, P.count - 1) * P.row_stride;
+        xs[u] = row[coff];
+        ys[u] = (KIND == SRP_ALIVE || KIND == SRP_FALSE_ALIVE || KIND == SRP_FALSE_ONES) ? row[M + cc] : 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) prs[u][k] = (KIND == SRP_PAIR_ORDER) ? row[2 * M + min(r0 + k, N - 1)] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        if (s0 + u >= P.count) break;
+        const int x = xs[u], y = ys[u];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int r = r0 + k;   /* output row: PAIR_ORDER site i; ALIVE.. site index j; EXP_* 0 */
+          int v;
+          if (KIND == SRP_PAIR_ORDER) {
+            v = (r == col) ? -1 : (prs[u][k] < x ? 1 : 0);   /* generate_po_matrix, script.py:183-188 */
+          } else if (KIND == SRP_ALIVE) {
+            v = (r >= x && r <= y) ? 1 : 0;                    /* script.py:326 */
+          } else if (KIND == SRP_FALSE_ALIVE) {
+            v = (r < x || r > y) ? 1 : 0;                      /* script.py:370 */
+          } else if (KIND == SRP_FALSE_ONES) {
+            v = (xo[k] == 1 && !(r >= x && r <= y)) ? 1 : 0;   /* script.py:408-413 */
+          } else {
+            v = x;                                             /* EXP_PI: pi[site]; EXP_A: a[taxon] */
+          }
+          acc[k] = acc[k] + (double)v;
         }
-        acc[k] = acc[k] + (double)v;
       }
     }
 #pragma unroll

@@ -107,7 +107,7 @@ __host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB, bo
   L.scnt = o;  o = sr_al16(o + g * 4 * M * 4);
   L.hpw = o;   o = sr_al16(o + (size_t)NWV * SR_NHMAX * 4);           /* per wave: hard positions */
   L.hbw = o;   o = sr_al16(o + (size_t)NWV * NW * 4);                 /* per wave: hard bitmap */
-  L.t4 = o;    o = sr_al16(o + (size_t)NWV * 96 * 8);                 /* per wave: 4-entry step tables */
+  L.t4 = o;    o = sr_al16(o + (size_t)NWV * 160 * 8);                /* per wave: 4-entry step tables (T4STRIDE) */
   L.pre = o;   o = sr_al16(o + g * (NW + 1) * M * 2);                 /* column prefix ones per word boundary */
   L.part = o;  o = sr_al16(o + (size_t)2 * 16 * NWV * 8 * 4);         /* [2][proposal][wave] count sums */
   L.tot = o;   o = sr_al16(o + (size_t)2 * NWV * 4 * 4);               /* [2][wave] t0, f0, t1, f1 */
@@ -641,6 +641,17 @@ __device__ __forceinline__ int walk_prefix(const uint32_t *Pm, int M, int N, int
   return s;
 }
 
+/* The 4-entry step tables of a wave, interleaved: entry (c, nib) = {sum of the first c prefix
+ * products of the nibble's ratios, product of all four} -- one 16-byte LDS read per group
+ * (c = valid entries of the group, 0..4; the product is the same in every row). */
+#define T4STRIDE 160   /* doubles per wave */
+__device__ __forceinline__ double2 t4sp(const double *T4, int c, uint32_t nib)
+{
+  return *reinterpret_cast<const double2 *>(T4 + 2 * (c * 16 + (int)nib));
+}
+__device__ __forceinline__ double t4s(const double *T4, int c, uint32_t nib) { return T4[2 * (c * 16 + (int)nib)]; }
+__device__ __forceinline__ double t4p(const double *T4, uint32_t nib) { return T4[2 * (64 + (int)nib) + 1]; }
+
 /* 2^q (q <= ~0) to ~1.6e-7 relative: exact f64 split q = n + f, f in [0,1), v_exp_f32(f) */
 __device__ __forceinline__ double exp2_split(double q)
 {
@@ -725,8 +736,9 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
       for (int g = 0; g < 8; ++g) {
         const uint32_t nib = (ww >> (4 * g)) & 15u;
         const int c = min(max(nb - 4 * g, 0), 4);
-        S = __builtin_fma(y, T4[c * 16 + nib], S);
-        y = y * T4[80 + nib];
+        const double2 t = t4sp(T4, c, nib);
+        S = __builtin_fma(y, t.x, S);
+        y = y * t.y;
       }
       ck[k * ckstride] = S;
     }
@@ -744,7 +756,7 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
         for (int k = klo; k < j; ++k) {   /* words before j are full (only the walk's last word is partial) */
       const uint32_t ww = walk_word(Pm, M, N, NW, rev, k);
 #pragma unroll
-      for (int g = 0; g < 8; ++g) y = y * T4[80 + ((ww >> (4 * g)) & 15u)];
+      for (int g = 0; g < 8; ++g) y = y * t4p(T4, (ww >> (4 * g)) & 15u);
     }
     const double Sp0 = (j == klo) ? 0.0 : ck[(j - 1) * ckstride];
     const int w0 = 32 * j;
@@ -761,9 +773,10 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
         const uint32_t nib = (ww >> (4 * g)) & 15u;
         const int c = min(max(nb - 4 * g, 0), 4);
         gy[g] = yy;
-        acc = __builtin_fma(yy, T4[c * 16 + nib], acc);
+        const double2 t = t4sp(T4, c, nib);
+        acc = __builtin_fma(yy, t.x, acc);
         gsum[g] = acc;
-        yy = yy * T4[80 + nib];
+        yy = yy * t.y;
       }
 #pragma unroll
       for (int g = 0; g < 8; ++g) ng += (g < nvg && gsum[g] * inv < u) ? 1 : 0;
@@ -777,8 +790,8 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
     }
     const uint32_t nibs = (ww >> (4 * gsel)) & 15u;
     const int cmax = min(nb - 4 * gsel, 4);
-    const double P1 = __builtin_fma(ys, T4[16 + nibs], base), P2 = __builtin_fma(ys, T4[32 + nibs], base);
-    const double P3 = __builtin_fma(ys, T4[48 + nibs], base), P4 = __builtin_fma(ys, T4[64 + nibs], base);
+    const double P1 = __builtin_fma(ys, t4s(T4, 1, nibs), base), P2 = __builtin_fma(ys, t4s(T4, 2, nibs), base);
+    const double P3 = __builtin_fma(ys, t4s(T4, 3, nibs), base), P4 = __builtin_fma(ys, t4s(T4, 4, nibs), base);
     const int nc = ((cmax > 1 && P1 * inv < u) ? 1 : 0) + ((cmax > 2 && P2 * inv < u) ? 1 : 0) +
                    ((cmax > 3 && P3 * inv < u) ? 1 : 0);
     const double Ph = (nc == 0) ? P1 : (nc == 1) ? P2 : (nc == 2) ? P3 : P4;
@@ -893,8 +906,9 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
       for (int g = 0; g < 8; ++g) {
         const uint32_t nib = (wk[k] >> (4 * g)) & 15u;
         const int c = min(max(nbe - 4 * g, 0), 4);
-        S = __builtin_fma(yk, T4[c * 16 + nib], S);
-        yk = yk * T4[80 + nib];
+        const double2 t = t4sp(T4, c, nib);
+        S = __builtin_fma(yk, t.x, S);
+        yk = yk * t.y;
       }
       y = act ? yk : y;
       ckr[k] = S;
@@ -928,9 +942,10 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
         const uint32_t nib = (ww >> (4 * g)) & 15u;
         const int c = min(max(nb - 4 * g, 0), 4);
         gy[g] = yy;
-        acc = __builtin_fma(yy, T4[c * 16 + nib], acc);
+        const double2 t = t4sp(T4, c, nib);
+        acc = __builtin_fma(yy, t.x, acc);
         gsum[g] = acc;
-        yy = yy * T4[80 + nib];
+        yy = yy * t.y;
       }
 #pragma unroll
       for (int g = 0; g < 8; ++g) ng += (g < nvg && gsum[g] * inv < u) ? 1 : 0;
@@ -944,8 +959,8 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
     }
     const uint32_t nibs = (ww >> (4 * gsel)) & 15u;
     const int cmax = min(nb - 4 * gsel, 4);
-    const double P1 = __builtin_fma(ys, T4[16 + nibs], base), P2 = __builtin_fma(ys, T4[32 + nibs], base);
-    const double P3 = __builtin_fma(ys, T4[48 + nibs], base), P4 = __builtin_fma(ys, T4[64 + nibs], base);
+    const double P1 = __builtin_fma(ys, t4s(T4, 1, nibs), base), P2 = __builtin_fma(ys, t4s(T4, 2, nibs), base);
+    const double P3 = __builtin_fma(ys, t4s(T4, 3, nibs), base), P4 = __builtin_fma(ys, t4s(T4, 4, nibs), base);
     const int nc = ((cmax > 1 && P1 * inv < u) ? 1 : 0) + ((cmax > 2 && P2 * inv < u) ? 1 : 0) +
                    ((cmax > 3 && P3 * inv < u) ? 1 : 0);
     const double Ph = (nc == 0) ? P1 : (nc == 1) ? P2 : (nc == 2) ? P3 : P4;
@@ -1298,7 +1313,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   int32_t *scnt = GM ? A.cnt + (size_t)chain * 4 * M : (int32_t *)(smem + L.scnt);  /* t0[M], f0[M], t1[M], f1[M] */
   int *hp = (int *)(smem + L.hpw) + wave * SR_NHMAX;   /* this wave's copy of the hard positions */
   uint32_t *hbw = (uint32_t *)(smem + L.hbw) + wave * NW;   /* this wave's hard bitmap */
-  double *T4w = (double *)(smem + L.t4) + wave * 96;     /* this wave's 4-step tables */
+  double *T4w = (double *)(smem + L.t4) + wave * T4STRIDE;   /* this wave's 4-step tables */
   int *part = (int *)(smem + L.part);
   int *tot = (int *)(smem + L.tot);
   double *xs = (double *)(smem + L.xs) + wave;
@@ -1402,13 +1417,15 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       const double rA = sr_exp_m(K.cc - K.d, &tb), rB = sr_exp_m(K.c - K.dd, &tb);   /* 2^-vA, 2^-vB */
       if (lane < 16) {   /* per-wave tables for 4 walk entries with bits = lane */
         double pr = 1.0, sm = 1.0;
-        T4w[lane] = 0.0;
-        T4w[16 + lane] = sm;
-        pr = pr * ((lane & 1) ? rB : rA); sm = sm + pr; T4w[32 + lane] = sm;
-        pr = pr * ((lane & 2) ? rB : rA); sm = sm + pr; T4w[48 + lane] = sm;
-        pr = pr * ((lane & 4) ? rB : rA); sm = sm + pr; T4w[64 + lane] = sm;
+        double sc[5];
+        sc[0] = 0.0;
+        sc[1] = sm;
+        pr = pr * ((lane & 1) ? rB : rA); sm = sm + pr; sc[2] = sm;
+        pr = pr * ((lane & 2) ? rB : rA); sm = sm + pr; sc[3] = sm;
+        pr = pr * ((lane & 4) ? rB : rA); sm = sm + pr; sc[4] = sm;
         pr = pr * ((lane & 8) ? rB : rA);
-        T4w[80 + lane] = pr;
+#pragma unroll
+        for (int c = 0; c < 5; ++c) { T4w[2 * (c * 16 + lane)] = sc[c]; T4w[2 * (c * 16 + lane) + 1] = pr; }
       }
       wsync();
 

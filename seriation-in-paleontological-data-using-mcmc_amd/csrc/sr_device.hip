@@ -992,10 +992,29 @@ __device__ __forceinline__ void load_walks(const uint32_t *Pm, int M, int N, int
 {
 #pragma unroll
   for (int k = 0; k < NWM; ++k) fw[k] = (k < NW) ? Pm[min(k, NW - 1) * M] : 0u;
-  /* reversed word k = brev(column bits [s, s+32)), s = N - 32 - 32k, read again from LDS (a
-     select over fw[] at the runtime index N/32 - 1 - k made the compiler spill fw to scratch) */
+  /* reversed word k = brev(column bits [s, s+32)), s = N - 32 - 32k = 32 (q - 1 - k) + r: built
+     from fw[] with compile-time indices inside a block-uniform switch on q = N / 32 (a select at
+     a runtime index made the compiler spill fw to scratch) */
+  const int q = N >> 5, r = N & 31;
+  bool done = false;
 #pragma unroll
-  for (int k = 0; k < NWM; ++k) rw[k] = (k < NW) ? walk_word(Pm, M, N, NW, true, k) : 0u;
+  for (int Q = 0; Q <= NWM; ++Q) {
+    if (q != Q) continue;
+#pragma unroll
+    for (int k = 0; k < NWM; ++k) {
+      const int wi = Q - 1 - k;
+      const uint32_t lo = (wi >= 0 && wi < NWM) ? fw[wi >= 0 && wi < NWM ? wi : 0] : 0u;
+      const uint32_t hi = (wi + 1 >= 0 && wi + 1 < NWM) ? fw[(wi + 1 >= 0 && wi + 1 < NWM) ? wi + 1 : 0] : 0u;
+      const uint32_t hiv = (wi + 1 < NW) ? hi : 0u;
+      const uint32_t v = r ? ((lo >> r) | (hiv << (32 - r))) : lo;
+      rw[k] = (k < NW) ? __brev(v) : 0u;
+    }
+    done = true;
+  }
+  if (!done) {
+#pragma unroll
+    for (int k = 0; k < NWM; ++k) rw[k] = (k < NW) ? walk_word(Pm, M, N, NW, true, k) : 0u;
+  }
 }
 
 /* bits of positions [lo, hi] inside word w */

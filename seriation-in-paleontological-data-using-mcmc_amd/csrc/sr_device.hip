@@ -61,6 +61,12 @@ __constant__ double c_log_llo[128] = SR_LOG_LLO_INIT;
 #ifndef SR_SWAP_ALONE
 #define SR_SWAP_ALONE 1
 #endif
+#ifndef SR_PI1_BALLOT
+#define SR_PI1_BALLOT 1
+#endif
+#ifndef SR_PRE_INCR
+#define SR_PRE_INCR 1
+#endif
 
 struct KArgs {
   int N, M, NW, nh, nchains;
@@ -1849,7 +1855,11 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               const int fl = __builtin_amdgcn_readlane(vfl, sI);
               if (sI >= p0 && sI < pend && !(fl & 4)) {
                 int X0, X1, Y0, Y1;
-                if (pack) {   /* per-wave sums of (dt + N) and |dt| fit 16-bit fields (N < 512) */
+                if (SR_PI1_BALLOT && prop_kind(sI) == PK_PI1) {   /* pi1: dt in {-1, 0, 1}: |dt| sums are ballot counts */
+                  const uint32_t u1 = (uint32_t)wave_sum_i32((int)((uint32_t)(d0s[sI] + 1) | ((uint32_t)(d1s[sI] + 1) << 16)));
+                  X0 = (int)(u1 & 0xffffu) - 64; X1 = (int)(u1 >> 16) - 64;
+                  Y0 = (int)__popcll(__ballot(d0s[sI] != 0)); Y1 = (int)__popcll(__ballot(d1s[sI] != 0));
+                } else if (pack) {   /* per-wave sums of (dt + N) and |dt| fit 16-bit fields (N < 512) */
                   const uint32_t u1 = (uint32_t)wave_sum_i32((int)((uint32_t)(d0s[sI] + N) | ((uint32_t)(d1s[sI] + N) << 16)));
                   const uint32_t u2 = (uint32_t)wave_sum_i32((int)((uint32_t)abs(d0s[sI]) | ((uint32_t)abs(d1s[sI]) << 16)));
                   X0 = (int)(u1 & 0xffffu) - 64 * N; X1 = (int)(u1 >> 16) - 64 * N;
@@ -2047,7 +2057,16 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 }
               }
             }
+#if SR_PRE_INCR
+            {   /* the move permutes positions [lo, hi] only: prefix entries (lo/32, hi/32] change */
+              const int lo = min(i, j), hi = max(i, j), rlo = (lo >> 5) + 1, rhi = hi >> 5;
+              uint16_t *prem = pre + m;
+              int sacc = prem[(rlo - 1) * M];
+              for (int r = rlo; r <= rhi; ++r) { sacc += __popc(Pm[(r - 1) * M]); prem[r * M] = (uint16_t)sacc; }
+            }
+#else
             col_pre_build(pre + m, Pm, M, NW);   /* the column moved: refresh its prefix table */
+#endif
           }
           FST(7);
           /* rpi (double-buffered full permutation, read only at save time) and hard positions */

@@ -3,9 +3,9 @@
 * every committed golden fixture (tests/golden/chains.json) reproduced by the HIP path;
 * config 2: g10s10, 100 chains (seeds 1..100), 1000 burn-in + 1000 saved mcmc_sample
   calls -- every saved sample bit-identical to the oracle, exp_data identical;
-* the statistical known answer of the reference (Docs/Report.pdf Table 1, g10s10 with 8
-  selected chains: E[c] 0.0119, E[d] 0.5127, CORRMN 0.940) within the acceptance band
-  proposed in SURVEY.md §8c (+-0.002, +-0.03, +-0.02);
+* the statistical known answers of the reference (Docs/Report.pdf Table 1: g10s10 with 8
+  selected chains: E[c] 0.0119, E[d] 0.5127, CORRMN 0.940; g5s5 and g10s2 with 2 each)
+  within the acceptance band proposed in SURVEY.md §8c (+-0.002, +-0.03, +-0.02);
 * the script.py launcher writes the same Chains/ tree as the oracle CLI.
 """
 import hashlib
@@ -108,3 +108,13 @@ def test_launcher_matches_oracle_cli(tmp_path):
             a = (d / "Chains" / "chain_00" / f).read_bytes()
             b = (tmp_path / "gpu" / "Chains" / ("chain_%02d" % k) / f).read_bytes()
             assert a == b, (k, f)
+
+
+@pytest.mark.parametrize("name", ["g5s5", "g10s2"])
+def test_table1_other_rows(name):
+    """The other two rows of Report Table 1 (2 selected chains each), same band as g10s10."""
+    import table1
+    r = table1.run_row(name)
+    print("%s selected %s: E[c]=%.4f E[d]=%.4f CORRMN=%.4f" % (name, r["selected"], r["E_c"], r["E_d"], r["CORRMN"]))
+    assert 1 <= len(r["selected"]) <= 100
+    assert all(r["within_band"]), r

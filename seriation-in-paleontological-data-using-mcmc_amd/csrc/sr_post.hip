@@ -21,8 +21,9 @@
  * pi[site] = position (mcmc_save_chain, mcmc.c:69-92), one row per saved mcmc_sample call;
  * chain k's rows start at rec + chain_off[k], consecutive rows row_stride apart.  A block owns a
  * tile of 16 output rows x 64 output columns: lane = column (its operand loads coalesce across
- * the wave), each thread keeps 4 rows' accumulators in registers; the row operand of PAIR_ORDER
- * (pi of the row site) is wave-uniform and loaded through the scalar unit.  The records of the
+ * the wave), each thread keeps 4 rows' accumulators in registers.  Operands are staged through
+ * LDS in chunks of CS samples, the next chunk's loads in flight while the current one is summed;
+ * the row operand of PAIR_ORDER (pi of the row site) is an LDS broadcast.  The records of the
  * selected chains (at most a few MB) stay L2/MALL-resident across the tiles: the kernel is
  * bound by the dependent f64 add chains, one per element.
  */
@@ -33,7 +34,7 @@
 
 #define TR 16   /* output rows per block (4 waves x 4 rows) */
 #define TCOL 64 /* output columns per block (lanes) */
-#define SU 8    /* samples whose operands are loaded together */
+#define CS 64   /* samples per LDS-staged chunk (two chunks: one consumed, one in flight) */
 
 struct PostArgs {
   const int16_t *rec;
@@ -62,47 +63,94 @@ __global__ __launch_bounds__(256) void sr_post_kernel(PostArgs P)
     for (int k = 0; k < 4; ++k) xo[k] = (r0 + k < P.R && cok) ? P.X[(size_t)(r0 + k) * M + cc] : 0;
   }
   double acc[4] = {0.0, 0.0, 0.0, 0.0}, tot[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int ch = 0; ch < P.n_sel; ++ch) {
-    const int16_t *base = P.rec + P.chain_off[ch];
-    /* samples in blocks of SU: the block's operand loads are issued together, then the
-       accumulation runs over them in sample order (the sum order is unchanged) */
-    for (int s0 = 0; s0 < P.count; s0 += SU) {
-      int xs[SU], ys[SU], prs[SU][4];
+  auto chain_end = [&]() {
 #pragma unroll
-      for (int u = 0; u < SU; ++u) {
-        const int16_t *row = base + (long long)min(s0 + u, P.count - 1) * P.row_stride;
-        xs[u] = row[coff];
-        ys[u] = (KIND == SRP_ALIVE || KIND == SRP_FALSE_ALIVE || KIND == SRP_FALSE_ONES) ? row[M + cc] : 0;
+    for (int k = 0; k < 4; ++k) {
+      acc[k] = acc[k] / 1000.0;
+      tot[k] = (KIND == SRP_EXP_PI) ? acc[k] : tot[k] + acc[k];
+    }
+  };
+  /* The selected chains' samples form one stream g = chain * count + s (selection order, then
+     sample order), consumed in chunks of CS samples.  A chunk's operands (x, y per column, the
+     pair-order row operands) are staged in LDS by the whole block; chunk c+1's global loads are
+     in flight while chunk c is accumulated, so one memory latency is paid per chunk, not per
+     sample.  The accumulation order per element is still the script's sample order. */
+  constexpr bool NEEDY = (KIND == SRP_ALIVE || KIND == SRP_FALSE_ALIVE || KIND == SRP_FALSE_ONES);
+  constexpr bool NEEDP = (KIND == SRP_PAIR_ORDER);
+  __shared__ int16_t xsh[2][CS][TCOL];
+  __shared__ int16_t ysh[NEEDY ? 2 : 1][NEEDY ? CS : 1][TCOL];
+  __shared__ int16_t psh[NEEDP ? 2 : 1][NEEDP ? CS : 1][TR];
+  const unsigned total = (unsigned)P.n_sel * (unsigned)P.count;
+  const int t = threadIdx.x;
+  const int prow = min((int)blockIdx.y * TR + (t & (TR - 1)), N - 1);   /* pair-order row operand */
+  int16_t lx[CS / 4], ly[NEEDY ? CS / 4 : 1], lp[NEEDP ? CS / 16 : 1];
+  auto rowp = [&](unsigned g) -> const int16_t * {
+    g = min(g, total - 1u);
+    const unsigned ch = g / (unsigned)P.count, sm = g - ch * (unsigned)P.count;
+    return P.rec + P.chain_off[ch] + (long long)sm * P.row_stride;
+  };
+  auto load_chunk = [&](unsigned g0) {   /* thread t: samples wave + 4k (x, y), t/16 + 16k (p) */
 #pragma unroll
-        for (int k = 0; k < 4; ++k) prs[u][k] = (KIND == SRP_PAIR_ORDER) ? row[2 * M + min(r0 + k, N - 1)] : 0;
-      }
+    for (int k = 0; k < CS / 4; ++k) {
+      const int16_t *row = rowp(g0 + wave + 4 * k);
+      lx[k] = row[coff];
+      if (NEEDY) ly[k] = row[M + cc];
+    }
+    if (NEEDP) {
 #pragma unroll
-      for (int u = 0; u < SU; ++u) {
-        if (s0 + u >= P.count) break;
-        const int x = xs[u], y = ys[u];
+      for (int k = 0; k < CS / 16; ++k) lp[k] = rowp(g0 + (t >> 4) + 16 * k)[2 * M + prow];
+    }
+  };
+  auto store_chunk = [&](int b) {
+#pragma unroll
+    for (int k = 0; k < CS / 4; ++k) {
+      xsh[b][wave + 4 * k][lane] = lx[k];
+      if (NEEDY) ysh[b][wave + 4 * k][lane] = ly[k];
+    }
+    if (NEEDP) {
+#pragma unroll
+      for (int k = 0; k < CS / 16; ++k) psh[b][(t >> 4) + 16 * k][t & (TR - 1)] = lp[k];
+    }
+  };
+  if (total == 0) {
+    for (int ch = 0; ch < P.n_sel; ++ch) chain_end();
+  } else {
+    const unsigned nchunk = (total + CS - 1) / CS;
+    load_chunk(0);
+    store_chunk(0);
+    __syncthreads();
+    int sm = 0;   /* sample index inside the current chain (uniform) */
+    for (unsigned c = 0; c < nchunk; ++c) {
+      const int b = c & 1;
+      if (c + 1 < nchunk) load_chunk((c + 1) * CS);
+      const unsigned g0 = c * CS;
+      const int nu = (int)min((unsigned)CS, total - g0);
+#pragma unroll 16
+      for (int u = 0; u < nu; ++u) {   /* unrolled: the LDS reads run ahead of the add chain */
+        const int x = xsh[b][u][lane];
+        const int y = NEEDY ? ysh[NEEDY ? b : 0][NEEDY ? u : 0][lane] : 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const int r = r0 + k;   /* output row: PAIR_ORDER site i; ALIVE.. site index j; EXP_* 0 */
           int v;
           if (KIND == SRP_PAIR_ORDER) {
-            v = (r == col) ? -1 : (prs[u][k] < x ? 1 : 0);   /* generate_po_matrix, script.py:183-188 */
+            const int pr = psh[NEEDP ? b : 0][NEEDP ? u : 0][wave * 4 + k];
+            v = (r == col) ? -1 : (pr < x ? 1 : 0);                /* generate_po_matrix, script.py:183-188 */
           } else if (KIND == SRP_ALIVE) {
-            v = (r >= x && r <= y) ? 1 : 0;                    /* script.py:326 */
+            v = (r >= x && r <= y) ? 1 : 0;                       /* script.py:326 */
           } else if (KIND == SRP_FALSE_ALIVE) {
-            v = (r < x || r > y) ? 1 : 0;                      /* script.py:370 */
+            v = (r < x || r > y) ? 1 : 0;                         /* script.py:370 */
           } else if (KIND == SRP_FALSE_ONES) {
-            v = (xo[k] == 1 && !(r >= x && r <= y)) ? 1 : 0;   /* script.py:408-413 */
+            v = (xo[k] == 1 && !(r >= x && r <= y)) ? 1 : 0;      /* script.py:408-413 */
           } else {
-            v = x;                                             /* EXP_PI: pi[site]; EXP_A: a[taxon] */
+            v = x;                                                /* EXP_PI: pi[site]; EXP_A: a[taxon] */
           }
           acc[k] = acc[k] + (double)v;
         }
+        if (++sm == P.count) { sm = 0; chain_end(); }
       }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      acc[k] = acc[k] / 1000.0;
-      tot[k] = (KIND == SRP_EXP_PI) ? acc[k] : tot[k] + acc[k];
+      if (c + 1 < nchunk) store_chunk(b ^ 1);   /* buffer b^1 was last read before the previous barrier */
+      __syncthreads();
     }
   }
   if (cok) {
@@ -135,6 +183,7 @@ extern "C" int srp_posterior_dev(int device, void *stream, int kind, const int16
     default: return -1;
   }
   if (n_sel <= 0 || count < 0 || N < 1 || M < 1 || chains_selected == 0) return -1;
+  if ((long long)n_sel * count >= (1LL << 31)) return -1;   /* the kernel indexes samples in 32 bits */
   if (kind == SRP_FALSE_ONES && !X_host) return -1;
   {
     HIPCHK(hipSetDevice(device));

@@ -222,11 +222,13 @@ def run_chains(dataset, seeds, burnin_calls=1000, sample_calls=1000, sweeps_per_
     return summ, recs
 
 
-def run_to_dirs(dataset, seeds, root=".", chain_ids=None, burnin_calls=1000, sample_calls=1000, device=0):
-    """sr_run_to_dirs: writes Chains/chain_NN/*.csv under root like the reference main()."""
+def run_to_dirs(dataset, seeds, root=".", chain_ids=None, burnin_calls=1000, sample_calls=1000, device=0,
+                sweeps_per_call=10):
+    """sr_run_to_dirs: writes Chains/chain_NN/*.csv under root like the reference main().
+    sweeps_per_call is the thinning (the reference's mcmc_sample runs 10, mcmc.c:225)."""
     n = len(seeds)
     specs = make_specs(seeds, chain_ids)
-    opts = make_opts(burnin_calls, sample_calls, 10, device)
+    opts = make_opts(burnin_calls, sample_calls, sweeps_per_call, device)
     out = (L.sr_chain_summary * n)()
     rc = L.lib().sr_run_to_dirs(ctypes.byref(dataset.c), specs, n, ctypes.byref(opts),
                                 os.fsencode(root), out)

@@ -43,7 +43,7 @@ def run_chain(chain_index, old_seeds, dataset, burnin_calls=1000, sample_calls=1
 
 
 def run_all_chains(dataset, n_chains=100, seeds=None, devices=None, burnin_calls=1000, sample_calls=1000,
-                   root=".", verbose=True):
+                   root=".", verbose=True, sweeps_per_call=10):
     """script.py:48-67: run all chains and print the wall time (seconds, 2 decimals).
 
     seeds: None -> unique 1-byte urandom seeds exactly like the reference (only 256 exist, so
@@ -64,7 +64,8 @@ def run_all_chains(dataset, n_chains=100, seeds=None, devices=None, burnin_calls
     def work(k, dev, idx):
         try:
             results[k] = core.run_to_dirs(ds, [seeds[i] for i in idx], root=root, chain_ids=list(idx),
-                                          burnin_calls=burnin_calls, sample_calls=sample_calls, device=dev)
+                                          burnin_calls=burnin_calls, sample_calls=sample_calls, device=dev,
+                                          sweeps_per_call=sweeps_per_call)
         except Exception as e:  # re-raised below
             errors.append(e)
 

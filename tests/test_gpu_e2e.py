@@ -118,3 +118,39 @@ def test_table1_other_rows(name):
     print("%s selected %s: E[c]=%.4f E[d]=%.4f CORRMN=%.4f" % (name, r["selected"], r["E_c"], r["E_d"], r["CORRMN"]))
     assert 1 <= len(r["selected"]) <= 100
     assert all(r["within_band"]), r
+
+
+def test_batched_cli_matches_oracle_cli(tmp_path):
+    """python -m seriation_amd (one session, many chains) writes the oracle CLI's files."""
+    import sys
+    pkg = os.path.join(os.path.dirname(HERE), "seriation-in-paleontological-data-using-mcmc_amd")
+    rc = subprocess.call([sys.executable, "-m", "seriation_amd", os.path.join(DS, "g10s10.txt"), "--chains", "3",
+                          "--burnin", "20", "--samples", "30", "--seed-base", "9", "--root", str(tmp_path / "gpu"),
+                          "--select", "2"], cwd=pkg, stdout=subprocess.DEVNULL)
+    assert rc == 0
+    cli = os.path.join(os.path.dirname(HERE), "oracle", "build", "mcmc_oracle")
+    for k in range(3):
+        d = tmp_path / ("cpu%d" % k)
+        (d / "Chains" / "chain_00").mkdir(parents=True)
+        with open(os.path.join(DS, "g10s10.txt"), "rb") as fin:
+            subprocess.check_call([cli, "0", "20", "30"], cwd=str(d), stdin=fin,
+                                  env=dict(os.environ, GSL_RNG_SEED=str(9 + k)), stderr=subprocess.DEVNULL)
+        for f in ("chain_data.csv", "exp_data.csv", "taxa.csv", "sites.csv", "hard_sites.csv"):
+            assert (d / "Chains" / "chain_00" / f).read_bytes() == \
+                (tmp_path / "gpu" / "Chains" / ("chain_%02d" % k) / f).read_bytes(), (k, f)
+
+
+@pytest.mark.parametrize("sweeps", [1, 5, 23])
+def test_thinning_bitexact(sweeps):
+    """sweeps_per_call other than the reference's 10 (the --thin flag) against the oracle."""
+    text = _text("g5s5.txt")
+    ds = sa.Dataset.parse(text)
+    seeds = [3, 4]
+    summ, (ri, rd) = sa.run_chains(ds, seeds, burnin_calls=7, sample_calls=11, sweeps_per_call=sweeps,
+                                   keep_records=True)
+    for k, s in enumerate(seeds):
+        o = oracle_ref.run_chain(text, s, 7, 11, sweeps=sweeps)
+        assert o["rc"] == 0
+        assert np.array_equal(ri[k], o["rec_int"]), (sweeps, s)
+        assert np.array_equal(rd[k].view(np.uint64), o["rec_dbl"].view(np.uint64)), (sweeps, s)
+        assert [summ[k]["exp_loglik"], summ[k]["exp_c"], summ[k]["exp_d"]] == list(o["exp"])

@@ -2,6 +2,7 @@
 import os
 
 import numpy as np
+import pytest
 
 from seriation_amd import launcher
 
@@ -55,3 +56,12 @@ def test_seed_generation_like_script_py():
     seeds = [launcher._unique_seed(old) for _ in range(20)]
     assert len(set(seeds)) == 20 and len(old) == 20
     assert all(0 <= x <= 255 for x in seeds)
+
+
+def test_batched_cli_rejects_bad_flags(capsys):
+    """Argument errors are reported before anything touches a GPU."""
+    from seriation_amd.__main__ import main
+    for argv in (["x.txt", "--chains", "0"], ["x.txt", "--thin", "0"], ["x.txt", "--chains", "300"]):
+        with pytest.raises(SystemExit) as e:
+            main(argv)
+        assert e.value.code == 2

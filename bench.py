@@ -175,7 +175,9 @@ def main():
     if args.no_save:   # summaries from the final state (c, d, loglik) when no records were kept
         sess.reset_records()
         sess.run(1, save=True)
-    _, cdl = sess.fetch_records()
+    stream.synchronize()
+    t_kernels = time.perf_counter()
+    cdl = sess.fetch_cdl()
     rows = sd.summaries_from_records(chain_ids, cdl)
     if dist:
         gathered = sd.gather_summaries(rows, C * world, device="cuda")
@@ -186,6 +188,7 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    tail_ms = (time.perf_counter() - t_kernels) * 1e3
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -241,6 +244,9 @@ def main():
             "launch_bytes": launch_bytes,
         },
         "cpu_baseline": cpu,
+        "timing": {"kernel_ms_per_step": kernel_ms, "gather_select_ms": tail_ms,
+                   "note": "gather_select_ms: after the last kernel, the record fetch, summary all-gather "
+                           "and one-sigma selection (inside the timed region)"},
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

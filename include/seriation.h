@@ -111,7 +111,8 @@ int sr_session_run(sr_session *s, int32_t calls, int32_t save);
 int sr_session_sync(sr_session *s);
 int32_t sr_session_records(const sr_session *s);
 int32_t sr_session_record_capacity(const sr_session *s);
-/* ab_pi: [n_chains][count][2M+N] int16 (a, b, pi); cdl: [n_chains][count][3] (c, d, loglik) */
+/* ab_pi: [n_chains][count][2M+N] int16 (a, b, pi); cdl: [n_chains][count][3] (c, d, loglik);
+   either may be NULL (not fetched) */
 int sr_session_fetch_records(sr_session *s, int32_t first, int32_t count, int16_t *ab_pi, double *cdl);
 int sr_session_reset_records(sr_session *s);
 /* Current state of one chain (any pointer may be NULL); counts = t0,f0,t1,f1 (4*M). */

@@ -2342,14 +2342,18 @@ extern "C" int srk_fetch_records(srk_dev *d, int first, int count, int16_t *ab_p
   if (first < 0 || count < 0 || first + count > d->rec_cap) return -1;
   HIPCHK(hipSetDevice(d->device));
   HIPCHK(hipStreamSynchronize(d->stream));
+  if (count == 0) return 0;
   const size_t W = 2 * (size_t)d->M + d->N;
-  for (int c = 0; c < d->nchains; ++c) {
+  /* chain c's rows [first, first + count) of its rec_cap-row slab; one copy when they are the whole slab */
+  const bool whole = (first == 0 && count == d->rec_cap);
+  for (int c = 0; c < (whole ? 1 : d->nchains); ++c) {
+    const size_t rows = whole ? (size_t)d->nchains * count : (size_t)count;
     if (ab_pi)
       HIPCHK(hipMemcpy(ab_pi + (size_t)c * count * W, d->args.rec_abpi + ((size_t)c * d->rec_cap + first) * W,
-                       (size_t)count * W * sizeof(int16_t), hipMemcpyDeviceToHost));
+                       rows * W * sizeof(int16_t), hipMemcpyDeviceToHost));
     if (cdl)
       HIPCHK(hipMemcpy(cdl + (size_t)c * count * 3, d->args.rec_cdl + ((size_t)c * d->rec_cap + first) * 3,
-                       (size_t)count * 3 * sizeof(double), hipMemcpyDeviceToHost));
+                       rows * 3 * sizeof(double), hipMemcpyDeviceToHost));
   }
   return 0;
 }

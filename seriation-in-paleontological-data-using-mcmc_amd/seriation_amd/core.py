@@ -152,6 +152,15 @@ class Session:
                                                     cdl.ctypes.data_as(ctypes.POINTER(ctypes.c_double))), "fetch")
         return ab, cdl
 
+    def fetch_cdl(self):
+        """(c, d, loglik) float64 [n, k, 3] of the k buffered calls, without the a/b/pi rows."""
+        k = L.lib().sr_session_records(self.h)
+        cdl = np.zeros((self.n, k, 3), np.float64)
+        if k:
+            _check(L.lib().sr_session_fetch_records(self.h, 0, k, None,
+                                                    cdl.ctypes.data_as(ctypes.POINTER(ctypes.c_double))), "fetch")
+        return cdl
+
     def state(self, chain):
         N, M = self.ds.N, self.ds.M
         a = np.zeros(M, np.int32)

@@ -7,6 +7,8 @@ exp_data.csv payload, mcmc.c:53-67) to ONE all-gather (RCCL over xGMI with the "
 backend, gloo in the CPU tests), after which every rank can run the one-sigma chain
 selection of script.py:70-99 locally and identically.
 """
+import math
+
 import numpy as np
 
 from .launcher import choose_from_values
@@ -25,14 +27,14 @@ def summaries_from_records(chain_ids, cdl):
     """Per-chain summary rows from saved-sample records cdl[chain, sample, (c, d, loglik)]
     exactly as compute_exp_data / print_exp_data (mcmc.c:53-67): sums over the saved
     samples in order, divided by 1000 (the reference hard-codes the divisor)."""
-    cdl = np.asarray(cdl, np.float64)
+    rows = np.asarray(cdl, np.float64).tolist()
     out = np.zeros((len(chain_ids), 4))
     for k, cid in enumerate(chain_ids):
         ls = cs = ds = 0.0
-        for c, d, ll in cdl[k]:
+        for c, d, ll in rows[k]:   # math.exp is the C library's exp, as in mcmc.c
             ls += -ll
-            cs += float(np.exp(c))
-            ds += float(np.exp(d))
+            cs += math.exp(c)
+            ds += math.exp(d)
         out[k] = (cid, ls / 1000, cs / 1000, ds / 1000)
     return out
 

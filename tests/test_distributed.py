@@ -75,3 +75,17 @@ def test_gloo_world2_gather_and_select(n_total):
     np.testing.assert_array_equal(allrows[:, 1], expect)
     ref = sd.choose_from_values({"chain_%02d" % i: v for i, v in enumerate(expect)}, 8)
     assert s0 == ref
+
+
+def test_summaries_match_exp_data_bits():
+    """summaries_from_records (the all-gather payload) equals compute_exp_data / print_exp_data
+    (mcmc.c:53-67) bit for bit: the oracle's exp_data over the same saved samples."""
+    import oracle_ref
+    from seriation_amd import dist as sd
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "datasets", "g10s10.txt"), "rb") as fh:
+        text = fh.read()
+    for seed in (1, 2, 3):
+        o = oracle_ref.run_chain(text, seed, 5, 40)
+        row = sd.summaries_from_records([7], o["rec_dbl"][None])[0]
+        assert row[0] == 7
+        assert [float(v).hex() for v in row[1:]] == [float(v).hex() for v in o["exp"]], seed

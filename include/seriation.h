@@ -126,6 +126,11 @@ int32_t sr_session_block_threads(const sr_session *s);
 /* Kernel variant the session runs: 0 = occurrence columns in LDS, 1 = columns in HBM
  * (chosen when the LDS layout exceeds 160 KB, e.g. 1024 sites x 2048 taxa). */
 int32_t sr_session_variant(const sr_session *s);
+/* Checkpoint / resume (the reference has none): the full chain state (columns, pi,
+   limits, counts, c/d/loglik, MT19937 ring and cursor, acceptance counters) to a file; restoring
+   it over the same dataset continues every chain exactly where it stopped.  Records are not kept. */
+int sr_session_checkpoint(sr_session *s, const char *path);
+int sr_session_restore(const sr_dataset *ds, const char *path, const sr_run_opts *opts, sr_session **out);
 void sr_session_destroy(sr_session *s);
 
 /* ---- posterior summaries over saved samples, on the GPU ----

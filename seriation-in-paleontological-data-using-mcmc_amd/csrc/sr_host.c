@@ -403,8 +403,10 @@ static int auto_calls_per_launch(const sr_run_opts *o)
   return o->calls_per_launch > 0 ? o->calls_per_launch : 100;
 }
 
-SR_API int sr_session_create(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n_chains,
-                             const sr_run_opts *opts, sr_session **out)
+/* A session over `ds`: every chain initialised as main() does (restore == NULL), or its state
+   filled by restore(ctx, st) (a checkpoint). */
+static int session_new(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n_chains, const sr_run_opts *opts,
+                       int (*restore)(void *, sr_state_host *), void *restore_ctx, sr_session **out)
 {
   if (!ds || !specs || n_chains <= 0 || !out || ds->N < 2 || ds->M < 1) return SR_EINVAL;
   sr_run_opts o;
@@ -428,7 +430,9 @@ SR_API int sr_session_create(const sr_dataset *ds, const sr_chain_spec *specs, i
   sr_state_host st;
   int rc = state_alloc(&st, ds->N, ds->M, ds->nh, n_chains);
   if (rc) { sr_session_destroy(s); return rc; }
-  for (int c = 0; c < n_chains && rc == SR_OK; c++) rc = init_chain(ds, specs[c].seed, &st, c);
+  if (restore) rc = restore(restore_ctx, &st);
+  else
+    for (int c = 0; c < n_chains && rc == SR_OK; c++) rc = init_chain(ds, specs[c].seed, &st, c);
   if (rc) { state_free(&st); sr_session_destroy(s); return rc; }
   s->rec_cap = auto_calls_per_launch(&o);
   const int gm_force = (o.flags & SR_F_HBM_COLUMNS) ? 1 : ((o.flags & SR_F_LDS_COLUMNS) ? 0 : -1);
@@ -437,6 +441,12 @@ SR_API int sr_session_create(const sr_dataset *ds, const sr_chain_spec *specs, i
   if (rc) { sr_session_destroy(s); return rc == -6 ? SR_EUNSUPPORTED : SR_EDEVICE; }
   *out = s;
   return SR_OK;
+}
+
+SR_API int sr_session_create(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n_chains,
+                             const sr_run_opts *opts, sr_session **out)
+{
+  return session_new(ds, specs, n_chains, opts, NULL, NULL, out);
 }
 
 SR_API int sr_session_set_stream(sr_session *s, void *hip_stream)
@@ -481,6 +491,94 @@ static int download(sr_session *s, sr_state_host *st)
   if (rc) return rc;
   if (srk_download_state(s->dev, st)) { state_free(st); return SR_EDEVICE; }
   return SR_OK;
+}
+
+/* ---- checkpoint / resume (the reference restarts every run; optional here) ----
+ * File: "SRCK" | u32 version 1 | i32 N, M, nh, nchains | u64 FNV-1a of the dataset (X, hard) |
+ * sr_chain_spec[nchains] | the device state as sr_state_host arrays (P, rpi, hp, ab, cnt, cdl, mt,
+ * rng, acc), little-endian.  Restoring uploads the same words, so the continued chains are the
+ * ones an uninterrupted session produces (tests/test_gpu_edge.py). */
+static uint64_t dataset_hash(const sr_dataset *ds)
+{
+  uint64_t h = 1469598103934665603ULL;
+  for (size_t k = 0; k < (size_t)ds->N * ds->M; k++) { h ^= ds->X[k]; h *= 1099511628211ULL; }
+  for (int k = 0; k < ds->N; k++) { h ^= ds->hard[k]; h *= 1099511628211ULL; }
+  return h;
+}
+
+typedef struct { size_t bytes; void *p; } ck_part;
+
+static int ck_parts(sr_state_host *st, ck_part *pt)
+{
+  const size_t C = (size_t)st->nchains;
+  ck_part q[9] = {
+    {C * st->NW * st->M * 4, st->P}, {C * st->N * 4, st->rpi}, {C * SR_NHMAX * 4, st->hp},
+    {C * 2 * st->M * 4, st->ab}, {C * 4 * st->M * 4, st->cnt}, {C * 4 * 8, st->cdl},
+    {C * SR_RING * SR_MT_N * 4, st->mt}, {C * 2 * 8, st->rng}, {C * 8 * 8, st->acc}};
+  memcpy(pt, q, sizeof q);
+  return 9;
+}
+
+SR_API int sr_session_checkpoint(sr_session *s, const char *path)
+{
+  if (!s || !path) return SR_EINVAL;
+  sr_state_host st;
+  int rc = download(s, &st);
+  if (rc) return rc;
+  FILE *f = fopen(path, "wb");
+  if (!f) { state_free(&st); return SR_EIO; }
+  const uint32_t ver = 1;
+  const int32_t dims[4] = {s->ds.N, s->ds.M, s->ds.nh, s->nchains};
+  const uint64_t h = dataset_hash(&s->ds);
+  int ok = fwrite("SRCK", 1, 4, f) == 4 && fwrite(&ver, 4, 1, f) == 1 && fwrite(dims, 4, 4, f) == 4 &&
+           fwrite(&h, 8, 1, f) == 1 && fwrite(s->specs, sizeof(sr_chain_spec), s->nchains, f) == (size_t)s->nchains;
+  ck_part pt[9];
+  const int np = ck_parts(&st, pt);
+  for (int k = 0; k < np && ok; k++) ok = fwrite(pt[k].p, 1, pt[k].bytes, f) == pt[k].bytes;
+  if (fclose(f) != 0) ok = 0;
+  state_free(&st);
+  return ok ? SR_OK : SR_EIO;
+}
+
+typedef struct { FILE *f; } ck_reader;
+
+static int ck_restore(void *ctx, sr_state_host *st)
+{
+  ck_reader *r = (ck_reader *)ctx;
+  ck_part pt[9];
+  const int np = ck_parts(st, pt);
+  for (int k = 0; k < np; k++)
+    if (fread(pt[k].p, 1, pt[k].bytes, r->f) != pt[k].bytes) return SR_EPARSE;
+  return fgetc(r->f) == EOF ? SR_OK : SR_EPARSE;
+}
+
+SR_API int sr_session_restore(const sr_dataset *ds, const char *path, const sr_run_opts *opts, sr_session **out)
+{
+  if (!ds || !path || !out) return SR_EINVAL;
+  FILE *f = fopen(path, "rb");
+  if (!f) return SR_EIO;
+  char magic[4];
+  uint32_t ver = 0;
+  int32_t dims[4];
+  uint64_t h = 0;
+  int rc = SR_OK;
+  sr_chain_spec *specs = NULL;
+  if (fread(magic, 1, 4, f) != 4 || memcmp(magic, "SRCK", 4) != 0 || fread(&ver, 4, 1, f) != 1 || ver != 1 ||
+      fread(dims, 4, 4, f) != 4 || fread(&h, 8, 1, f) != 1 || dims[3] <= 0)
+    rc = SR_EPARSE;
+  else if (dims[0] != ds->N || dims[1] != ds->M || dims[2] != ds->nh || h != dataset_hash(ds))
+    rc = SR_EINVAL;   /* the checkpoint belongs to another dataset */
+  else if (!(specs = (sr_chain_spec *)malloc(sizeof(sr_chain_spec) * dims[3])))
+    rc = SR_ENOMEM;
+  else if (fread(specs, sizeof(sr_chain_spec), dims[3], f) != (size_t)dims[3])
+    rc = SR_EPARSE;
+  if (rc == SR_OK) {
+    ck_reader r = {f};
+    rc = session_new(ds, specs, dims[3], opts, ck_restore, &r, out);
+  }
+  free(specs);
+  fclose(f);
+  return rc;
 }
 
 SR_API int sr_session_state(sr_session *s, int32_t chain, int32_t *a, int32_t *b, int32_t *pi,

@@ -113,6 +113,27 @@ class Session:
                                          ctypes.byref(h)), "sr_session_create")
         self.h = h
 
+    def checkpoint(self, path):
+        """sr_session_checkpoint: the full chain state to `path` (records are not kept)."""
+        _check(L.lib().sr_session_checkpoint(self.h, os.fsencode(path)), "sr_session_checkpoint")
+
+    @classmethod
+    def restore(cls, dataset, path, device=0, sweeps_per_call=10, calls_per_launch=0, block_threads=0,
+                columns="auto"):
+        """sr_session_restore: a session continuing the chains of a checkpoint over `dataset`."""
+        self = cls.__new__(cls)
+        self.ds = dataset
+        self.opts = make_opts(sweeps_per_call=sweeps_per_call, device=device, block_threads=block_threads,
+                              calls_per_launch=calls_per_launch, columns=columns)
+        h = ctypes.c_void_p()
+        _check(L.lib().sr_session_restore(ctypes.byref(dataset.c), os.fsencode(path), ctypes.byref(self.opts),
+                                          ctypes.byref(h)), "sr_session_restore")
+        self.h = h
+        with open(path, "rb") as fh:   # header: magic, version, N, M, nh, nchains
+            self.n = int(np.frombuffer(fh.read(24)[20:24], "<i4")[0])
+        self.specs = None
+        return self
+
     @property
     def record_capacity(self):
         return L.lib().sr_session_record_capacity(self.h)

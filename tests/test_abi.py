@@ -81,3 +81,27 @@ def test_no_cpu_fallback_without_device():
     with pytest.raises(sa.SrError) as e:
         sa.Session(ds, [1])
     assert e.value.code == L.SR_EDEVICE
+
+
+def test_restore_rejects_bad_checkpoints(tmp_path):
+    """sr_session_restore validates the file before touching a device: missing file, bad magic,
+    another dataset's checkpoint."""
+    import struct
+    ds = sa.Dataset.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "datasets", "g10s10.txt"))
+    h = ctypes.c_void_p()
+    opts = L.sr_run_opts()
+    L.lib().sr_default_opts(ctypes.byref(opts))
+
+    def restore(p):
+        return L.lib().sr_session_restore(ctypes.byref(ds.c), os.fsencode(str(p)), ctypes.byref(opts), ctypes.byref(h))
+
+    assert restore(tmp_path / "missing.srck") == -7                       # SR_EIO
+    bad = tmp_path / "bad.srck"
+    bad.write_bytes(b"XXXX" + bytes(40))
+    assert restore(bad) == -2                                              # SR_EPARSE
+    other = tmp_path / "other.srck"
+    other.write_bytes(b"SRCK" + struct.pack("<I4iQ", 1, ds.N + 1, ds.M, 0, 2, 0))
+    assert restore(other) == -1                                            # SR_EINVAL: other dataset
+    samedims = tmp_path / "hash.srck"
+    samedims.write_bytes(b"SRCK" + struct.pack("<I4iQ", 1, ds.N, ds.M, ds.nh, 2, 12345))
+    assert restore(samedims) == -1                                         # SR_EINVAL: dataset hash differs

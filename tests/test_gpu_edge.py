@@ -84,3 +84,27 @@ def test_edge_parity_hbm_columns(name, N, M, nh, tb):
         np.testing.assert_array_equal(ri[k], o["rec_int"], err_msg="%s seed %d" % (name, s))
         assert np.array_equal(rd[k].view(np.uint64), o["rec_dbl"].view(np.uint64)), (name, s)
         assert summ[k]["consistent"] == 0
+
+
+def test_checkpoint_resume_continues_exactly(tmp_path):
+    """sr_session_checkpoint after 10 calls + sr_session_restore + 20 calls == 30 calls straight."""
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "datasets", "g5s5.txt")
+    ds = sa.Dataset.load(path)
+    seeds = [1, 2, 3, 4]
+    with sa.Session(ds, seeds, calls_per_launch=30) as s:
+        s.run(30, save=True)
+        ab_full, cdl_full = s.fetch_records()
+    ck = str(tmp_path / "chains.srck")
+    with sa.Session(ds, seeds, calls_per_launch=30) as s:
+        s.run(10, save=False)
+        s.checkpoint(ck)
+    r = sa.Session.restore(ds, ck, calls_per_launch=30)
+    try:
+        assert r.n == len(seeds)
+        r.run(20, save=True)
+        ab2, cdl2 = r.fetch_records()
+    finally:
+        r.close()
+    assert np.array_equal(ab_full[:, 10:], ab2)
+    assert np.array_equal(cdl_full[:, 10:].view(np.uint64), cdl2.view(np.uint64))

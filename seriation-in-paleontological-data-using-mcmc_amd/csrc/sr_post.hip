@@ -125,29 +125,34 @@ __global__ __launch_bounds__(256) void sr_post_kernel(PostArgs P)
       if (c + 1 < nchunk) load_chunk((c + 1) * CS);
       const unsigned g0 = c * CS;
       const int nu = (int)min((unsigned)CS, total - g0);
+      for (int u0 = 0; u0 < nu;) {   /* runs of samples up to the next chain boundary: no branch inside */
+        const int run = min(nu - u0, P.count - sm);
 #pragma unroll 16
-      for (int u = 0; u < nu; ++u) {   /* unrolled: the LDS reads run ahead of the add chain */
-        const int x = xsh[b][u][lane];
-        const int y = NEEDY ? ysh[NEEDY ? b : 0][NEEDY ? u : 0][lane] : 0;
+        for (int u = u0; u < u0 + run; ++u) {   /* unrolled: the LDS reads run ahead of the add chain */
+          const int x = xsh[b][u][lane];
+          const int y = NEEDY ? ysh[NEEDY ? b : 0][NEEDY ? u : 0][lane] : 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int r = r0 + k;   /* output row: PAIR_ORDER site i; ALIVE.. site index j; EXP_* 0 */
-          int v;
-          if (KIND == SRP_PAIR_ORDER) {
-            const int pr = psh[NEEDP ? b : 0][NEEDP ? u : 0][wave * 4 + k];
-            v = (r == col) ? -1 : (pr < x ? 1 : 0);                /* generate_po_matrix, script.py:183-188 */
-          } else if (KIND == SRP_ALIVE) {
-            v = (r >= x && r <= y) ? 1 : 0;                       /* script.py:326 */
-          } else if (KIND == SRP_FALSE_ALIVE) {
-            v = (r < x || r > y) ? 1 : 0;                         /* script.py:370 */
-          } else if (KIND == SRP_FALSE_ONES) {
-            v = (xo[k] == 1 && !(r >= x && r <= y)) ? 1 : 0;      /* script.py:408-413 */
-          } else {
-            v = x;                                                /* EXP_PI: pi[site]; EXP_A: a[taxon] */
+          for (int k = 0; k < 4; ++k) {
+            const int r = r0 + k;   /* output row: PAIR_ORDER site i; ALIVE.. site index j; EXP_* 0 */
+            int v;
+            if (KIND == SRP_PAIR_ORDER) {
+              const int pr = psh[NEEDP ? b : 0][NEEDP ? u : 0][wave * 4 + k];
+              v = (r == col) ? -1 : (pr < x ? 1 : 0);                /* generate_po_matrix, script.py:183-188 */
+            } else if (KIND == SRP_ALIVE) {
+              v = (r >= x && r <= y) ? 1 : 0;                       /* script.py:326 */
+            } else if (KIND == SRP_FALSE_ALIVE) {
+              v = (r < x || r > y) ? 1 : 0;                         /* script.py:370 */
+            } else if (KIND == SRP_FALSE_ONES) {
+              v = (xo[k] == 1 && !(r >= x && r <= y)) ? 1 : 0;      /* script.py:408-413 */
+            } else {
+              v = x;                                                /* EXP_PI: pi[site]; EXP_A: a[taxon] */
+            }
+            acc[k] = acc[k] + (double)v;
           }
-          acc[k] = acc[k] + (double)v;
         }
-        if (++sm == P.count) { sm = 0; chain_end(); }
+        u0 += run;
+        sm += run;
+        if (sm == P.count) { sm = 0; chain_end(); }
       }
       if (c + 1 < nchunk) store_chunk(b ^ 1);   /* buffer b^1 was last read before the previous barrier */
       __syncthreads();

@@ -79,7 +79,7 @@ __global__ __launch_bounds__(256) void sr_post_kernel(PostArgs P)
   constexpr bool NEEDP = (KIND == SRP_PAIR_ORDER);
   __shared__ int16_t xsh[2][CS][TCOL];
   __shared__ int16_t ysh[NEEDY ? 2 : 1][NEEDY ? CS : 1][TCOL];
-  __shared__ int16_t psh[NEEDP ? 2 : 1][NEEDP ? CS : 1][TR];
+  __shared__ __attribute__((aligned(8))) int16_t psh[NEEDP ? 2 : 1][NEEDP ? CS : 1][TR];
   const unsigned total = (unsigned)P.n_sel * (unsigned)P.count;
   const int t = threadIdx.x;
   const int prow = min((int)blockIdx.y * TR + (t & (TR - 1)), N - 1);   /* pair-order row operand */
@@ -131,12 +131,14 @@ __global__ __launch_bounds__(256) void sr_post_kernel(PostArgs P)
         for (int u = u0; u < u0 + run; ++u) {   /* unrolled: the LDS reads run ahead of the add chain */
           const int x = xsh[b][u][lane];
           const int y = NEEDY ? ysh[NEEDY ? b : 0][NEEDY ? u : 0][lane] : 0;
+          /* the wave's 4 row operands: one 8-byte LDS broadcast */
+          const uint64_t pr4 = NEEDP ? *(const uint64_t *)&psh[NEEDP ? b : 0][NEEDP ? u : 0][wave * 4] : 0;
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             const int r = r0 + k;   /* output row: PAIR_ORDER site i; ALIVE.. site index j; EXP_* 0 */
             int v;
             if (KIND == SRP_PAIR_ORDER) {
-              const int pr = psh[NEEDP ? b : 0][NEEDP ? u : 0][wave * 4 + k];
+              const int pr = (int16_t)(uint16_t)(pr4 >> (16 * k));
               v = (r == col) ? -1 : (pr < x ? 1 : 0);                /* generate_po_matrix, script.py:183-188 */
             } else if (KIND == SRP_ALIVE) {
               v = (r >= x && r <= y) ? 1 : 0;                       /* script.py:326 */

@@ -29,6 +29,7 @@
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 #include <stdio.h>
 #include "sr_internal.h"
 
@@ -77,8 +78,8 @@ __global__ __launch_bounds__(256) void sr_post_kernel(PostArgs P)
      sample.  The accumulation order per element is still the script's sample order. */
   constexpr bool NEEDY = (KIND == SRP_ALIVE || KIND == SRP_FALSE_ALIVE || KIND == SRP_FALSE_ONES);
   constexpr bool NEEDP = (KIND == SRP_PAIR_ORDER);
-  __shared__ int16_t xsh[2][CS][TCOL];
-  __shared__ int16_t ysh[NEEDY ? 2 : 1][NEEDY ? CS : 1][TCOL];
+  typedef typename std::conditional<NEEDY, uint32_t, uint16_t>::type xy_t;
+  __shared__ xy_t xsh[2][CS][TCOL];   /* x (low half), y in the high half for NEEDY kinds */
   __shared__ __attribute__((aligned(8))) int16_t psh[NEEDP ? 2 : 1][NEEDP ? CS : 1][TR];
   const unsigned total = (unsigned)P.n_sel * (unsigned)P.count;
   const int t = threadIdx.x;
@@ -104,8 +105,7 @@ __global__ __launch_bounds__(256) void sr_post_kernel(PostArgs P)
   auto store_chunk = [&](int b) {
 #pragma unroll
     for (int k = 0; k < CS / 4; ++k) {
-      xsh[b][wave + 4 * k][lane] = lx[k];
-      if (NEEDY) ysh[b][wave + 4 * k][lane] = ly[k];
+      xsh[b][wave + 4 * k][lane] = (xy_t)((uint32_t)(uint16_t)lx[k] | (NEEDY ? (uint32_t)(uint16_t)ly[k] << 16 : 0u));
     }
     if (NEEDP) {
 #pragma unroll
@@ -129,8 +129,9 @@ __global__ __launch_bounds__(256) void sr_post_kernel(PostArgs P)
         const int run = min(nu - u0, P.count - sm);
 #pragma unroll 16
         for (int u = u0; u < u0 + run; ++u) {   /* unrolled: the LDS reads run ahead of the add chain */
-          const int x = xsh[b][u][lane];
-          const int y = NEEDY ? ysh[NEEDY ? b : 0][NEEDY ? u : 0][lane] : 0;
+          const uint32_t xy = (uint32_t)xsh[b][u][lane];
+          const int x = (int16_t)(uint16_t)(xy & 0xffffu);
+          const int y = NEEDY ? (int16_t)(uint16_t)(xy >> 16) : 0;
           /* the wave's 4 row operands: one 8-byte LDS broadcast */
           const uint64_t pr4 = NEEDP ? *(const uint64_t *)&psh[NEEDP ? b : 0][NEEDP ? u : 0][wave * 4] : 0;
 #pragma unroll

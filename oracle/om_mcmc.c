@@ -9,7 +9,8 @@
  * expression order line by line (each function cites the lines it restates), with
  * these documented differences:
  *   - GSL 2.6 is restated in om_gsl.h (GSL is absent here); glibc exp/log are
- *     replaced by the deterministic om_exp/om_log (om_libm.h);
+ *     restated in om_libm.h (om_exp/om_log: bit-identical to libm.so.6, pinned by
+ *     oracle_libm_mismatch in tests/test_host.py);
  *   - plain int arrays instead of gsl_vector/gsl_permutation (same values);
  *   - mcmc_randomize's read of q[nh] past the end (mcmc.c:530, UB) is guarded;
  *   - the library entry points return error codes instead of exit(1).
@@ -789,6 +790,22 @@ OM_API void oracle_exp_log(const double *in, long n, double *out_exp, double *ou
     if (out_exp) out_exp[k] = om_exp(in[k]);
     if (out_log) out_log[k] = om_log(in[k]);
   }
+}
+
+/* The pin of om_libm.h: count inputs where om_exp / om_log differ (bitwise, NaN == NaN) from
+ * this machine's glibc exp() / log(), the functions the reference calls.  Called through a
+ * volatile pointer so the compiler neither folds nor inlines them. */
+static int om_same(double a, double b) { return om_bits(a) == om_bits(b) || (a != a && b != b); }
+OM_API void oracle_libm_mismatch(const double *in, long n, long *bad_exp, long *bad_log)
+{
+  double (*volatile gexp)(double) = exp, (*volatile glog)(double) = log;
+  long be = 0, bl = 0;
+  for (long k = 0; k < n; k++) {
+    be += !om_same(om_exp(in[k]), gexp(in[k]));
+    bl += !om_same(om_log(in[k]), glog(in[k]));
+  }
+  *bad_exp = be;
+  *bad_log = bl;
 }
 
 /* ---------------------------------------------------------------- CLI */

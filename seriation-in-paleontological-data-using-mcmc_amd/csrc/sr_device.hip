@@ -36,11 +36,8 @@
 __constant__ double c_zig_y[128] = SR_ZIG_YTAB_INIT;
 __constant__ unsigned int c_zig_k[128] = SR_ZIG_KTAB_INIT;
 __constant__ double c_zig_w[128] = SR_ZIG_WTAB_INIT;
-__constant__ double c_exp_thi[128] = SR_EXP_THI_INIT;
-__constant__ double c_exp_tlo[128] = SR_EXP_TLO_INIT;
-__constant__ double c_log_invc[128] = SR_LOG_INVC_INIT;
-__constant__ double c_log_lhi[128] = SR_LOG_LHI_INIT;
-__constant__ double c_log_llo[128] = SR_LOG_LLO_INIT;
+__constant__ uint64_t c_exp_tab[256] = SR_EXP_TAB_INIT;
+__constant__ double c_log_tab[256] = SR_LOG_TAB_INIT;
 
 #ifndef SR_EXP
 #define SR_EXP 0   /* timing experiments only (break the sampler): 1 skip proposals, 2 skip Gibbs, 4/8/16 skip pi3/pi2/pi1 terms */
@@ -99,7 +96,7 @@ __host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB, bo
   size_t o = 0;
   const int KT = (M + 63) / 64, NWV = TB / 64;
   const size_t g = gm ? 0 : 1;
-  L.tab = o;   o = sr_al16(o + 640 * sizeof(double));
+  L.tab = o;   o = sr_al16(o + 512 * sizeof(double));   /* glibc exp/log tables */
   L.cbuf = o;  o = sr_al16(o + g * 2 * KT * 64 * sizeof(double));       /* [2][KT*64] by proposal parity */
   L.lbuf = o;  o = sr_al16(o + g * M * sizeof(double));
   L.mt = o;    o = sr_al16(o + (size_t)SR_RING * SR_MT_N * 4);
@@ -1345,15 +1342,12 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   uint64_t *misc = (uint64_t *)(smem + L.misc);
 
   /* ---- load tables and state */
-  for (int i = tid; i < 128; i += TB) {
-    tabs[i] = c_exp_thi[i];
-    tabs[128 + i] = c_exp_tlo[i];
-    tabs[256 + i] = c_log_invc[i];
-    tabs[384 + i] = c_log_lhi[i];
-    tabs[512 + i] = c_log_llo[i];
+  for (int i = tid; i < 256; i += TB) {
+    ((uint64_t *)tabs)[i] = c_exp_tab[i];
+    tabs[256 + i] = c_log_tab[i];
   }
   sr_mtab tb;
-  tb.exp_thi = tabs; tb.exp_tlo = tabs + 128; tb.log_invc = tabs + 256; tb.log_lhi = tabs + 384; tb.log_llo = tabs + 512;
+  tb.exp_tab = (const uint64_t *)tabs; tb.log_tab = tabs + 256;
   {
     const uint32_t *gP = A.P + (size_t)chain * NW * M;
     if (!GM) for (int i = tid; i < NW * M; i += TB) P[i] = gP[i];
@@ -2461,17 +2455,14 @@ extern "C" void srk_destroy(srk_dev *d)
 /* Device copies of the deterministic exp/log, for the host<->device bit-parity test. */
 __global__ void sr_math_selftest_kernel(const double *in, long n, double *oe, double *ol)
 {
-  __shared__ double tabs[640];
-  for (int i = threadIdx.x; i < 128; i += blockDim.x) {
-    tabs[i] = c_exp_thi[i];
-    tabs[128 + i] = c_exp_tlo[i];
-    tabs[256 + i] = c_log_invc[i];
-    tabs[384 + i] = c_log_lhi[i];
-    tabs[512 + i] = c_log_llo[i];
+  __shared__ double tabs[512];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    ((uint64_t *)tabs)[i] = c_exp_tab[i];
+    tabs[256 + i] = c_log_tab[i];
   }
   __syncthreads();
   sr_mtab tb;
-  tb.exp_thi = tabs; tb.exp_tlo = tabs + 128; tb.log_invc = tabs + 256; tb.log_lhi = tabs + 384; tb.log_llo = tabs + 512;
+  tb.exp_tab = (const uint64_t *)tabs; tb.log_tab = tabs + 256;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     oe[i] = sr_exp_m(in[i], &tb);
     ol[i] = sr_log_m(in[i], &tb);

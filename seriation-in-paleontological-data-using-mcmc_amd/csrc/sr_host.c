@@ -31,7 +31,7 @@
 #define SR_API __attribute__((visibility("default")))
 #define SR_MAX_WRITERS 64   /* chain_data.csv formatting threads (SR_WRITER_THREADS, default = online CPUs) */
 
-static const sr_mtab SR_HOST_TAB = {sr_exp_thi, sr_exp_tlo, sr_log_invc, sr_log_lhi, sr_log_llo};
+static const sr_mtab SR_HOST_TAB = {(const uint64_t *)sr_exp_tab, sr_log_tab};
 static double h_exp(double x) { return sr_exp_m(x, &SR_HOST_TAB); }
 static double h_log(double x) { return sr_log_m(x, &SR_HOST_TAB); }
 

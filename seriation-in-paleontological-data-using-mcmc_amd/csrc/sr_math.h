@@ -6,9 +6,10 @@
  * draw (mcmc.c:644, 734, 757-760, 847-848, 1214, 1261, 1441, 1636).  A GPU cannot call
  * glibc, and OCML's exp/log differ from it in the last bit, which would flip
  * data-dependent RNG consumption (mcmc.c:1261 draws uniform_pos only when delta < 0).
- * So the sampler uses one table-driven algorithm (~0.51 ulp; agrees with glibc on
- * >99.8% of inputs) built only from correctly rounded IEEE operations; host and
- * device produce bitwise-identical results (tests/test_math.py, tests/test_gpu_parity.py).
+ * So the sampler restates glibc's own algorithm (the x86-64 FMA build of e_exp.c / e_log.c,
+ * built only from correctly rounded IEEE operations and explicit fma); host, device and
+ * this machine's libm.so.6 produce bitwise-identical results (tests/test_host.py,
+ * tests/test_gpu_parity.py).
  *
  * sr_run_add / sr_run_sub reproduce L sequential roundings x = fl(x + e) / r = fl(r - p)
  * in O(binades) instead of O(L) steps: inside one binade every step moves x by the same
@@ -43,93 +44,108 @@ SR_HD double sr_from_bits(uint64_t u) { union { double d; uint64_t u; } v; v.u =
 
 /* Table pointers: the device passes LDS copies, the host the static tables. */
 typedef struct {
-  const double *exp_thi, *exp_tlo, *log_invc, *log_lhi, *log_llo;
+  const uint64_t *exp_tab;   /* glibc __exp_data.tab[256] */
+  const double *log_tab;     /* glibc __log_data.tab[128] {invc, logc} */
 } sr_mtab;
 
-SR_HD double sr_exp_t(double x, const double *thi_t, const double *tlo_t)
+/* glibc exp (sysdeps/ieee754/dbl-64/e_exp.c), x86-64 FMA ifunc build: the fma() calls are that
+ * build's contractions; bit-identical to libm.so.6 (tests/test_host.py, tests/test_gpu_parity.py) */
+SR_HD double sr_exp_m(double x, const sr_mtab *t)
 {
-  if (x != x) return x;
-  if (x > 709.782712893384) return __builtin_inf();
-  if (x < -745.1332191019412) return 0.0;
-  double kd = __builtin_rint(x * SR_EXP_INVL);
-  int k = (int)kd;
-  double r = __builtin_fma(-kd, SR_EXP_L1, x);
-  r = __builtin_fma(-kd, SR_EXP_L2, r);
-  int idx = k & 127;
-  int e = (k - idx) / 128;
-  double r2 = r * r;
-  double h = __builtin_fma(r, 1.0 / 720.0, 1.0 / 120.0);
-  h = __builtin_fma(r, h, 1.0 / 24.0);
-  h = __builtin_fma(r, h, 1.0 / 6.0);
-  h = __builtin_fma(r, h, 0.5);
-  double p = __builtin_fma(r2, h, r);
-  double thi = thi_t[idx];
-  double tmp = __builtin_fma(thi, p, tlo_t[idx]);
-  double res = thi + tmp;
-  if (e > 1000) return (res * sr_from_bits((uint64_t)(e - 1 + 1023) << 52)) * 2.0;
-  if (e >= -1022) return res * sr_from_bits((uint64_t)(e + 1023) << 52);
-  return (res * sr_from_bits((uint64_t)(e + 600 + 1023) << 52)) * 0x1p-600;
+  uint32_t abstop = (uint32_t)(sr_bits(x) >> 52) & 0x7ff;
+  if (abstop - 0x3c9u >= 0x408u - 0x3c9u) {          /* |x| < 2^-54 or |x| >= 512 */
+    if ((int32_t)(abstop - 0x3c9u) < 0) return 1.0 + x;
+    if (abstop >= 0x409u) {
+      if (sr_bits(x) == 0xFFF0000000000000ULL) return 0.0;
+      if (abstop >= 0x7ffu) return 1.0 + x;
+      return (sr_bits(x) >> 63) ? 0.0 : __builtin_inf();
+    }
+    abstop = 0;
+  }
+  double kd = __builtin_fma(x, SR_GEXP_INVLN2N, SR_GEXP_SHIFT);
+  const uint64_t ki = sr_bits(kd);
+  kd -= SR_GEXP_SHIFT;
+  double r = __builtin_fma(kd, SR_GEXP_NEGLN2HIN, x);
+  r = __builtin_fma(kd, SR_GEXP_NEGLN2LON, r);
+  const uint64_t idx = 2 * (ki % 128), top = ki << 45;
+  const double tail = sr_from_bits(t->exp_tab[idx]);
+  uint64_t sbits = t->exp_tab[idx + 1] + top;
+  const double r2 = r * r;
+  const double p1 = __builtin_fma(r, SR_GEXP_C3, SR_GEXP_C2);
+  const double p2 = __builtin_fma(r, SR_GEXP_C5, SR_GEXP_C4);
+  double tmp = __builtin_fma(r2, p1, tail + r);
+  tmp = __builtin_fma(r2 * r2, p2, tmp);
+  if (abstop == 0) {                                  /* specialcase(): |x| >= 512 */
+    if ((ki & 0x80000000u) == 0) {
+      sbits -= 1009ull << 52;
+      const double scale = sr_from_bits(sbits);
+      return 0x1p1009 * __builtin_fma(scale, tmp, scale);
+    }
+    sbits += 1022ull << 52;                           /* k < 0: not contracted in glibc's build */
+    const double scale = sr_from_bits(sbits);
+    const double st = scale * tmp;
+    double y = scale + st;
+    if (y < 1.0) {
+      double lo = scale - y + st;
+      const double hi = 1.0 + y;
+      lo = 1.0 - hi + y + lo;
+      y = (hi + lo) - 1.0;
+      if (y == 0.0) y = 0.0;
+    }
+    return 0x1p-1022 * y;
+  }
+  const double scale = sr_from_bits(sbits);
+  return __builtin_fma(scale, tmp, scale);
 }
 
-SR_HD double sr_log_t(double x, const double *invc_t, const double *lhi_t, const double *llo_t)
+/* glibc log (sysdeps/ieee754/dbl-64/e_log.c), x86-64 FMA ifunc build */
+SR_HD double sr_log_m(double x, const sr_mtab *t)
 {
-  if (x != x) return x;
-  if (x <= 0.0) return x == 0.0 ? -__builtin_inf() : (x - x) / (x - x);
-  if (x == __builtin_inf()) return x;
-  if (x > 0.96875 && x < 1.03125) {
-    double r = x - 1.0;
-    double P = __builtin_fma(r, -1.0 / 14.0, 1.0 / 13.0);
-    P = __builtin_fma(r, P, -1.0 / 12.0);
-    P = __builtin_fma(r, P, 1.0 / 11.0);
-    P = __builtin_fma(r, P, -1.0 / 10.0);
-    P = __builtin_fma(r, P, 1.0 / 9.0);
-    P = __builtin_fma(r, P, -1.0 / 8.0);
-    P = __builtin_fma(r, P, 1.0 / 7.0);
-    P = __builtin_fma(r, P, -1.0 / 6.0);
-    P = __builtin_fma(r, P, 1.0 / 5.0);
-    P = __builtin_fma(r, P, -1.0 / 4.0);
-    P = __builtin_fma(r, P, 1.0 / 3.0);
-    P = __builtin_fma(r, P, -0.5);
-    double r2 = r * r;
-    return __builtin_fma(r2, P, r);
-  }
   uint64_t ix = sr_bits(x);
-  int64_t kadj = 0;
-  if (ix < 0x0010000000000000ULL) {
-    ix = sr_bits(x * 0x1p52);
-    kadj = -52;
+  const uint32_t top = (uint32_t)(ix >> 48);
+  if (ix - 0x3FEE000000000000ULL < 0x3FF1090000000000ULL - 0x3FEE000000000000ULL) {   /* near 1 */
+    if (ix == 0x3FF0000000000000ULL) return 0.0;
+    const double r = x - 1.0, r2 = r * r, r3 = r * r2;
+    double p = __builtin_fma(r, SR_GLOG_B8, SR_GLOG_B7);
+    p = __builtin_fma(r2, SR_GLOG_B9, p);
+    p = __builtin_fma(r3, SR_GLOG_B10, p);
+    double q = __builtin_fma(r, SR_GLOG_B5, SR_GLOG_B4);
+    q = __builtin_fma(r2, SR_GLOG_B6, q);
+    q = __builtin_fma(p, r3, q);
+    double s = __builtin_fma(r, SR_GLOG_B2, SR_GLOG_B1);
+    s = __builtin_fma(r2, SR_GLOG_B3, s);
+    const double P = __builtin_fma(q, r3, s);
+    const double rhi = __builtin_fma(-0x1p27, r, __builtin_fma(r, 0x1p27, r));
+    const double rlo = r - rhi;
+    const double rr = rhi * rhi;
+    const double hi = __builtin_fma(rr, SR_GLOG_B0, r);
+    double lo = __builtin_fma(rr, SR_GLOG_B0, r - hi);
+    lo = __builtin_fma(SR_GLOG_B0 * rlo, rhi + r, lo);
+    const double y = __builtin_fma(P, r3, lo);
+    return y + hi;
   }
-  uint64_t tmp = ix - SR_LOG_OFF;
-  int i = (int)((tmp >> 45) & 127);
-  int64_t k = ((int64_t)tmp >> 52) + kadj;
-  uint64_t iz = ix - (tmp & (0xFFFULL << 52));
-  double z = sr_from_bits(iz);
-  double r = __builtin_fma(z, invc_t[i], -1.0);
-  double kd = (double)k;
-  double w1 = kd * SR_LOG_LN2HI;
-  double lhi = lhi_t[i];
-  double w = w1 + lhi;
-  double bb = w - w1;
-  double werr = (w1 - (w - bb)) + (lhi - bb);
-  double hi = w + r;
-  double b2 = hi - w;
-  double e2 = (w - (hi - b2)) + (r - b2);
-  double P = __builtin_fma(r, -1.0 / 8.0, 1.0 / 7.0);
-  P = __builtin_fma(r, P, -1.0 / 6.0);
-  P = __builtin_fma(r, P, 1.0 / 5.0);
-  P = __builtin_fma(r, P, -1.0 / 4.0);
-  P = __builtin_fma(r, P, 1.0 / 3.0);
-  P = __builtin_fma(r, P, -0.5);
-  double r2 = r * r;
-  double lo = werr + e2;
-  lo = __builtin_fma(kd, SR_LOG_LN2LO, lo);
-  lo = lo + llo_t[i];
-  lo = __builtin_fma(r2, P, lo);
-  return hi + lo;
+  if (top - 0x0010u >= 0x7ff0u - 0x0010u) {
+    if (ix * 2 == 0) return -__builtin_inf();
+    if (ix == 0x7FF0000000000000ULL) return x;
+    if ((top & 0x8000u) || (top & 0x7ff0u) == 0x7ff0u) return (x - x) / (x - x);
+    ix = sr_bits(x * 0x1p52);
+    ix -= 52ULL << 52;
+  }
+  const uint64_t tmp = ix - 0x3FE6000000000000ULL;
+  const int i = (int)((tmp >> 45) % 128);
+  const int64_t k = (int64_t)tmp >> 52;
+  const uint64_t iz = ix - (tmp & (0xFFFULL << 52));
+  const double invc = t->log_tab[2 * i], logc = t->log_tab[2 * i + 1];
+  const double z = sr_from_bits(iz);
+  const double r = __builtin_fma(z, invc, -1.0);
+  const double kd = (double)k;
+  const double w = __builtin_fma(kd, SR_GLOG_LN2HI, logc);
+  const double hi = w + r;
+  const double lo = __builtin_fma(kd, SR_GLOG_LN2LO, w - hi + r);
+  const double r2 = r * r;
+  const double q = __builtin_fma(r2, __builtin_fma(r, SR_GLOG_A4, SR_GLOG_A3), __builtin_fma(r, SR_GLOG_A2, SR_GLOG_A1));
+  return __builtin_fma(r * r2, q, __builtin_fma(r2, SR_GLOG_A0, lo)) + hi;
 }
-
-SR_HD double sr_exp_m(double x, const sr_mtab *t) { return sr_exp_t(x, t->exp_thi, t->exp_tlo); }
-SR_HD double sr_log_m(double x, const sr_mtab *t) { return sr_log_t(x, t->log_invc, t->log_lhi, t->log_llo); }
 
 /* ulp of a positive normal double */
 SR_HD double sr_ulp(double x) { return sr_from_bits((sr_bits(x) & 0x7FF0000000000000ULL) - (52ULL << 52)); }

@@ -35,6 +35,8 @@ def lib():
         L.oracle_shuffle.argtypes = [ctypes.c_ulong, P(ctypes.c_int32), ctypes.c_long]
         L.oracle_choose.argtypes = [ctypes.c_ulong, P(ctypes.c_int32), ctypes.c_long, P(ctypes.c_int32), ctypes.c_long]
         L.oracle_exp_log.argtypes = [P(ctypes.c_double), ctypes.c_long, P(ctypes.c_double), P(ctypes.c_double)]
+        L.oracle_libm_mismatch.restype = None
+        L.oracle_libm_mismatch.argtypes = [P(ctypes.c_double), ctypes.c_long, P(ctypes.c_long), P(ctypes.c_long)]
         _L = L
     return _L
 

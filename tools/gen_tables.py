@@ -20,10 +20,13 @@ Contents
    reproduces the published GSL values ytab[0..15], ktab[0..15], wtab[0..7]
    (asserted below); the remaining entries follow from the same construction.
 
-2. Tables for the deterministic exp/log used by BOTH the oracle and the device
-   (2^(i/128) in double-double; 1/c_i and -log(1/c_i) in double-double for a
-   128-interval log).  Both sides execute the identical IEEE operation sequence,
-   so their results are bitwise identical (see DESIGN.md "deterministic libm").
+2. glibc's exp/log tables (the reference calls glibc exp()/log(); its binary imports
+   exp@GLIBC_2.29): __exp_data.tab is computed from its definition and cross-checked
+   against this machine's libm.so.6; __log_data.tab {invc, logc} comes out of a search
+   procedure with no closed form, so it is read from libm.so.6 (Ubuntu glibc 2.35), located
+   by the struct's leading constants.  oracle/om_libm.h and csrc/sr_math.h restate the
+   x86-64 FMA ifunc variant of glibc's exp/log on these tables; tests/test_host.py checks
+   both equal glibc bit for bit.
 """
 import os
 import sys
@@ -88,42 +91,84 @@ def dd(v):
     return hi, lo
 
 
+GLIBC_LIBM = "/lib/x86_64-linux-gnu/libm.so.6"
+
+# glibc >= 2.28 exp/log (the ARM optimized-routines code; the reference binary imports
+# exp@GLIBC_2.29 / log@GLIBC_2.29): sysdeps/ieee754/dbl-64/e_exp.c, e_log.c with
+# EXP_TABLE_BITS = LOG_TABLE_BITS = 7, EXP_POLY_ORDER = 5, LOG_POLY_ORDER = 6,
+# LOG_POLY1_ORDER = 12.  Scalar constants (published in e_exp_data.c / e_log_data.c):
+EXP_CONST = dict(invln2N="0x1.71547652b82fep7", shift="0x1.8p52", negln2hiN="-0x1.62e42fefa0000p-8",
+                 negln2loN="-0x1.cf79abc9e3b3ap-47", C2="0x1.ffffffffffdbdp-2", C3="0x1.555555555543cp-3",
+                 C4="0x1.55555cf172b91p-5", C5="0x1.1111167a4d017p-7")
+LOG_CONST = dict(ln2hi="0x1.62e42fefa3800p-1", ln2lo="0x1.ef35793c76730p-45")
+LOG_A = ["-0x1.0000000000001p-1", "0x1.555555551305bp-2", "-0x1.fffffffeb459p-3", "0x1.999b324f10111p-3",
+         "-0x1.55575e506c89fp-3"]
+LOG_B = ["-0x1p-1", "0x1.5555555555577p-2", "-0x1.ffffffffffdcbp-3", "0x1.999999995dd0cp-3",
+         "-0x1.55555556745a7p-3", "0x1.24924a344de3p-3", "-0x1.fffffa4423d65p-4", "0x1.c7184282ad6cap-4",
+         "-0x1.999eb43b068ffp-4", "0x1.78182f7afd085p-4", "-0x1.5521375d145cdp-4"]
+
+
+def _u64(x):
+    import struct
+    return struct.unpack("<Q", struct.pack("<d", x))[0]
+
+
+def _libm_bytes():
+    with open(GLIBC_LIBM, "rb") as fh:
+        return fh.read()
+
+
+def _find_block(data, head):
+    """offset of the data block whose leading doubles are `head` (hex strings); unique or error"""
+    import struct
+    pat = b"".join(struct.pack("<d", float.fromhex(h)) for h in head)
+    i = data.find(pat)
+    if i < 0 or data.find(pat, i + 1) >= 0:
+        raise SystemExit("gen_tables: cannot locate a unique %s... block in %s" % (head[0], GLIBC_LIBM))
+    return i
+
+
 def exp_tables():
-    thi, tlo = [], []
-    for i in range(128):
-        v = mpf(2) ** (mpf(i) / 128)
-        hi, lo = dd(v)
-        thi.append(hi)
-        tlo.append(lo)
-    ln2_128 = log(2) / 128
-    L1, L2 = dd(ln2_128)
-    inv = float(128 / log(2))
-    return thi, tlo, L1, L2, inv
-
-
-LOG_OFF = 0x3FE6A00000000000  # bits of 0.70703125
+    """__exp_data.tab: for k < 128, tab[2k] = bits of the tail (2^(k/128) - H_k) / H_k and
+    tab[2k+1] = bits of H_k - (k << 45), H_k = 2^(k/128) rounded to nearest.  Computed here
+    from the definition and checked against the table inside this machine's libm.so.6."""
+    import struct
+    mp.dps = 80
+    tab = []
+    for k in range(128):
+        v = mpf(2) ** (mpf(k) / 128)
+        H = float(v)
+        tail = float((v - mpf(H)) / mpf(H))
+        tab.append(_u64(tail))
+        tab.append((_u64(H) - (k << 45)) & 0xFFFFFFFFFFFFFFFF)
+    mp.dps = 60
+    if os.path.exists(GLIBC_LIBM):
+        data = _libm_bytes()
+        e = _find_block(data, [EXP_CONST["invln2N"], EXP_CONST["shift"], EXP_CONST["negln2hiN"]])
+        # struct exp_data: invln2N, shift, negln2hiN, negln2loN, poly[4], exp2_shift, exp2_poly[5], tab[256]
+        head = struct.unpack("<8d", data[e:e + 64])
+        want = [float.fromhex(EXP_CONST[k]) for k in ("invln2N", "shift", "negln2hiN", "negln2loN", "C2", "C3", "C4",
+                                                       "C5")]
+        assert list(head) == want, "exp constants differ from " + GLIBC_LIBM
+        got = list(struct.unpack("<256Q", data[e + 14 * 8:e + 14 * 8 + 256 * 8]))
+        assert got == tab, "computed exp table differs from " + GLIBC_LIBM
+    return tab
 
 
 def log_tables():
+    """__log_data.tab[128] = {invc, logc}: chosen by glibc's search procedure (not a closed
+    form), so they are read from this machine's libm.so.6 (located by the leading constants
+    ln2hi, ln2lo, A[0..4], B[0..10] of struct log_data, which are checked)."""
     import struct
-    invc, lhi, llo = [], [], []
-    for i in range(128):
-        lo_bits = LOG_OFF + (i << 45)
-        hi_bits = LOG_OFF + ((i + 1) << 45)
-        zlo = struct.unpack("<d", struct.pack("<Q", lo_bits))[0]
-        zhi = struct.unpack("<d", struct.pack("<Q", hi_bits))[0]
-        c = (mpf(zlo) + mpf(zhi)) / 2
-        ic = float(1 / c)
-        v = -log(mpf(ic))
-        h, l = dd(v)
-        invc.append(ic)
-        lhi.append(h)
-        llo.append(l)
-    ln2 = log(2)
-    # Ln2hi with 42 significant bits so k*Ln2hi is exact for |k| < 2^11
-    ln2hi = float(mpf(int(ln2 * 2 ** 42)) / 2 ** 42)
-    ln2lo = float(ln2 - mpf(ln2hi))
-    return invc, lhi, llo, ln2hi, ln2lo
+    data = _libm_bytes()
+    head = [LOG_CONST["ln2hi"], LOG_CONST["ln2lo"]] + LOG_A + LOG_B
+    L = _find_block(data, head)
+    t = list(struct.unpack("<256d", data[L + 18 * 8:L + 18 * 8 + 256 * 8]))
+    for i in range(128):   # invc ~ 1/c with c inside interval i of [0x1.6p-1, 0x1.6p0)
+        z0 = struct.unpack("<d", struct.pack("<Q", 0x3FE6000000000000 + (i << 45)))[0]
+        assert 1 / t[2 * i] >= z0 * (1 - 2 ** -7) and 1 / t[2 * i] <= z0 * 2 ** (1 / 64) * (1 + 2 ** -7), i
+        assert abs(float(log(1 / mpf(t[2 * i]))) - t[2 * i + 1]) < 2 ** -40, i
+    return t
 
 
 def emit(prefix, guard, path):
@@ -137,8 +182,8 @@ def emit(prefix, guard, path):
         assert k[i] == p, (i, k[i], p)
     for i, p in enumerate(PIN_W):
         assert float(ws[i]) == float(p), (i, ws[i], p)
-    thi, tlo, L1, L2, inv = exp_tables()
-    invc, lhi, llo, ln2hi, ln2lo = log_tables()
+    etab = exp_tables()
+    ltab = log_tables()
     P = prefix
     U = P.upper()
     out = []
@@ -159,20 +204,19 @@ def emit(prefix, guard, path):
     arr("double", "zig_ytab", ys)
     arr("unsigned int", "zig_ktab", k, lambda v: "%du" % v)
     arr("double", "zig_wtab", ws)
-    out.append("/* exp: 2^(i/128) = thi[i] + tlo[i] (double-double). */")
-    out.append("#define %sEXP_INVL %s" % (U, hexd(inv)))
-    out.append("#define %sEXP_L1 %s" % (U, hexd(L1)))
-    out.append("#define %sEXP_L2 %s" % (U, hexd(L2)))
-    arr("double", "exp_thi", thi, hexd)
-    arr("double", "exp_tlo", tlo, hexd)
-    out.append("/* log: interval i of z in [0.70703125,1.4140625) (bit-uniform), invc ~ 1/center,")
-    out.append("   -log(invc) = lhi + llo. */")
-    out.append("#define %sLOG_OFF 0x%016XULL" % (U, LOG_OFF))
-    out.append("#define %sLOG_LN2HI %s" % (U, hexd(ln2hi)))
-    out.append("#define %sLOG_LN2LO %s" % (U, hexd(ln2lo)))
-    arr("double", "log_invc", invc, hexd)
-    arr("double", "log_lhi", lhi, hexd)
-    arr("double", "log_llo", llo, hexd)
+    out.append("/* glibc exp (e_exp.c, N = 128): scalar constants and __exp_data.tab[2N] (tail, scale bits). */")
+    for name, h in EXP_CONST.items():
+        out.append("#define %sGEXP_%s %s" % (U, name.upper(), float.fromhex(h).hex()))
+    arr("unsigned long long", "exp_tab", etab, lambda v: "0x%016xULL" % v)
+    out.append("/* glibc log (e_log.c, N = 128): ln2 split, poly A[5] (|x-1| >= 0x1p-4 path), poly1 B[11]")
+    out.append("   (near 1), __log_data.tab[N] = {invc, logc} interleaved. */")
+    for name, h in LOG_CONST.items():
+        out.append("#define %sGLOG_%s %s" % (U, name.upper(), float.fromhex(h).hex()))
+    for i, h in enumerate(LOG_A):
+        out.append("#define %sGLOG_A%d %s" % (U, i, float.fromhex(h).hex()))
+    for i, h in enumerate(LOG_B):
+        out.append("#define %sGLOG_B%d %s" % (U, i, float.fromhex(h).hex()))
+    arr("double", "log_tab", ltab, hexd)
     out.append("#endif")
     with open(path, "w") as fh:
         fh.write("\n".join(out) + "\n")

@@ -30,6 +30,20 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 SYNTH = os.path.join(ROOT, "tests", "golden", "datasets", "synth_256x512.txt")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+CHAINS_SELECTED = 8    # choose_chains(8) as in Report Table 1 for g10s10
+
+
+def launch_ranks(n):
+    """python bench.py --gpus N without a launcher: start N ranks with torch.distributed.run
+    (one process per GPU, rendezvous on 127.0.0.1) as a child process and return its status."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def algorithmic_bytes_per_iter(N, M):
@@ -62,16 +76,39 @@ def measured_traffic(N, M, chains, sweeps_per_step):
 
 
 def _cpu_worker(args):
-    text, seed, calls = args
+    text, seed, calls, variant = args
     import oracle_ref
+    if variant != "O2":
+        oracle_ref.use_variant(variant)
     t0 = time.perf_counter()
     o = oracle_ref.run_chain(text, seed, 0, calls, sweeps=10)
     return time.perf_counter() - t0, o["rc"]
 
 
-def cpu_baseline(path, calls, workers):
-    """The CPU oracle (restatement of mcmc.c, -O2) on `workers` processes, one chain each,
-    `calls` mcmc_sample calls per chain: aggregate chain-iterations/s."""
+def cpu_share():
+    """CPU cores this process may use: the launcher's thread budget (OMP_NUM_THREADS: the GPU
+    box's per-GPU share; its nproc counts the whole machine), else the affinity mask and the
+    cgroup quota."""
+    nproc = os.cpu_count() or 1
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return n, nproc
+
+
+def cpu_baseline(path, calls, workers, variant="O2"):
+    """The CPU oracle (C restatement of mcmc.c; recount after every accepted proposal as the
+    reference) on `workers` processes, one chain each, `calls` mcmc_sample calls per chain:
+    aggregate chain-iterations/s.  variant "O2" (gcc -O2) or "O0" (reference-like: the shipped
+    binary was built at -O0)."""
     import multiprocessing as mp
     with open(path, "rb") as fh:
         text = fh.read()
@@ -80,14 +117,17 @@ def cpu_baseline(path, calls, workers):
     ctx = mp.get_context("fork")
     t0 = time.perf_counter()
     with ctx.Pool(workers) as pool:
-        res = pool.map(_cpu_worker, [(text, s + 1, calls) for s in range(workers)])
+        res = pool.map(_cpu_worker, [(text, s + 1, calls, variant) for s in range(workers)])
     wall = time.perf_counter() - t0
     assert all(rc == 0 for _, rc in res)
     iters = workers * calls * 10
+    share, nproc = cpu_share()
     return {"value": iters / wall, "unit": "chain-iterations/s", "cores": workers, "kind": "port",
+            "nproc": nproc, "cpu_share": share,
             "sample": "%d chains x %d mcmc_sample calls (%d sweeps each) of the bench workload, oracle/ "
-                      "(C restatement of mcmc.c, gcc -O2, recount after accept as the reference) on %d "
-                      "processes, wall %.1f s" % (workers, calls, 10, workers, wall)}
+                      "(C restatement of mcmc.c, gcc -%s, recount after accept as the reference) on %d "
+                      "processes (one per core of this process's CPU share; nproc %d), wall %.1f s"
+                      % (workers, calls, 10, variant, workers, nproc, wall)}
 
 
 def main():
@@ -102,7 +142,7 @@ def main():
                     "(seed 20261015 for 256x512, 20261016 otherwise: SURVEY.md 8(d) configs 3 and 5)")
     ap.add_argument("--taxa", type=int, default=0)
     ap.add_argument("--columns", default="auto", choices=("auto", "lds", "hbm"))
-    ap.add_argument("--cpu-calls", type=int, default=800)
+    ap.add_argument("--cpu-calls", type=int, default=600)
     ap.add_argument("--cpu-workers", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--block-threads", type=int, default=0)
@@ -110,9 +150,16 @@ def main():
                     "asks for both; the default saves one record per call, as the reference's sampling phase)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: launch the ranks as children (this process has not touched the
+        # GPU and never will) and exit with their status
+        return launch_ranks(args.gpus)
+
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but the launcher started %d rank(s)" % (args.gpus, world))
 
     if args.sites and args.taxa:
         import tempfile
@@ -126,10 +173,12 @@ def main():
         gen_synthetic.write(256, 512, 20261015, args.dataset)
 
     # CPU baseline first, before this process touches the GPU (it forks workers).
-    cpu = None
+    cpu = cpu_o0 = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        workers = args.cpu_workers or max(1, min(16, os.cpu_count() or 1))
+        workers = args.cpu_workers or min(cpu_share()[0], args.chains_per_gpu)
         cpu = cpu_baseline(args.dataset, args.cpu_calls, workers)
+        cpu_o0 = cpu_baseline(args.dataset, max(1, args.cpu_calls // 4), workers, "O0")
+        cpu_o0["kind"] = "port (reference-like -O0 build)"
 
     import numpy as np
     import torch
@@ -137,12 +186,12 @@ def main():
     from seriation_amd import dist as sd
 
     dist = None
+    torch.cuda.set_device(local_rank)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
-    else:
-        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        assert dist.get_world_size() == args.gpus, "RCCL world does not match --gpus"
+        world = dist.get_world_size()
 
     ds = sa.Dataset.load(args.dataset, maxs=0)
     C = args.chains_per_gpu
@@ -177,24 +226,33 @@ def main():
         sess.run(1, save=True)
     stream.synchronize()
     t_kernels = time.perf_counter()
-    cdl = sess.fetch_cdl()
+    # the end of the run: summaries all-gathered -> one-sigma selection on every
+    # rank -> the selected chains' saved samples gathered from their owners
+    ab_pi, cdl = sess.fetch_records()
     rows = sd.summaries_from_records(chain_ids, cdl)
     if dist:
         gathered = sd.gather_summaries(rows, C * world, device="cuda")
     else:
         gathered = rows
-    selected = sd.select_chains(gathered, 8)
+    selected = sd.select_chains(gathered, CHAINS_SELECTED)
+    if dist:
+        sel_ab, sel_cdl = sd.gather_selected_records(selected, C * world, chain_ids, ab_pi, cdl, device="cuda")
+    else:
+        sel_ab, sel_cdl = ab_pi[selected], cdl[selected]
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     tail_ms = (time.perf_counter() - t_kernels) * 1e3
+    # posterior statistics of the selected chains (script.py:100-152), outside the timed region
+    ec, ed, corr = sd.selection_statistics(sel_ab, sel_cdl, ds.N, ds.M, CHAINS_SELECTED)
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
     assert len(gathered) == C * world and np.isfinite(gathered).all() and selected
+    assert sel_ab.shape[0] == len(selected) and (sel_ab[:, :, 2 * ds.M:] >= 0).all()
 
     total_chains = C * world
     sweeps_per_step = cps * 10
@@ -244,9 +302,13 @@ def main():
             "launch_bytes": launch_bytes,
         },
         "cpu_baseline": cpu,
+        "cpu_baseline_O0": cpu_o0,
         "timing": {"kernel_ms_per_step": kernel_ms, "gather_select_ms": tail_ms,
-                   "note": "gather_select_ms: after the last kernel, the record fetch, summary all-gather "
-                           "and one-sigma selection (inside the timed region)"},
+                   "note": "gather_select_ms: after the last kernel, the record fetch, summary all-gather, "
+                           "one-sigma selection and the gather of the selected chains' records (inside the "
+                           "timed region)"},
+        "selection": {"chains_selected": selected, "exp_c": ec, "exp_d": ed, "corr_mn": corr,
+                      "note": "script.py:70-152 over the last step's saved samples of the selected chains"},
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -256,4 +318,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

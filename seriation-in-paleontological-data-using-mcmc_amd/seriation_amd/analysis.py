@@ -1,12 +1,12 @@
 """Posterior summaries over the selected chains (script.py:102-429).
 
-Scalar statistics (E[c], E[d], CORRMN: per-chain sums of ~1000 values) are host numpy, in
-two forms:
+Scalar statistics (E[c], E[d], CORRMN: per-chain sums of ~1000 values) are host Python, in
+two forms with identical results:
   * file form -- reads Chains/chain_NN/chain_data.csv exactly as script.py does (token
     positions, the hard-coded /1000), for drop-in use after `run_all_chains`;
-  * record form -- the same arithmetic on in-memory records (c, d in log scale as the
-    sampler keeps them; pi as int arrays), as produced by `run_chains(keep_records=True)`
-    or gathered across ranks, without the text round trip.
+  * record form -- the same operation sequence on in-memory records (c, d in log scale as
+    the sampler keeps them; pi as int arrays), as produced by `run_chains(keep_records=True)`
+    or gathered across ranks (dist.gather_selected_records), without writing the files.
 
 The per-sample matrix accumulations (pair-order matrix, taxon alive / false-alive /
 false-ones probabilities, E[pi], E[a]) run on the GPU (csrc/sr_post.hip through
@@ -14,6 +14,7 @@ sr_posterior / sr_session_posterior), bit for bit as the script computes them; o
 final argsort reorderings are host numpy.  There is no CPU fallback for them.
 """
 import ctypes
+import math
 import os
 
 import numpy as np
@@ -28,7 +29,8 @@ def _chain_lines(root, chain):
 
 
 def compute_exp_cd(chains, chains_selected, root="."):
-    """script.py:102-124: mean over chains of (sum over samples of the first c / d token)/1000."""
+    """script.py:100-124: mean over chains of (sum over samples of the first c / d token)/1000,
+    divided by chains_selected."""
     c_chain = d_chain = 0.0
     for chain in chains:
         c_sum = d_sum = 0.0
@@ -42,15 +44,16 @@ def compute_exp_cd(chains, chains_selected, root="."):
 
 
 def _pearson_identity(pi):
-    x = np.asarray(pi, np.float64)
-    y = np.arange(len(x), dtype=np.float64)
-    xm, ym = x - x.mean(), y - y.mean()
-    return float((xm * ym).sum() / np.sqrt((xm * xm).sum() * (ym * ym).sum()))
+    """script.py:147: scipy.stats.pearsonr(pi_chain, np.arange(0, sites))[0] -- the reference's
+    own call (scipy of this image; the reference pinned scipy 1.4.1, whose formula may differ
+    from it in the last bits)."""
+    from scipy.stats import pearsonr
+    return float(pearsonr(pi, np.arange(0, len(pi)))[0])
 
 
 def compute_exp_ages(chains, chains_selected, sites, root="."):
     """script.py:127-152 (CORRMN): mean over chains of (sum over samples of
-    pearson(pi, 0..N-1))/1000."""
+    pearson(pi, 0..N-1))/1000, divided by chains_selected."""
     total = 0.0
     for chain in chains:
         s = 0.0
@@ -62,22 +65,42 @@ def compute_exp_ages(chains, chains_selected, sites, root="."):
 
 
 # ---------------------------------------------------------------- record forms
-def exp_cd_from_records(cdl_per_chain):
-    """cdl_per_chain: iterable of [ts, 3] arrays (c, d, loglik) -> (E[c], E[d]) with the
-    reference's /1000 per chain and mean over the chains given."""
+# The same operation sequences on in-memory records (c, d in log scale as the sampler keeps them;
+# pi as int rows), as produced by run_chains(keep_records=True) or gathered across ranks
+# (dist.gather_selected_records): each c / d is the value the file form reads back, i.e.
+# mcmc_save_chain's "%.14f" of the C library's exp (mcmc.c:82-85), summed sequentially; so the
+# record forms equal the file forms bit for bit (tests/test_analysis.py).
+def _token(v):
+    return float("%.14f" % math.exp(v))
+
+
+def exp_cd_from_records(cdl_per_chain, chains_selected=None):
+    """cdl_per_chain: iterable of [ts, 3] arrays (c, d, loglik) -> (E[c], E[d]) as
+    compute_exp_cd; chains_selected defaults to the number of chains given."""
     cdl_per_chain = list(cdl_per_chain)
-    c = sum(np.exp(np.asarray(r)[:, 0]).sum() / 1000 for r in cdl_per_chain)
-    d = sum(np.exp(np.asarray(r)[:, 1]).sum() / 1000 for r in cdl_per_chain)
-    return c / len(cdl_per_chain), d / len(cdl_per_chain)
+    c_chain = d_chain = 0.0
+    for r in cdl_per_chain:
+        c_sum = d_sum = 0.0
+        for c, d, _ll in np.asarray(r, np.float64).tolist():
+            c_sum += _token(c)
+            d_sum += _token(d)
+        c_chain += c_sum / 1000
+        d_chain += d_sum / 1000
+    n = len(cdl_per_chain) if chains_selected is None else chains_selected
+    return c_chain / n, d_chain / n
 
 
-def corr_mn_from_records(pi_per_chain):
+def corr_mn_from_records(pi_per_chain, chains_selected=None):
     """pi_per_chain: iterable of [ts, N] int arrays -> CORRMN as compute_exp_ages."""
     pi_per_chain = list(pi_per_chain)
     tot = 0.0
     for P in pi_per_chain:
-        tot += sum(_pearson_identity(p) for p in np.asarray(P)) / 1000
-    return tot / len(pi_per_chain)
+        s = 0.0
+        for p in np.asarray(P).tolist():
+            s += _pearson_identity(p)
+        tot += s / 1000
+    n = len(pi_per_chain) if chains_selected is None else chains_selected
+    return tot / n
 
 
 # ---------------------------------------------------------------- GPU posterior summaries

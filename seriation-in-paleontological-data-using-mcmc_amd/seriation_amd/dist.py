@@ -1,11 +1,16 @@
 """Multi-GPU chain sharding and the one collective.
 
 Chains are independent given their seed, so ranks never talk while sampling.  One
-process per GPU owns a contiguous block of chains; at the end every rank contributes a
-fixed-size summary record per chain (chain_id, exp_loglik, exp_c, exp_d -- the
-exp_data.csv payload, mcmc.c:53-67) to ONE all-gather (RCCL over xGMI with the "nccl"
-backend, gloo in the CPU tests), after which every rank can run the one-sigma chain
-selection of script.py:70-99 locally and identically.
+process per GPU owns a contiguous block of chains.  At the end:
+  1. every rank contributes a fixed-size summary record per chain (chain_id, exp_loglik,
+     exp_c, exp_d -- the exp_data.csv payload, mcmc.c:53-67) to ONE all-gather (RCCL over
+     xGMI with the "nccl" backend, gloo in the CPU tests), after which every rank runs the
+     one-sigma chain selection of script.py:70-99 locally and identically;
+  2. the selected chains' saved samples (a, b, pi rows + c, d, loglik) -- the input of
+     script.py:102-189 (E[c], E[d], CORRMN, pair-order matrix) -- are all-gathered from the
+     ranks that own them (one collective of k_max selected chains per rank, k_max = the
+     largest number of selected chains any one rank owns), so any rank can compute the
+     posterior statistics exactly as a single-GPU run does.
 """
 import math
 
@@ -64,3 +69,61 @@ def select_chains(all_rows, chains_selected):
     """script.py choose_chains on gathered rows (chain dirs named as the reference does)."""
     vals = {"chain_%02d" % int(r[0]): float(r[1]) for r in all_rows}
     return choose_from_values(vals, chains_selected)
+
+
+def owner(chain_id, n_total, world):
+    """Rank whose contiguous shard holds chain_id."""
+    for r in range(world):
+        sh = shard(n_total, world, r)
+        if sh.start <= chain_id < sh.stop:
+            return r
+    raise ValueError("chain %d outside 0..%d" % (chain_id, n_total - 1))
+
+
+def gather_selected_records(selected, n_total, local_ids, ab_pi, cdl, device="cpu", group=None):
+    """Step 2 of the collective: the saved samples of the `selected` chain ids, in selection
+    order, on every rank.  local_ids: this rank's chain ids (its shard); ab_pi [n_local, T, W]
+    int16 and cdl [n_local, T, 3] float64 are its records (T saved calls, W = 2M + N).
+    One all_gather per array of [k_max, T, ...] slabs (int16 rows travel as bytes: RCCL has no
+    16-bit integer type).  Returns (ab_pi [k, T, W] int16, cdl [k, T, 3] float64)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    ab_pi = np.ascontiguousarray(ab_pi, np.int16)
+    cdl = np.ascontiguousarray(cdl, np.float64)
+    T, W = ab_pi.shape[1], ab_pi.shape[2]
+    owners = [owner(int(c), n_total, world) for c in selected]
+    k_max = max([owners.count(r) for r in range(world)] + [1])
+    pos = {int(c): k for k, c in enumerate(local_ids)}
+    mine = [int(c) for c, o in zip(selected, owners) if o == rank]
+    sab = np.zeros((k_max, T, W), np.int16)
+    scd = np.zeros((k_max, T, 3), np.float64)
+    for j, c in enumerate(mine):
+        sab[j] = ab_pi[pos[c]]
+        scd[j] = cdl[pos[c]]
+    tab = torch.as_tensor(sab.view(np.uint8), device=device)
+    tcd = torch.as_tensor(scd, device=device)
+    pab = [torch.empty_like(tab) for _ in range(world)]
+    pcd = [torch.empty_like(tcd) for _ in range(world)]
+    dist.all_gather(pab, tab, group=group)
+    dist.all_gather(pcd, tcd, group=group)
+    gab = [p.cpu().numpy().view(np.int16).reshape(k_max, T, W) for p in pab]
+    gcd = [p.cpu().numpy() for p in pcd]
+    out_ab = np.zeros((len(selected), T, W), np.int16)
+    out_cd = np.zeros((len(selected), T, 3), np.float64)
+    slot = [0] * world
+    for k, o in enumerate(owners):
+        out_ab[k] = gab[o][slot[o]]
+        out_cd[k] = gcd[o][slot[o]]
+        slot[o] += 1
+    return out_ab, out_cd
+
+
+def selection_statistics(ab_pi, cdl, N, M, chains_selected):
+    """E[c], E[d], CORRMN of script.py:102-152 on the selected chains' records (record form of
+    analysis.compute_exp_cd / compute_exp_ages)."""
+    from . import analysis
+    ec, ed = analysis.exp_cd_from_records(list(cdl), chains_selected)
+    corr = analysis.corr_mn_from_records([np.asarray(r)[:, 2 * M:2 * M + N] for r in ab_pi], chains_selected)
+    return ec, ed, corr

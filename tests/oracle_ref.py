@@ -18,27 +18,38 @@ P = ctypes.POINTER
 def lib():
     global _L
     if _L is None:
-        if not os.path.exists(LIB):
-            subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
-        L = ctypes.CDLL(LIB)
-        L.oracle_parse.restype = ctypes.c_int
-        L.oracle_parse.argtypes = [ctypes.c_char_p, ctypes.c_long, ctypes.c_int, P(ctypes.c_int), P(ctypes.c_int),
-                                   P(ctypes.c_int), P(ctypes.c_int32), P(ctypes.c_int32)]
-        L.oracle_run_chain.restype = ctypes.c_int
-        L.oracle_run_chain.argtypes = [ctypes.c_char_p, ctypes.c_long, ctypes.c_int, ctypes.c_ulong, ctypes.c_int,
-                                       ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                       P(ctypes.c_int32), P(ctypes.c_double), P(ctypes.c_int32), P(ctypes.c_double),
-                                       P(ctypes.c_double), P(ctypes.c_longlong), P(ctypes.c_ulonglong)]
-        L.oracle_rng_stream.restype = None
-        L.oracle_rng_stream.argtypes = [ctypes.c_ulong, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_long,
-                                        P(ctypes.c_double), P(ctypes.c_ulonglong)]
-        L.oracle_shuffle.argtypes = [ctypes.c_ulong, P(ctypes.c_int32), ctypes.c_long]
-        L.oracle_choose.argtypes = [ctypes.c_ulong, P(ctypes.c_int32), ctypes.c_long, P(ctypes.c_int32), ctypes.c_long]
-        L.oracle_exp_log.argtypes = [P(ctypes.c_double), ctypes.c_long, P(ctypes.c_double), P(ctypes.c_double)]
-        L.oracle_libm_mismatch.restype = None
-        L.oracle_libm_mismatch.argtypes = [P(ctypes.c_double), ctypes.c_long, P(ctypes.c_long), P(ctypes.c_long)]
-        _L = L
+        _L = load(LIB)
     return _L
+
+
+def use_variant(name):
+    """Switch this process to another build of the oracle: "O0" = oracle/build/O0/liboracle.so
+    (the reference-like -O0 CPU baseline of bench.py)."""
+    global _L
+    _L = load(os.path.join(ORACLE_DIR, "build", name, "liboracle.so"))
+
+
+def load(path):
+    if not os.path.exists(path):
+        subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
+    L = ctypes.CDLL(path)
+    L.oracle_parse.restype = ctypes.c_int
+    L.oracle_parse.argtypes = [ctypes.c_char_p, ctypes.c_long, ctypes.c_int, P(ctypes.c_int), P(ctypes.c_int),
+                               P(ctypes.c_int), P(ctypes.c_int32), P(ctypes.c_int32)]
+    L.oracle_run_chain.restype = ctypes.c_int
+    L.oracle_run_chain.argtypes = [ctypes.c_char_p, ctypes.c_long, ctypes.c_int, ctypes.c_ulong, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                   P(ctypes.c_int32), P(ctypes.c_double), P(ctypes.c_int32), P(ctypes.c_double),
+                                   P(ctypes.c_double), P(ctypes.c_longlong), P(ctypes.c_ulonglong)]
+    L.oracle_rng_stream.restype = None
+    L.oracle_rng_stream.argtypes = [ctypes.c_ulong, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_long,
+                                    P(ctypes.c_double), P(ctypes.c_ulonglong)]
+    L.oracle_shuffle.argtypes = [ctypes.c_ulong, P(ctypes.c_int32), ctypes.c_long]
+    L.oracle_choose.argtypes = [ctypes.c_ulong, P(ctypes.c_int32), ctypes.c_long, P(ctypes.c_int32), ctypes.c_long]
+    L.oracle_exp_log.argtypes = [P(ctypes.c_double), ctypes.c_long, P(ctypes.c_double), P(ctypes.c_double)]
+    L.oracle_libm_mismatch.restype = None
+    L.oracle_libm_mismatch.argtypes = [P(ctypes.c_double), ctypes.c_long, P(ctypes.c_long), P(ctypes.c_long)]
+    return L
 
 
 def _p(a, t):

@@ -1,5 +1,5 @@
 """Posterior summaries (script.py:102-189) on oracle-written chain files: file form equals
-the literal restatement, record form equals file form up to the %.14f text rounding."""
+the literal restatement, record form equals file form bit for bit."""
 import os
 import subprocess
 
@@ -38,10 +38,13 @@ def test_file_and_record_forms_agree(tmp_path):
     N, M = 124, 139
     c, d = analysis.compute_exp_cd(chains, 3, root=str(tmp_path))
     c2, d2 = analysis.exp_cd_from_records([recs[k]["rec_dbl"] for k in chains])
-    assert abs(c - c2) < 1e-13 and abs(d - d2) < 1e-13
+    assert (c, d) == (c2, d2)
+    # chains_selected larger than the chains found (the script divides by chains_selected)
+    assert analysis.compute_exp_cd(chains[:2], 3, root=str(tmp_path)) == \
+        analysis.exp_cd_from_records([recs[k]["rec_dbl"] for k in chains[:2]], 3)
     r = analysis.compute_exp_ages(chains, 3, N, root=str(tmp_path))
     r2 = analysis.corr_mn_from_records([recs[k]["rec_int"][:, 2 * M:] for k in chains])
-    assert abs(r - r2) < 1e-12
+    assert r == r2
     # the oracle's vectorised pair-order (checker of the GPU kernel) equals the script's literal
     # loops (script.py:155-189 with generate_po_matrix), read back from the chain files
     po_ref = np.zeros((N, N))
@@ -61,3 +64,14 @@ def test_file_and_record_forms_agree(tmp_path):
     prod = analysis.read_chain_rows(str(tmp_path), chains, N, M)
     for k in range(3):
         assert np.array_equal(prod[k], rows[k])
+
+
+def test_pearson_is_the_scripts_call():
+    """CORRMN's per-sample coefficient is script.py:147's scipy.stats.pearsonr(pi_chain,
+    np.arange(0, sites))[0] (list of ints against an int range), bit for bit."""
+    from scipy.stats import pearsonr
+    rng = np.random.default_rng(3)
+    for n in (124, 273, 256, 2):
+        for _ in range(200 if n > 2 else 2):
+            pi = [int(v) for v in rng.permutation(n)]
+            assert analysis._pearson_identity(pi) == pearsonr(pi, np.arange(0, n))[0]

@@ -1,5 +1,6 @@
-"""N>1 path on the CPU: world_size-2 gloo processes shard chains, all-gather the summary
-records (the one collective) and select identical chains on every rank.
+"""N>1 path on the CPU: world_size-2 gloo processes shard chains (run by the CPU oracle),
+all-gather the summary records, select identical chains on every rank and gather the selected
+chains' records (the two collectives), matching a single-process run exactly.
 """
 import os
 import socket
@@ -41,22 +42,53 @@ def _free_port():
     return port
 
 
+DS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "datasets", "g10s10.txt")
+TB, TS, K = 2, 6, 3   # burn-in calls, saved calls, chains selected
+
+
+def _oracle_shard(ids):
+    """The chains of one shard (seed = chain id + 1), run by the CPU oracle: records as the
+    GPU session returns them (a|b|pi int16 rows, c/d/loglik)."""
+    import oracle_ref
+    with open(DS, "rb") as fh:
+        text = fh.read()
+    runs = [oracle_ref.run_chain(text, i + 1, TB, TS) for i in ids]
+    ab = np.array([r["rec_int"] for r in runs], np.int16).reshape(len(ids), TS, -1)
+    cdl = np.array([r["rec_dbl"] for r in runs]).reshape(len(ids), TS, 3)
+    return ab, cdl
+
+
+def _single_process(n_total):
+    ids = list(range(n_total))
+    ab, cdl = _oracle_shard(ids)
+    rows = sd.summaries_from_records(ids, cdl)
+    sel = sd.select_chains(rows, K)
+    sab, scd = ab[sel], cdl[sel]
+    return rows, sel, sab, scd, sd.selection_statistics(sab, scd, 124, 139, K)
+
+
 def _worker(rank, world, port, n_total, out):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         ids = list(sd.shard(n_total, world, rank))
-        # deterministic fake per-chain summaries (value depends only on chain id)
-        rows = np.array([[i, 1000.0 + ((i * 37) % 23) * 0.5, 0.01, 0.5] for i in ids]).reshape(-1, 4)
-        allrows = sd.gather_summaries(rows, n_total)
-        out[rank] = (allrows.tobytes(), sd.select_chains(allrows, 8))
+        ab, cdl = _oracle_shard(ids)
+        rows = sd.summaries_from_records(ids, cdl)
+        allrows = sd.gather_summaries(rows, n_total)           # collective 1
+        sel = sd.select_chains(allrows, K)
+        sab, scd = sd.gather_selected_records(sel, n_total, ids, ab, cdl)   # collective 2
+        stats = sd.selection_statistics(sab, scd, 124, 139, K)
+        out[rank] = (allrows.tobytes(), sel, sab.tobytes(), scd.tobytes(), stats)
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n_total", [100, 7])
-def test_gloo_world2_gather_and_select(n_total):
+@pytest.mark.parametrize("n_total", [8, 5])
+def test_gloo_world2_matches_single_process(n_total):
+    """Two gloo ranks shard real (oracle-run) chains, all-gather the summaries, select, gather the
+    selected chains' records and compute E[c] / E[d] / CORRMN: every rank gets exactly what one
+    process running all chains gets."""
     ctx = mp.get_context("spawn")
     mgr = ctx.Manager()
     out = mgr.dict()
@@ -65,16 +97,22 @@ def test_gloo_world2_gather_and_select(n_total):
     for p in procs:
         p.start()
     for p in procs:
-        p.join(120)
+        p.join(180)
         assert p.exitcode == 0
-    (b0, s0), (b1, s1) = out[0], out[1]
-    assert b0 == b1 and s0 == s1
-    allrows = np.frombuffer(b0).reshape(-1, 4)
-    assert allrows[:, 0].tolist() == list(range(n_total))
-    expect = np.array([1000.0 + ((i * 37) % 23) * 0.5 for i in range(n_total)])
-    np.testing.assert_array_equal(allrows[:, 1], expect)
-    ref = sd.choose_from_values({"chain_%02d" % i: v for i, v in enumerate(expect)}, 8)
-    assert s0 == ref
+    rows, sel, sab, scd, stats = _single_process(n_total)
+    assert 0 < len(sel) <= K
+    for r in range(2):
+        b, s_, ab_b, cd_b, st = out[r]
+        assert b == rows.tobytes()
+        assert s_ == sel
+        assert ab_b == sab.tobytes() and cd_b == scd.tobytes()
+        assert st == stats
+
+
+def test_owner_matches_shard():
+    for n, world in ((800, 8), (7, 3), (5, 2)):
+        for c in range(n):
+            assert c in sd.shard(n, world, sd.owner(c, n, world))
 
 
 def test_summaries_match_exp_data_bits():

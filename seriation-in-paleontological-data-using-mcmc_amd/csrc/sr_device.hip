@@ -2284,6 +2284,9 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
 extern "C" int srk_set_stream(srk_dev *d, void *stream)
 {
   HIPCHK(hipSetDevice(d->device));
+  /* work already queued on the old stream reads and writes the chain state the next launch
+     uses: drain it before switching, so the launch order is the call order */
+  HIPCHK(hipStreamSynchronize(d->stream));
   if (d->own_stream) { (void)hipStreamDestroy(d->stream); d->own_stream = 0; }
   d->stream = (hipStream_t)stream;
   return 0;

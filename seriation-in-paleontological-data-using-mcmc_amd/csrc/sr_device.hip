@@ -82,9 +82,15 @@ struct KArgs {
 
 /* ---------------------------------------------------------------- LDS carve */
 struct Lay {
-  size_t tab, cbuf, lbuf, mt, P, rpi0, rpi1, ht, ck, ccnt, sab, scnt, hpw, hbw, t4, pre, part, tot, xs, misc, total;
+  size_t tab, cbuf, lbuf, mt, P, rpi0, rpi1, ht, ck, ccnt, sab, scnt, hpw, hbw, t4, t8, pre, part, tot, xs, misc, total;
 };
 __host__ __device__ static inline size_t sr_al16(size_t x) { return (x + 15) & ~(size_t)15; }
+/* walk words held in registers by the register-column kernels (NWM template argument): 9 for
+ * N <= 287, 17 for N <= 543, else 0 (columns walked in LDS, Gibbs checkpoints in LDS) */
+__host__ __device__ static inline int sr_nwm(int N) { const int nk = (N >> 5) + 1; return nk <= 9 ? 9 : (nk <= 17 ? 17 : 0); }
+/* the register-column kernels exist for TB 256 and 512 (LDS columns only) */
+__host__ __device__ static inline bool sr_regwalk(int N, int TB, bool gm) { return !gm && TB <= 512 && sr_nwm(N) > 0; }
+#define T8STRIDE 514   /* doubles per wave: 256 byte entries {sum, product} + the dead entry {0, 1} */
 /* Gibbs checkpoint slots per word: one per thread that owns a taxon */
 __host__ __device__ static inline int sr_ckstride(int M, int TB) { return M >= TB ? TB : ((M + 63) & ~63); }
 /* gm: the global-memory variant (columns too large for LDS, e.g. 1024 x 2048): the per-taxon
@@ -104,13 +110,15 @@ __host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB, bo
   L.rpi0 = o;  o = sr_al16(o + (size_t)N * 4);
   L.rpi1 = o;  o = sr_al16(o + (size_t)N * 4);
   L.ht = o;    o = sr_al16(o + (size_t)NWV * (2 * N + 2) * 2);           /* per wave: hcnt[N+1], nhall[N] (int16) */
-  L.ck = o;    o = sr_al16(o + g * ((N >> 5) + 1) * sr_ckstride(M, TB) * sizeof(double));
+  const size_t rw = sr_regwalk(N, TB, gm) ? 1 : 0;   /* register walks: byte tables instead of LDS checkpoints */
+  L.ck = o;    o = sr_al16(o + g * (1 - rw) * ((N >> 5) + 1) * sr_ckstride(M, TB) * sizeof(double));
   L.ccnt = o;  o = sr_al16(o + (size_t)2 * KT * 4);
   L.sab = o;   o = sr_al16(o + g * 2 * M * 4);
   L.scnt = o;  o = sr_al16(o + g * 4 * M * 4);
   L.hpw = o;   o = sr_al16(o + (size_t)NWV * SR_NHMAX * 4);           /* per wave: hard positions */
   L.hbw = o;   o = sr_al16(o + (size_t)NWV * NW * 4);                 /* per wave: hard bitmap */
   L.t4 = o;    o = sr_al16(o + (size_t)NWV * 160 * 8);                /* per wave: 4-entry step tables (T4STRIDE) */
+  L.t8 = o;    o = sr_al16(o + rw * NWV * T8STRIDE * 8);              /* per wave: 8-entry step tables (T8STRIDE) */
   L.pre = o;   o = sr_al16(o + g * (NW + 1) * M * 2);                 /* column prefix ones per word boundary */
   L.part = o;  o = sr_al16(o + (size_t)2 * 16 * NWV * 8 * 4);         /* [2][proposal][wave] count sums */
   L.tot = o;   o = sr_al16(o + (size_t)2 * NWV * 4 * 4);               /* [2][wave] t0, f0, t1, f1 */
@@ -856,7 +864,8 @@ __device__ __forceinline__ int walk_prefix_s(const uint32_t (&wk)[NWM], int w)
 template <int NWM>
 __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint32_t *Pm, int M, int N, bool rev, int o,
                                            int L, double u, const CD &K, const sr_mtab &tb, double vA, double vB,
-                                           const double *T4, uint64_t *fbk, int &dt0, int &df0, int &dt1, int &df1)
+                                           const double *T4, const double *T8, uint64_t *fbk, int &dt0, int &df0, int &dt1,
+                                           int &df1)
 {
   const int POo = walk_prefix_s<NWM>(wk, o);
   const int nk = (L >> 5) + 1;
@@ -893,35 +902,53 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
     atomicAdd((unsigned long long *)fbk + 29, 1ull);
   }
 #endif
-  /* pass 1: S over the window; word-start y and end-of-word checkpoints kept in registers */
+  /* pass 1: S over the window; word-start y and end-of-word checkpoints kept in registers.
+     Byte steps: T8[byte] = {sum of the byte's 8 prefix products, their product}; T8[256] =
+     {0, 1} is the dead entry, read for every byte outside the window or not wholly inside the
+     walk (it leaves S and y unchanged), so no step needs a select.  A word's 4 entries are read
+     together (one LDS round trip per word).  The walk's partial last byte ((L + 1) mod 8
+     entries) follows from the 4-entry tables (T4 rows c = 0..4). */
   const double y0 = exp2_split(qlo);
   double S = 0.0;
   double ckr[NWM], yst[NWM];
+  double y = y0;
   {
-    double y = y0;
 #pragma unroll
     for (int k = 0; k < NWM; ++k) {
-      const bool act = k >= klo && k <= khi;
-      const int nbe = act ? min(32, L + 1 - 32 * k) : 0;
+      const bool inw = k >= klo && k <= khi;
+      const int nfk = inw ? min(max((L + 1 - 32 * k) >> 3, 0), 4) : 0;   /* whole bytes of word k in the walk */
       yst[k] = y;
-      double yk = y;
+      double2 t[4];
 #pragma unroll
-      for (int g = 0; g < 8; ++g) {
-        const uint32_t nib = (wk[k] >> (4 * g)) & 15u;
-        const int c = min(max(nbe - 4 * g, 0), 4);
-        const double2 t = t4sp(T4, c, nib);
-        S = __builtin_fma(yk, t.x, S);
-        yk = yk * t.y;
+      for (int g = 0; g < 4; ++g) {
+        const uint32_t e = (g < nfk) ? ((wk[k] >> (8 * g)) & 255u) : 256u;
+        t[g] = *reinterpret_cast<const double2 *>(T8 + 2 * e);
       }
-      y = act ? yk : y;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        S = __builtin_fma(y, t[g].x, S);
+        y = y * t[g].y;
+      }
       ckr[k] = S;
+      __builtin_amdgcn_sched_barrier(0);   /* keep each word's loads next to their use (register pressure) */
     }
+    /* the partial byte (c8 entries) when its word lies in the window */
+    const int nfull = (L + 1) >> 3, c8 = (L + 1) & 7, kb = nfull >> 2;
+    const bool actb = c8 > 0 && kb >= klo && kb <= khi;
+    uint32_t wb = 0u;   /* word kb by masks (a select at a runtime index becomes a scratch array) */
+#pragma unroll
+    for (int k = 0; k < NWM; ++k) wb |= wk[k] & (0u - (uint32_t)(k == kb));
+    const uint32_t eb = (wb >> (8 * (nfull & 3))) & 255u;
+    const double2 tlo = t4sp(T4, actb ? min(c8, 4) : 0, eb & 15u);
+    const double shi = t4s(T4, actb ? max(c8 - 4, 0) : 0, eb >> 4);
+    S = __builtin_fma(y, tlo.x, S);
+    S = __builtin_fma(y * tlo.y, shi, S);
   }
   /* pass 2: locate the word, then the group and entry where u falls; certify */
   int res = -1;
   if (S > 0.0 && S < 0x1p1000) {
     const double inv = 1.0 / S;
-    const double REL = (double)(N + 1) * 0x1p-50;
+    const double REL = (double)(N + 33) * 0x1p-50;   /* + the byte tables' own rounding (<= 16 ulp per entry) */
     const double ABS = (double)(N + 1) * 0x1p-39;
     int j = klo;
 #pragma unroll
@@ -941,14 +968,22 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
     {
       double yy = y, acc = Sp0;
 #pragma unroll
-      for (int g = 0; g < 8; ++g) {
-        const uint32_t nib = (ww >> (4 * g)) & 15u;
-        const int c = min(max(nb - 4 * g, 0), 4);
-        gy[g] = yy;
-        const double2 t = t4sp(T4, c, nib);
-        acc = __builtin_fma(yy, t.x, acc);
-        gsum[g] = acc;
-        yy = yy * t.y;
+      for (int h = 0; h < 2; ++h) {   /* 4 table entries per LDS round trip */
+        double2 tt[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const uint32_t nib = (ww >> (4 * (4 * h + g))) & 15u;
+          const int c = min(max(nb - 4 * (4 * h + g), 0), 4);
+          tt[g] = t4sp(T4, c, nib);
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          gy[4 * h + g] = yy;
+          acc = __builtin_fma(yy, tt[g].x, acc);
+          gsum[4 * h + g] = acc;
+          yy = yy * tt[g].y;
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
       for (int g = 0; g < 8; ++g) ng += (g < nvg && gsum[g] * inv < u) ? 1 : 0;
@@ -989,12 +1024,18 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
   return res;
 }
 
-/* the forward and reversed walk words of column m (positions; positions N-1-w), NW <= NWM */
+/* the forward walk words of column m (positions), NW <= NWM */
 template <int NWM>
-__device__ __forceinline__ void load_walks(const uint32_t *Pm, int M, int N, int NW, uint32_t (&fw)[NWM], uint32_t (&rw)[NWM])
+__device__ __forceinline__ void load_fwd(const uint32_t *Pm, int M, int NW, uint32_t (&fw)[NWM])
 {
 #pragma unroll
   for (int k = 0; k < NWM; ++k) fw[k] = (k < NW) ? Pm[min(k, NW - 1) * M] : 0u;
+}
+
+/* the reversed walk words (positions N-1-w) built from the forward words fw[] */
+template <int NWM>
+__device__ __forceinline__ void make_rev(const uint32_t *Pm, int M, int N, int NW, const uint32_t (&fw)[NWM], uint32_t (&rw)[NWM])
+{
   /* reversed word k = brev(column bits [s, s+32)), s = N - 32 - 32k = 32 (q - 1 - k) + r: built
      from fw[] with compile-time indices inside a block-uniform switch on q = N / 32 (a select at
      a runtime index made the compiler spill fw to scratch) */
@@ -1336,6 +1377,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   int *hp = (int *)(smem + L.hpw) + wave * SR_NHMAX;   /* this wave's copy of the hard positions */
   uint32_t *hbw = (uint32_t *)(smem + L.hbw) + wave * NW;   /* this wave's hard bitmap */
   double *T4w = (double *)(smem + L.t4) + wave * T4STRIDE;   /* this wave's 4-step tables */
+  double *T8w = (double *)(smem + L.t8) + wave * T8STRIDE;   /* this wave's 8-step tables (register walks) */
   int *part = (int *)(smem + L.part);
   int *tot = (int *)(smem + L.tot);
   double *xs = (double *)(smem + L.xs) + wave;
@@ -1446,6 +1488,18 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 #pragma unroll
         for (int c = 0; c < 5; ++c) { T4w[2 * (c * 16 + lane)] = sc[c]; T4w[2 * (c * 16 + lane) + 1] = pr; }
       }
+      if constexpr (NWM > 0) {   /* per-wave tables for 8 walk entries with bits = e: {sum of the 8 prefix
+                                    products, product of all 8}; 4 entries per lane */
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int e = lane + 64 * q;
+          double pr = 1.0, sm = 0.0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) { sm = sm + pr; pr = pr * (((e >> k) & 1) ? rB : rA); }
+          *reinterpret_cast<double2 *>(T8w + 2 * e) = make_double2(sm, pr);
+        }
+        if (lane == 0) *reinterpret_cast<double2 *>(T8w + 2 * 256) = make_double2(0.0, 1.0);
+      }
       wsync();
 
 #ifdef SR_STAMP_GIBBS
@@ -1476,16 +1530,19 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
              inlined copy of the draw, two trips */
           int na = a0, nb = b0;
           if constexpr (NWM > 0) {   /* column in registers, branch-free draws */
-            uint32_t fw[NWM], rw[NWM];
-            load_walks<NWM>(Pm, M, N, NW, fw, rw);
+            uint32_t wk[NWM];   /* forward walk words, then (second trip) the reversed ones */
+            load_fwd<NWM>(Pm, M, NW, wk);
             for (int pass = 0; pass < 2; ++pass) {
               int d0, e0, d1, e1;
               const bool rev = pass != 0;
-              uint32_t wk[NWM];
+              if (rev) {
+                uint32_t rw[NWM];
+                make_rev<NWM>(Pm, M, N, NW, wk, rw);
 #pragma unroll
-              for (int k = 0; k < NWM; ++k) wk[k] = rev ? rw[k] : fw[k];
+                for (int k = 0; k < NWM; ++k) wk[k] = rw[k];
+              }
               const int res = draw_fast_s<NWM>(wk, Pm, M, N, rev, rev ? N - b0 : a0, rev ? N - na : b0, rev ? ub : ua, K,
-                                               tb, vA, vB, T4w, &misc[MS_FBK], d0, e0, d1, e1);
+                                               tb, vA, vB, T4w, T8w, &misc[MS_FBK], d0, e0, d1, e1);
               t0 += d0; f0 += e0; t1 += d1; f1 += e1;
               if (rev) nb = N - res; else na = res;
             }
@@ -2187,7 +2244,6 @@ typedef void (*sr_kfn)(KArgs);
 
 /* NWM: walks of <= 9 / 17 words (N + 1 entries: N <= 287 / 543) use the register-resident
  * Gibbs draw, longer ones the LDS walk.  gm: the HBM-column variant (sr_layout) */
-static int sr_nwm(int N) { const int nk = (N >> 5) + 1; return nk <= 9 ? 9 : (nk <= 17 ? 17 : 0); }
 static sr_kfn sr_pick_kernel(int TB, int N, bool gm)
 {
   if (gm) {
@@ -2196,7 +2252,7 @@ static sr_kfn sr_pick_kernel(int TB, int N, bool gm)
     if (TB == 1024) return (sr_kfn)sr_sweep_kernel<1024, 0, true>;
     return nullptr;
   }
-  const int nwm = sr_nwm(N);
+  const int nwm = sr_regwalk(N, TB, false) ? sr_nwm(N) : 0;
   if (TB == 256) return nwm == 9 ? (sr_kfn)sr_sweep_kernel<256, 9, false> : nwm == 17 ? (sr_kfn)sr_sweep_kernel<256, 17, false> : (sr_kfn)sr_sweep_kernel<256, 0, false>;
   if (TB == 512) return nwm == 9 ? (sr_kfn)sr_sweep_kernel<512, 9, false> : nwm == 17 ? (sr_kfn)sr_sweep_kernel<512, 17, false> : (sr_kfn)sr_sweep_kernel<512, 0, false>;
   if (TB == 1024) return (sr_kfn)sr_sweep_kernel<1024, 0, false>;

@@ -39,31 +39,7 @@ __constant__ double c_zig_w[128] = SR_ZIG_WTAB_INIT;
 __constant__ uint64_t c_exp_tab[256] = SR_EXP_TAB_INIT;
 __constant__ double c_log_tab[256] = SR_LOG_TAB_INIT;
 
-#ifndef SR_EXP
-#define SR_EXP 0   /* timing experiments only (break the sampler): 1 skip proposals, 2 skip Gibbs, 4/8/16 skip pi3/pi2/pi1 terms */
-#endif
-#define SR_ZIGR 3.44428647676
-#ifndef SR_ZIG_UNIFORM
-#define SR_ZIG_UNIFORM 1
-#endif
-#ifndef SR_HALF_DRAWS
-#define SR_HALF_DRAWS 1
-#endif
-#ifndef SR_GATHER_SCAN
-#define SR_GATHER_SCAN 1
-#endif
-#ifndef SR_CD_FAST
-#define SR_CD_FAST 1
-#endif
-#ifndef SR_SWAP_ALONE
-#define SR_SWAP_ALONE 1
-#endif
-#ifndef SR_PI1_BALLOT
-#define SR_PI1_BALLOT 1
-#endif
-#ifndef SR_PRE_INCR
-#define SR_PRE_INCR 1
-#endif
+#define SR_ZIGR 3.44428647676   /* GSL gaussian_ziggurat PARAM_R */
 
 struct KArgs {
   int N, M, NW, nh, nchains;
@@ -373,13 +349,9 @@ template <bool WAVE>
 __device__ __forceinline__ double d_gauss_zig(DRng &r, int lane, int nthr, const sr_mtab &tb)
 {
   for (;;) {
-#if SR_ZIG_UNIFORM
     /* the word is block-uniform: keep it (and the table index) in SGPRs so the ziggurat table
        lookups are scalar constant-cache loads */
     uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)rng_get<WAVE>(r, lane, nthr));
-#else
-    uint32_t k = rng_get<WAVE>(r, lane, nthr);
-#endif
     uint32_t i = k & 0xFF;
     uint32_t j = (k >> 8) & 0xFFFFFF;
     int sign = (i & 0x80) ? +1 : -1;
@@ -913,24 +885,31 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
   double ckr[NWM], yst[NWM];
   double y = y0;
   {
-#pragma unroll
-    for (int k = 0; k < NWM; ++k) {
+    /* word k's 4 entries (whole bytes of the walk inside the window; the dead entry otherwise) */
+    auto wload = [&](int k, double2 (&t)[4]) {
       const bool inw = k >= klo && k <= khi;
-      const int nfk = inw ? min(max((L + 1 - 32 * k) >> 3, 0), 4) : 0;   /* whole bytes of word k in the walk */
-      yst[k] = y;
-      double2 t[4];
+      const int nfk = inw ? min(max((L + 1 - 32 * k) >> 3, 0), 4) : 0;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const uint32_t e = (g < nfk) ? ((wk[k] >> (8 * g)) & 255u) : 256u;
         t[g] = *reinterpret_cast<const double2 *>(T8 + 2 * e);
       }
+    };
+    double2 t[4], tn[4];
+    wload(0, t);
+#pragma unroll
+    for (int k = 0; k < NWM; ++k) {
+      if (k + 1 < NWM) wload(k + 1, tn);   /* next word's reads in flight while this word is summed */
+      yst[k] = y;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         S = __builtin_fma(y, t[g].x, S);
         y = y * t[g].y;
       }
       ckr[k] = S;
-      __builtin_amdgcn_sched_barrier(0);   /* keep each word's loads next to their use (register pressure) */
+#pragma unroll
+      for (int g = 0; g < 4; ++g) t[g] = tn[g];
+      __builtin_amdgcn_sched_barrier(0);   /* one word of reads ahead, no more (register pressure) */
     }
     /* the partial byte (c8 entries) when its word lies in the window */
     const int nfull = (L + 1) >> 3, c8 = (L + 1) & 7, kb = nfull >> 2;
@@ -1459,7 +1438,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           s0 += tw[0]; s1 += tw[1]; s2 += tw[2]; s3 += tw[3];
         }
         /* mcmc_samplec then mcmc_sampled: Beta(1 + f1, 1 + t0), Beta(1 + f0, 1 + t1) */
-        if (!(SR_CD_FAST && draw_cd_fast(R, c, d, s3, s0, s1, s2, tb, lane))) {
+        if (!draw_cd_fast(R, c, d, s3, s0, s1, s2, tb, lane)) {
           double cd2[2] = {c, d};
           for (int k = 0; k < 2; ++k)
             cd2[k] = d_samplebeta<false>(R, cd2[k], (double)(k ? s1 : s3), (double)(k ? s2 : s0), k ? SR_MIND : SR_MINC,
@@ -1471,11 +1450,16 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         if (tid == 0) { misc[MS_ACC + 0]++; misc[MS_ACC + 1]++; }
       }
       CD K;
-      K.c = c; K.d = d; K.cc = sr_log_m(1. - sr_exp_m(c, &tb), &tb); K.dd = sr_log_m(1. - sr_exp_m(d, &tb), &tb); K.ec = ec;
+      /* cc = log(1 - e^c) on even lanes, dd = log(1 - e^d) on odd lanes: one evaluation chain
+         instead of two */
+      const bool oddl = (lane & 1) != 0;
+      const double l1 = sr_log_m(1. - sr_exp_m(oddl ? d : c, &tb), &tb);
+      K.c = c; K.d = d; K.cc = readlane_f64(l1, 0); K.dd = readlane_f64(l1, 1); K.ec = ec;
       /* one position's value in q (log2 units): zero -> d - cc, one -> dd - c */
       const double vA = (K.d - K.cc) * 1.4426950408889634;
       const double vB = (K.dd - K.c) * 1.4426950408889634;
-      const double rA = sr_exp_m(K.cc - K.d, &tb), rB = sr_exp_m(K.c - K.dd, &tb);   /* 2^-vA, 2^-vB */
+      const double r2 = sr_exp_m(oddl ? K.c - K.dd : K.cc - K.d, &tb);
+      const double rA = readlane_f64(r2, 0), rB = readlane_f64(r2, 1);   /* 2^-vA, 2^-vB */
       if (lane < 16) {   /* per-wave tables for 4 walk entries with bits = lane */
         double pr = 1.0, sm = 1.0;
         double sc[5];
@@ -1520,7 +1504,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         FST(1);
         rng_ensure(R, min(2 * (mhi - mlo) + SR_RNG_SLACK, rcap), tid, TB);
         FST(8);
-        for (int m = mlo + tid; m < mhi && !(SR_EXP & 2); m += TB) {
+        for (int m = mlo + tid; m < mhi; m += TB) {
           const uint32_t *Pm = P + m;
           const double ua = rng_peek(R, 2 * (m - mlo)) / 4294967296.0;
           const double ub = rng_peek(R, 2 * (m - mlo) + 1) / 4294967296.0;
@@ -1595,7 +1579,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
          computed against the current state (one barrier), and decided lane-parallel; the first
          one that is accepted (or needs the exact delta) ends the batch: it is applied with the
          cursor it really consumed, and the proposals after it are re-batched. */
-      if (!(SR_EXP & 1)) {
+      {
         int vi = 0, vj = 0, vfl = 4, vkn = 0, vuw = 1, vnd = 0, voff = 0, vr0 = 0;   /* lane p: proposal p */
         int p0 = 0;
         while (p0 < 16) {
@@ -1687,10 +1671,9 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               pend = p + 1;
               return true;
           };
-          /* the swap (accepted ~44 %) is drawn first; with SR_SWAP_ALONE it forms its own batch,
-             otherwise proposals 1.. join its batch */
+          /* the swap (accepted ~44 %) is drawn first and forms its own batch */
           if (p0 == 0) (void)scalar_one(0);
-          if (p0 > 0 || (!SR_SWAP_ALONE && pend == 1)) {
+          if (p0 > 0) {
             /* Lane-parallel draws: lane l evaluates "a pi1 / pi2 / pi3 proposal starting at word
                offset o" for o = l and o = l + 64 (words o..o+4); the scan below then walks the
                batch's actual offsets reading those results.  ok = no GSL rejection and a nonzero
@@ -1698,7 +1681,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             uint32_t rA1[2] = {0u, 0u}, rA2[2] = {0u, 0u}, rA3[2] = {0u, 0u}, rB3[2] = {0u, 0u}, rU1[2] = {0u, 0u},
                      rU2[2] = {0u, 0u};
             /* the second 64 offsets only when the batch's proposals can reach them (<= 5 words each) */
-            const int nh2 = (SR_HALF_DRAWS && 5 * (16 - p0) + 5 <= 64) ? 1 : 2;
+            const int nh2 = (5 * (16 - p0) + 5 <= 64) ? 1 : 2;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
               if (h >= nh2) break;
@@ -1749,7 +1732,6 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               }
             }
             FST(15);
-#if SR_GATHER_SCAN
             /* scan, two steps.  (1) the offset chain: proposal p starts where p-1 ended; a 5-bit
                entry per offset (lane l: offset l in bits 0-15, l + 64 in bits 16-31) holds, per kind,
                whether the fast path applies there and how many words it consumes (pi1 2 / 3,
@@ -1805,42 +1787,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               }
             }
           }
-#else
-            /* scan: the batch's proposals at their actual offsets (all-rejected hypothesis) */
-#pragma unroll
-            for (int sI = 1; sI < 16; ++sI) {
-              if (sI < p0 || pend != sI || off + 5 > 128) continue;
-              const int kind = prop_kind(sI);
-              const int h = off >> 6, l = off & 63;
-              uint32_t ra, rb = 0, ru;
-              if (kind == PK_PI1) { ra = (uint32_t)__builtin_amdgcn_readlane((int)(h ? rA1[1] : rA1[0]), l);
-                                    ru = (uint32_t)__builtin_amdgcn_readlane((int)(h ? rU1[1] : rU1[0]), l); }
-              else if (kind == PK_PI2) { ra = (uint32_t)__builtin_amdgcn_readlane((int)(h ? rA2[1] : rA2[0]), l);
-                                         ru = (uint32_t)__builtin_amdgcn_readlane((int)(h ? rU2[1] : rU2[0]), l); }
-              else { ra = (uint32_t)__builtin_amdgcn_readlane((int)(h ? rA3[1] : rA3[0]), l);
-                     rb = (uint32_t)__builtin_amdgcn_readlane((int)(h ? rB3[1] : rB3[0]), l);
-                     ru = (uint32_t)__builtin_amdgcn_readlane((int)(h ? rU2[1] : rU2[0]), l); }
-              if (!(ra & (1u << 23))) continue;   /* rejection or zero word: scalar path */
-              const bool veto = (ra >> 22) & 1u;
-              const int i = (int)(ra & 2047u), j = (int)((ra >> 11) & 2047u);
-              const int inc = (int)((ra >> 24) & 3u);
-              const int nd = off + (kind == PK_PI1 ? 2 : (kind == PK_PI2 ? (veto ? 2 : 4) : 4));
-              const int ofa = nd + (veto ? 0 : 1);
-              vi = (lane == sI) ? i : vi;
-              vj = (lane == sI) ? j : vj;
-              vfl = (lane == sI) ? (inc | (veto ? 4 : 0)) : vfl;
-              vkn = (lane == sI) ? (int)(rb >> 16) : vkn;
-              vr0 = (lane == sI) ? (int)(rb & 0xffffu) : vr0;
-              vuw = (lane == sI) ? (int)ru : vuw;
-              vnd = (lane == sI) ? nd : vnd;
-              voff = (lane == sI) ? ofa : voff;
-              off = ofa;
-              pend = sI + 1;
-            }
-          }
-#endif
           for (int p = pend; p < 16; ++p) {   /* scalar path: the batch's first proposal after a fast-path stop */
-            if (p0 == 0 && p == 1) break;     /* the swap batch (SR_SWAP_ALONE) */
+            if (p0 == 0 && p == 1) break;     /* the swap batch */
             if (p > p0) break;                /* only the batch's first proposal goes scalar */
             if (!scalar_one(p)) break;
           }
@@ -1892,10 +1840,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               if (sI >= p0 && sI < pend && !(fl & 4)) {
                 const Prop q = load_prop(sI);
                 int dt0 = 0, dt1 = 0;
-                const int kx = prop_kind(sI);
-                const bool skip = ((SR_EXP & 4) && kx == PK_PI3) || ((SR_EXP & 8) && (kx == PK_PI2 || kx == PK_SWAP)) ||
-                                  ((SR_EXP & 16) && kx == PK_PI1);
-                if (tid < M && !skip) taxon_dt(prop_kind(sI), q, a1, b1, P + tid, pre + tid, M, hb1, hcnt, nhall, dt0, dt1);
+                if (tid < M) taxon_dt(prop_kind(sI), q, a1, b1, P + tid, pre + tid, M, hb1, hcnt, nhall, dt0, dt1);
                 d0s[sI] = dt0; d1s[sI] = dt1;
                 nzs[sI] = __popcll(__ballot((dt0 | dt1) != 0));
               }
@@ -1906,7 +1851,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               const int fl = __builtin_amdgcn_readlane(vfl, sI);
               if (sI >= p0 && sI < pend && !(fl & 4)) {
                 int X0, X1, Y0, Y1;
-                if (SR_PI1_BALLOT && prop_kind(sI) == PK_PI1) {   /* pi1: dt in {-1, 0, 1}: |dt| sums are ballot counts */
+                if (prop_kind(sI) == PK_PI1) {   /* pi1: dt in {-1, 0, 1}: |dt| sums are ballot counts */
                   const uint32_t u1 = (uint32_t)wave_sum_i32((int)((uint32_t)(d0s[sI] + 1) | ((uint32_t)(d1s[sI] + 1) << 16)));
                   X0 = (int)(u1 & 0xffffu) - 64; X1 = (int)(u1 >> 16) - 64;
                   Y0 = (int)__popcll(__ballot(d0s[sI] != 0)); Y1 = (int)__popcll(__ballot(d1s[sI] != 0));
@@ -2108,16 +2053,12 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 }
               }
             }
-#if SR_PRE_INCR
             {   /* the move permutes positions [lo, hi] only: prefix entries (lo/32, hi/32] change */
               const int lo = min(i, j), hi = max(i, j), rlo = (lo >> 5) + 1, rhi = hi >> 5;
               uint16_t *prem = pre + m;
               int sacc = prem[(rlo - 1) * M];
               for (int r = rlo; r <= rhi; ++r) { sacc += __popc(Pm[(r - 1) * M]); prem[r * M] = (uint16_t)sacc; }
             }
-#else
-            col_pre_build(pre + m, Pm, M, NW);   /* the column moved: refresh its prefix table */
-#endif
           }
           FST(7);
           /* rpi (double-buffered full permutation, read only at save time) and hard positions */

@@ -519,28 +519,69 @@ static int ck_parts(sr_state_host *st, ck_part *pt)
   return 9;
 }
 
+static int ck_write(const char *path, const sr_dataset *ds, const sr_chain_spec *specs, int32_t n, sr_state_host *st)
+{
+  FILE *f = fopen(path, "wb");
+  if (!f) return SR_EIO;
+  const uint32_t ver = 1;
+  const int32_t dims[4] = {ds->N, ds->M, ds->nh, n};
+  const uint64_t h = dataset_hash(ds);
+  int ok = fwrite("SRCK", 1, 4, f) == 4 && fwrite(&ver, 4, 1, f) == 1 && fwrite(dims, 4, 4, f) == 4 &&
+           fwrite(&h, 8, 1, f) == 1 && fwrite(specs, sizeof(sr_chain_spec), n, f) == (size_t)n;
+  ck_part pt[9];
+  const int np = ck_parts(st, pt);
+  for (int k = 0; k < np && ok; k++) ok = fwrite(pt[k].p, 1, pt[k].bytes, f) == pt[k].bytes;
+  if (fclose(f) != 0) ok = 0;
+  return ok ? SR_OK : SR_EIO;
+}
+
 SR_API int sr_session_checkpoint(sr_session *s, const char *path)
 {
   if (!s || !path) return SR_EINVAL;
   sr_state_host st;
   int rc = download(s, &st);
   if (rc) return rc;
-  FILE *f = fopen(path, "wb");
-  if (!f) { state_free(&st); return SR_EIO; }
-  const uint32_t ver = 1;
-  const int32_t dims[4] = {s->ds.N, s->ds.M, s->ds.nh, s->nchains};
-  const uint64_t h = dataset_hash(&s->ds);
-  int ok = fwrite("SRCK", 1, 4, f) == 4 && fwrite(&ver, 4, 1, f) == 1 && fwrite(dims, 4, 4, f) == 4 &&
-           fwrite(&h, 8, 1, f) == 1 && fwrite(s->specs, sizeof(sr_chain_spec), s->nchains, f) == (size_t)s->nchains;
-  ck_part pt[9];
-  const int np = ck_parts(&st, pt);
-  for (int k = 0; k < np && ok; k++) ok = fwrite(pt[k].p, 1, pt[k].bytes, f) == pt[k].bytes;
-  if (fclose(f) != 0) ok = 0;
+  rc = ck_write(path, &s->ds, s->specs, s->nchains, &st);
   state_free(&st);
-  return ok ? SR_OK : SR_EIO;
+  return rc;
 }
 
-typedef struct { FILE *f; } ck_reader;
+/* test hook: a checkpoint of freshly initialised chains (main()'s initial state), written on
+   the host without a device (restore validation tests) */
+SR_API int sr_host_initial_checkpoint(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n_chains, const char *path)
+{
+  if (!ds || !specs || n_chains <= 0 || !path || ds->nh > SR_NHMAX) return SR_EINVAL;
+  sr_state_host st;
+  int rc = state_alloc(&st, ds->N, ds->M, ds->nh, n_chains);
+  if (rc) return rc;
+  for (int c = 0; c < n_chains && rc == SR_OK; c++) rc = init_chain(ds, specs[c].seed, &st, c);
+  if (rc == SR_OK) rc = ck_write(path, ds, specs, n_chains, &st);
+  state_free(&st);
+  return rc;
+}
+
+typedef struct { FILE *f; const sr_dataset *ds; } ck_reader;
+
+static int check_chain(const sr_dataset *ds, const sr_state_host *st, int c);
+
+/* A restored state is uploaded into kernels that use hp and the RNG cursor as LDS indices and
+ * a, b, pi as positions: every chain must pass the mcmc_consistent port (limits, permutation,
+ * hard-site order, counts, loglik, P == X in position order), its hard positions must be the
+ * ascending positions of the hard sites, and its RNG cursor must lie inside the generated ring. */
+static int ck_validate(const sr_dataset *ds, const sr_state_host *st)
+{
+  const int N = ds->N, nh = ds->nh;
+  for (int c = 0; c < st->nchains; c++) {
+    if (check_chain(ds, st, c)) return SR_EPARSE;
+    const int32_t *hp = st->hp + (size_t)c * SR_NHMAX, *rpi = st->rpi + (size_t)c * N;
+    for (int k = 0; k < nh; k++)
+      if (hp[k] < 0 || hp[k] >= N || (k > 0 && hp[k] <= hp[k - 1]) || !ds->hard[rpi[hp[k]]]) return SR_EPARSE;
+    const uint64_t pos = st->rng[(size_t)c * 2 + 0], gen = st->rng[(size_t)c * 2 + 1];
+    const uint64_t blk = pos / SR_MT_N;
+    if (gen < 1 || blk > gen || gen - blk > SR_RING || gen > 0xffffffffULL) return SR_EPARSE;
+  }
+  return SR_OK;
+}
 
 static int ck_restore(void *ctx, sr_state_host *st)
 {
@@ -549,7 +590,8 @@ static int ck_restore(void *ctx, sr_state_host *st)
   const int np = ck_parts(st, pt);
   for (int k = 0; k < np; k++)
     if (fread(pt[k].p, 1, pt[k].bytes, r->f) != pt[k].bytes) return SR_EPARSE;
-  return fgetc(r->f) == EOF ? SR_OK : SR_EPARSE;
+  if (fgetc(r->f) != EOF) return SR_EPARSE;
+  return ck_validate(r->ds, st);
 }
 
 SR_API int sr_session_restore(const sr_dataset *ds, const char *path, const sr_run_opts *opts, sr_session **out)
@@ -573,7 +615,7 @@ SR_API int sr_session_restore(const sr_dataset *ds, const char *path, const sr_r
   else if (fread(specs, sizeof(sr_chain_spec), dims[3], f) != (size_t)dims[3])
     rc = SR_EPARSE;
   if (rc == SR_OK) {
-    ck_reader r = {f};
+    ck_reader r = {f, ds};
     rc = session_new(ds, specs, dims[3], opts, ck_restore, &r, out);
   }
   free(specs);

@@ -130,6 +130,7 @@ def _lib():
         "sr_host_exp_log": (None, [P(c_double), ctypes.c_long, P(c_double), P(c_double)]),
         "sr_host_run_add": (c_double, [c_double, c_double, ctypes.c_long]),
         "sr_host_run_sub": (ctypes.c_long, [P(c_double), c_double, ctypes.c_long]),
+        "sr_host_initial_checkpoint": (c_int, [P(sr_dataset), P(sr_chain_spec), c_i32, ctypes.c_char_p]),
         "sr_host_init_chain": (c_int, [P(sr_dataset), ctypes.c_uint64, P(c_i32), P(c_i32), P(c_i32),
                                        P(c_double), P(ctypes.c_uint64)]),
         "sr_session_debug_counters": (c_int, [c_void_p, P(ctypes.c_ulonglong)]),

@@ -105,3 +105,60 @@ def test_restore_rejects_bad_checkpoints(tmp_path):
     samedims = tmp_path / "hash.srck"
     samedims.write_bytes(b"SRCK" + struct.pack("<I4iQ", 1, ds.N, ds.M, ds.nh, 2, 12345))
     assert restore(samedims) == -1                                         # SR_EINVAL: dataset hash differs
+
+
+def test_restore_validates_chain_state(tmp_path):
+    """A checkpoint whose chain state is damaged (the file length still right) is refused with
+    SR_EPARSE before any upload: limits, permutation, counts, P == X, hard positions and the RNG
+    cursor are checked.  The undamaged file passes validation (SR_EDEVICE without a GPU)."""
+    import numpy as np
+    ds = sa.Dataset.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "datasets", "g10s10.txt"))
+    C = 2
+    specs = (L.sr_chain_spec * C)()
+    for k in range(C):
+        specs[k].seed = k + 1
+        specs[k].chain_id = k
+    good = tmp_path / "good.srck"
+    assert L.lib().sr_host_initial_checkpoint(ctypes.byref(ds.c), specs, C, os.fsencode(str(good))) == 0
+    opts = L.sr_run_opts()
+    L.lib().sr_default_opts(ctypes.byref(opts))
+
+    def restore(p):
+        h = ctypes.c_void_p()
+        rc = L.lib().sr_session_restore(ctypes.byref(ds.c), os.fsencode(str(p)), ctypes.byref(opts), ctypes.byref(h))
+        if rc == 0:
+            L.lib().sr_session_destroy(h)
+        return rc
+
+    assert restore(good) in (0, L.SR_EDEVICE)
+    N, M, nh, NW = ds.N, ds.M, ds.nh, (ds.N + 31) // 32
+    off = 32 + C * ctypes.sizeof(L.sr_chain_spec)
+    sizes = [("P", C * NW * M * 4), ("rpi", C * N * 4), ("hp", C * 32 * 4), ("ab", C * 2 * M * 4),
+             ("cnt", C * 4 * M * 4), ("cdl", C * 4 * 8), ("mt", C * 8 * 624 * 4), ("rng", C * 2 * 8), ("acc", C * 8 * 8)]
+    base = {}
+    for name, n in sizes:
+        base[name] = off
+        off += n
+    raw = good.read_bytes()
+    assert len(raw) == off
+
+    def damaged(name, word, value, dtype="<i4"):
+        b = bytearray(raw)
+        itemsize = np.dtype(dtype).itemsize
+        b[base[name] + word * itemsize: base[name] + (word + 1) * itemsize] = np.array([value], dtype=dtype).tobytes()
+        p = tmp_path / ("bad_%s_%d.srck" % (name, word))
+        p.write_bytes(bytes(b))
+        return p
+
+    P0 = int(np.frombuffer(raw, "<u4", 1, base["P"])[0])
+    assert restore(damaged("P", 0, P0 ^ 1, "<u4")) == -2                   # a column bit differs from X
+    assert restore(damaged("rpi", 1, 0)) == -2                             # not a permutation
+    assert restore(damaged("ab", 0, N + 5)) == -2                          # a limit outside [0, N]
+    assert restore(damaged("cnt", 0, 10 ** 6)) == -2                       # counts disagree with X
+    cdl = np.frombuffer(raw, "<f8", 4, base["cdl"]).copy()
+    assert restore(damaged("cdl", 2, cdl[2] + 1.0, "<f8")) == -2           # loglik disagrees
+    assert restore(damaged("rng", 1, 0, "<u8")) == -2                      # no generated block
+    pos = int(np.frombuffer(raw, "<u8", 1, base["rng"])[0])
+    assert restore(damaged("rng", 0, pos + 624 * 20, "<u8")) == -2         # cursor beyond the ring
+    if nh:
+        assert restore(damaged("hp", 0, N + 3)) == -2                      # hard position out of range

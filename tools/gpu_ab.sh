@@ -1,6 +1,6 @@
 #!/bin/bash
-# A/B timing of the default library against build/var/<name> variants (parity tests on the default first).
-#   tools/gpu_ab.sh OUTNAME var1 var2 ...
+# A/B timing of the default library against build/var/<name> variants on the same box, runs
+# interleaved (parity subset on the default first).   tools/gpu_ab.sh OUTNAME var1 var2 ...
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
@@ -9,7 +9,7 @@ mkdir -p "$OUT"
 V=seriation-in-paleontological-data-using-mcmc_amd/build/var
 timeout -k 10 300 python -m pytest tests/test_gpu_parity.py tests/test_gpu_edge.py -x -q > "$OUT/parity.log" 2>&1 || { tail -20 "$OUT/parity.log"; exit 1; }
 tail -1 "$OUT/parity.log"
-for rep in 1 2; do
+for rep in 1 2 3; do
   timeout -k 10 100 python bench.py --no-cpu-baseline --steps 20 > "$OUT/base_$rep.json" 2>/dev/null || exit 1
   for v in "$@"; do
     SERIATION_LIB=$V/$v/libseriation.so timeout -k 10 100 python bench.py --no-cpu-baseline --steps 20 > "$OUT/${v}_$rep.json" 2>/dev/null || exit 1
@@ -17,6 +17,3 @@ for rep in 1 2; do
 done
 for f in "$OUT"/*.json; do python3 -c "
 import json,sys;b=json.load(open('$f'));print('%-40s %10.0f  kernel %.3f ms' % ('$f'.split('/')[-1], b['value'], b['roofline']['kernel_ms']))"; done
-if [ -n "$SR_AB_FINE" ]; then
-  SR_FINE=1 SERIATION_LIB=$V/fine/libseriation.so timeout -k 10 120 python tools/stamp_profile.py > "$OUT/stamps.log" 2>&1 && cat "$OUT/stamps.log"
-fi

@@ -120,6 +120,10 @@ int sr_session_state(sr_session *s, int32_t chain, int32_t *a, int32_t *b, int32
                      double *c_d_loglik, int32_t *counts);
 /* Acceptance counters cc, cd, cab, cpi1, cpi20, cpi21, cpi3 (mcmc.c:220). */
 int sr_session_accept_counts(sr_session *s, int32_t chain, int64_t *acc7);
+/* How often the fast paths fell back to the reference's own computation (no counterpart in
+   mcmc.c; every fallback is bit-exact): fb3 = {proposals decided by the exact sequential delta,
+   Gibbs draws by the exact three-pass walk, c/d draws by the sequential GSL path}. */
+int sr_session_fallback_counts(sr_session *s, int32_t chain, int64_t *fb3);
 /* Device time of the last sr_session_run (ms, HIP events on the session stream; syncs). */
 double sr_session_last_kernel_ms(sr_session *s);
 int32_t sr_session_block_threads(const sr_session *s);

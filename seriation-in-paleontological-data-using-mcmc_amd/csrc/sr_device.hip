@@ -124,6 +124,7 @@ __host__ __device__ static inline size_t sr_gm_cbuf(int M) { return (size_t)2 * 
 #define MS_FBK 14   /* +1 prev fail, +2 here fail, +3 S==0 (slots 15,16,17) */
 #define MS_RCUR 18
 #define MS_ACC 24   /* 7 acceptance counters (thread 0) */
+#define MS_CDSEQ 44 /* c/d draws by the sequential GSL path */
 
 /* ---------------------------------------------------------------- sync */
 template <bool WAVE>
@@ -434,6 +435,9 @@ __device__ __forceinline__ double readlane_f64(double v, int l)
 __device__ __forceinline__ bool draw_cd_fast(DRng &r, double &c, double &d, int f1, int t0, int f0, int t1,
                                              const sr_mtab &tb, int lane)
 {
+#ifdef SR_FORCE_EXACT   /* test build: the sequential GSL draws */
+  return false;
+#endif
   if (r.blk + (r.off + 7) / SR_MT_N >= r.gen) return false;
   const uint32_t base = (r.blk & (SR_RING - 1)) * SR_MT_N + r.off;
   const int g = lane & 3;
@@ -785,14 +789,18 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
     const double eprev = 2.0 * REL * fmin(Pp, S - Pp) * inv + ABS;
     const bool prev_ok = (w == 0) || (tprev > eprev);
     const bool here_ok = (w == L) || (t < -e);
+#ifndef SR_FORCE_EXACT
     if (prev_ok && here_ok) res = w;
+#else   /* test build: every Gibbs draw takes the exact three-pass walk */
+    (void)prev_ok; (void)here_ok; (void)w;
+#endif
 #ifdef SR_STAMPS
     else atomicAdd((unsigned long long *)fbk + (prev_ok ? 2 : 1), 1ull);
 #endif
   }
   if (res < 0) {
+    atomicAdd((unsigned long long *)fbk, 1ull);   /* exact-walk fallbacks (rare: counted always) */
 #ifdef SR_STAMPS
-    atomicAdd((unsigned long long *)fbk, 1ull);
     if (!(S > 0.0)) atomicAdd((unsigned long long *)fbk + 3, 1ull);
 #endif
     return draw_exact(Pm, M, N, rev, o, L, u, K, tb, dt0, df0, dt1, df1);
@@ -988,12 +996,14 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
     const double eprev = 2.0 * REL * fmin(Pp, S - Pp) * inv + ABS;
     const bool prev_ok = (w == 0) || (tprev > eprev);
     const bool here_ok = (w == L) || (t < -e);
+#ifndef SR_FORCE_EXACT
     if (prev_ok && here_ok) res = w;
+#else   /* test build: every Gibbs draw takes the exact three-pass walk */
+    (void)prev_ok; (void)here_ok; (void)w;
+#endif
   }
   if (res < 0) {
-#ifdef SR_STAMPS
-    atomicAdd((unsigned long long *)fbk, 1ull);
-#endif
+    atomicAdd((unsigned long long *)fbk, 1ull);   /* exact-walk fallbacks (rare: counted always) */
     return draw_exact(Pm, M, N, rev, o, L, u, K, tb, dt0, df0, dt1, df1);
   }
   const int POp = walk_prefix_s<NWM>(wk, res);
@@ -1439,6 +1449,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         }
         /* mcmc_samplec then mcmc_sampled: Beta(1 + f1, 1 + t0), Beta(1 + f0, 1 + t1) */
         if (!draw_cd_fast(R, c, d, s3, s0, s1, s2, tb, lane)) {
+          if (tid == 0) misc[MS_CDSEQ]++;
           double cd2[2] = {c, d};
           for (int k = 0; k < 2; ++k)
             cd2[k] = d_samplebeta<false>(R, cd2[k], (double)(k ? s1 : s3), (double)(k ? s2 : s0), k ? SR_MIND : SR_MINC,
@@ -1924,6 +1935,10 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 const double B = (double)Y0 * aC + (double)Y1 * aD;
                 Ebp = ((double)Knz + 16.0) * 0x1p-52 * B;
                 uwp = (uint32_t)vuw;
+#ifdef SR_FORCE_EXACT   /* test build: every decision by the exact sequential delta */
+                if (Knz == 0) cls = 1; else cls = 2;
+                Ebp = __builtin_inf();
+#else
                 if (Knz == 0 || Sp > Ebp) cls = 1;
                 else if (Sp < -Ebp) {
                   const float uf = (float)((double)uwp / 4294967296.0);
@@ -1931,6 +1946,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                   const double dl = 0x1p-16 * (1.0 + __builtin_fabs(lua));
                   cls = (Sp - Ebp > lua + dl) ? 1 : ((Sp + Ebp < lua - dl) ? 0 : 2);
                 } else cls = 2;
+#endif
               }
             }
           }
@@ -2159,9 +2175,11 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
     A.cdl[(size_t)chain * 4 + 2] = loglik;
     A.rng[(size_t)chain * 2 + 0] = (uint64_t)R.blk * SR_MT_N + R.off;
     A.rng[(size_t)chain * 2 + 1] = R.gen;
-    for (int k = 0; k < 7; ++k) A.acc[(size_t)chain * 8 + k] += misc[MS_ACC + k];
-    A.acc[(size_t)chain * 8 + 2] += misc[MS_CAB];
-    A.acc[(size_t)chain * 8 + 7] += misc[MS_NEXACT];
+    for (int k = 0; k < 7; ++k) A.acc[(size_t)chain * SR_NACC + k] += misc[MS_ACC + k];
+    A.acc[(size_t)chain * SR_NACC + 2] += misc[MS_CAB];
+    A.acc[(size_t)chain * SR_NACC + 7] += misc[MS_NEXACT];
+    A.acc[(size_t)chain * SR_NACC + 8] += misc[MS_FBK];
+    A.acc[(size_t)chain * SR_NACC + 9] += misc[MS_CDSEQ];
   }
 }
 
@@ -2255,7 +2273,7 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
   rc |= dev_alloc_copy(d, &A.cdl, st->cdl, C * 4);
   rc |= dev_alloc_copy(d, &A.mt, st->mt, C * SR_RING * SR_MT_N);
   rc |= dev_alloc_copy(d, &A.rng, st->rng, C * 2);
-  rc |= dev_alloc_copy(d, &A.acc, st->acc, C * 8);
+  rc |= dev_alloc_copy(d, &A.acc, st->acc, C * SR_NACC);
   rc |= dev_alloc_copy(d, &A.rec_abpi, (const int16_t *)nullptr, C * d->rec_cap * (2 * st->M + st->N));
   rc |= dev_alloc_copy(d, &A.rec_cdl, (const double *)nullptr, C * d->rec_cap * 3);
   rc |= dev_alloc_copy(d, &A.dbg, (const unsigned long long *)nullptr, C * 17 * 8);
@@ -2436,7 +2454,7 @@ extern "C" int srk_download_state(srk_dev *d, sr_state_host *st)
   if (st->cdl) HIPCHK(hipMemcpy(st->cdl, A.cdl, C * 4 * 8, hipMemcpyDeviceToHost));
   if (st->mt) HIPCHK(hipMemcpy(st->mt, A.mt, C * SR_RING * SR_MT_N * 4, hipMemcpyDeviceToHost));
   if (st->rng) HIPCHK(hipMemcpy(st->rng, A.rng, C * 2 * 8, hipMemcpyDeviceToHost));
-  if (st->acc) HIPCHK(hipMemcpy(st->acc, A.acc, C * 8 * 8, hipMemcpyDeviceToHost));
+  if (st->acc) HIPCHK(hipMemcpy(st->acc, A.acc, C * SR_NACC * 8, hipMemcpyDeviceToHost));
   return 0;
 }
 

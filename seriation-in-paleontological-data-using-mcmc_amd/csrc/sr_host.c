@@ -346,7 +346,7 @@ static int state_alloc(sr_state_host *st, int N, int M, int nh, int C)
   st->cdl = (double *)calloc((size_t)C * 4, 8);
   st->mt = (uint32_t *)calloc((size_t)C * SR_RING * SR_MT_N, 4);
   st->rng = (uint64_t *)calloc((size_t)C * 2, 8);
-  st->acc = (uint64_t *)calloc((size_t)C * 8, 8);
+  st->acc = (uint64_t *)calloc((size_t)C * SR_NACC, 8);
   if (!st->P || !st->rpi || !st->hp || !st->ab || !st->cnt || !st->cdl || !st->mt || !st->rng || !st->acc) {
     state_free(st);
     return SR_ENOMEM;
@@ -494,7 +494,7 @@ static int download(sr_session *s, sr_state_host *st)
 }
 
 /* ---- checkpoint / resume (the reference restarts every run; optional here) ----
- * File: "SRCK" | u32 version 1 | i32 N, M, nh, nchains | u64 FNV-1a of the dataset (X, hard) |
+ * File: "SRCK" | u32 version 2 | i32 N, M, nh, nchains | u64 FNV-1a of the dataset (X, hard) |
  * sr_chain_spec[nchains] | the device state as sr_state_host arrays (P, rpi, hp, ab, cnt, cdl, mt,
  * rng, acc), little-endian.  Restoring uploads the same words, so the continued chains are the
  * ones an uninterrupted session produces (tests/test_gpu_edge.py). */
@@ -507,6 +507,7 @@ static uint64_t dataset_hash(const sr_dataset *ds)
 }
 
 typedef struct { size_t bytes; void *p; } ck_part;
+#define SR_CK_VERSION 2   /* 2: SR_NACC counters per chain */
 
 static int ck_parts(sr_state_host *st, ck_part *pt)
 {
@@ -514,7 +515,7 @@ static int ck_parts(sr_state_host *st, ck_part *pt)
   ck_part q[9] = {
     {C * st->NW * st->M * 4, st->P}, {C * st->N * 4, st->rpi}, {C * SR_NHMAX * 4, st->hp},
     {C * 2 * st->M * 4, st->ab}, {C * 4 * st->M * 4, st->cnt}, {C * 4 * 8, st->cdl},
-    {C * SR_RING * SR_MT_N * 4, st->mt}, {C * 2 * 8, st->rng}, {C * 8 * 8, st->acc}};
+    {C * SR_RING * SR_MT_N * 4, st->mt}, {C * 2 * 8, st->rng}, {C * SR_NACC * 8, st->acc}};
   memcpy(pt, q, sizeof q);
   return 9;
 }
@@ -523,7 +524,7 @@ static int ck_write(const char *path, const sr_dataset *ds, const sr_chain_spec 
 {
   FILE *f = fopen(path, "wb");
   if (!f) return SR_EIO;
-  const uint32_t ver = 1;
+  const uint32_t ver = SR_CK_VERSION;
   const int32_t dims[4] = {ds->N, ds->M, ds->nh, n};
   const uint64_t h = dataset_hash(ds);
   int ok = fwrite("SRCK", 1, 4, f) == 4 && fwrite(&ver, 4, 1, f) == 1 && fwrite(dims, 4, 4, f) == 4 &&
@@ -605,7 +606,7 @@ SR_API int sr_session_restore(const sr_dataset *ds, const char *path, const sr_r
   uint64_t h = 0;
   int rc = SR_OK;
   sr_chain_spec *specs = NULL;
-  if (fread(magic, 1, 4, f) != 4 || memcmp(magic, "SRCK", 4) != 0 || fread(&ver, 4, 1, f) != 1 || ver != 1 ||
+  if (fread(magic, 1, 4, f) != 4 || memcmp(magic, "SRCK", 4) != 0 || fread(&ver, 4, 1, f) != 1 || ver != SR_CK_VERSION ||
       fread(dims, 4, 4, f) != 4 || fread(&h, 8, 1, f) != 1 || dims[3] <= 0)
     rc = SR_EPARSE;
   else if (dims[0] != ds->N || dims[1] != ds->M || dims[2] != ds->nh || h != dataset_hash(ds))
@@ -646,7 +647,18 @@ SR_API int sr_session_accept_counts(sr_session *s, int32_t chain, int64_t *acc7)
   sr_state_host st;
   int rc = download(s, &st);
   if (rc) return rc;
-  for (int k = 0; k < 7; k++) acc7[k] = (int64_t)st.acc[(size_t)chain * 8 + k];
+  for (int k = 0; k < 7; k++) acc7[k] = (int64_t)st.acc[(size_t)chain * SR_NACC + k];
+  state_free(&st);
+  return SR_OK;
+}
+
+SR_API int sr_session_fallback_counts(sr_session *s, int32_t chain, int64_t *fb3)
+{
+  if (!s || chain < 0 || chain >= s->nchains || !fb3) return SR_EINVAL;
+  sr_state_host st;
+  int rc = download(s, &st);
+  if (rc) return rc;
+  for (int k = 0; k < 3; k++) fb3[k] = (int64_t)st.acc[(size_t)chain * SR_NACC + 7 + k];
   state_free(&st);
   return SR_OK;
 }

@@ -19,6 +19,11 @@
  *   cnt [4][M]  i32  t0, f0, t1, f1 (mcmc.h:42)
  *   cdl [4]     f64  c, d, loglik, unused
  *   mt  [RING][624] u32, rng [2] u64 (pos, gen), acc [8] u64                       */
+/* per-chain counters: [0..6] acceptances cc, cd, cab, cpi1, cpi20, cpi21, cpi3 (mcmc.c:220),
+ * [7] proposals decided by the exact sequential delta, [8] Gibbs draws taken by the exact
+ * three-pass walk, [9] c/d draws taken by the sequential GSL path (the fast paths' fallbacks) */
+#define SR_NACC 10
+
 typedef struct {
   int N, M, NW, nh, nchains;
   uint32_t *P;

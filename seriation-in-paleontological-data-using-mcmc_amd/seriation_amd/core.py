@@ -202,6 +202,14 @@ class Session:
                "accept_counts")
         return acc
 
+    def fallback_counts(self, chain):
+        """sr_session_fallback_counts: {exact sequential deltas, exact Gibbs walks, sequential c/d
+        draws} taken by `chain` so far."""
+        fb = np.zeros(3, np.int64)
+        _check(L.lib().sr_session_fallback_counts(self.h, chain, fb.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))),
+               "fallback_counts")
+        return fb
+
     def close(self):
         if self.h:
             L.lib().sr_session_destroy(self.h)

@@ -100,10 +100,10 @@ def test_restore_rejects_bad_checkpoints(tmp_path):
     bad.write_bytes(b"XXXX" + bytes(40))
     assert restore(bad) == -2                                              # SR_EPARSE
     other = tmp_path / "other.srck"
-    other.write_bytes(b"SRCK" + struct.pack("<I4iQ", 1, ds.N + 1, ds.M, 0, 2, 0))
+    other.write_bytes(b"SRCK" + struct.pack("<I4iQ", 2, ds.N + 1, ds.M, 0, 2, 0))
     assert restore(other) == -1                                            # SR_EINVAL: other dataset
     samedims = tmp_path / "hash.srck"
-    samedims.write_bytes(b"SRCK" + struct.pack("<I4iQ", 1, ds.N, ds.M, ds.nh, 2, 12345))
+    samedims.write_bytes(b"SRCK" + struct.pack("<I4iQ", 2, ds.N, ds.M, ds.nh, 2, 12345))
     assert restore(samedims) == -1                                         # SR_EINVAL: dataset hash differs
 
 
@@ -134,7 +134,7 @@ def test_restore_validates_chain_state(tmp_path):
     N, M, nh, NW = ds.N, ds.M, ds.nh, (ds.N + 31) // 32
     off = 32 + C * ctypes.sizeof(L.sr_chain_spec)
     sizes = [("P", C * NW * M * 4), ("rpi", C * N * 4), ("hp", C * 32 * 4), ("ab", C * 2 * M * 4),
-             ("cnt", C * 4 * M * 4), ("cdl", C * 4 * 8), ("mt", C * 8 * 624 * 4), ("rng", C * 2 * 8), ("acc", C * 8 * 8)]
+             ("cnt", C * 4 * M * 4), ("cdl", C * 4 * 8), ("mt", C * 8 * 624 * 4), ("rng", C * 2 * 8), ("acc", C * 10 * 8)]
     base = {}
     for name, n in sizes:
         base[name] = off

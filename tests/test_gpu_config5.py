@@ -30,12 +30,20 @@ def test_config5_variant_is_hbm(config5):
 
 
 def test_config5_parity(config5):
+    """8 chains x (1 burn-in + 20 saved calls) against the oracle, bit for bit."""
+    from concurrent.futures import ThreadPoolExecutor
     ds = sa.Dataset.parse(config5, maxs=0)
-    seeds = [1, 2]
-    summ, (ri, rd) = sa.run_chains(ds, seeds, burnin_calls=1, sample_calls=2, keep_records=True)
-    for k, s in enumerate(seeds):
-        o = oracle_ref.run_chain(config5, s, 1, 2, maxs=0)
-        assert o["rc"] == 0
-        np.testing.assert_array_equal(ri[k], o["rec_int"], err_msg="seed %d" % s)
-        assert np.array_equal(rd[k].view(np.uint64), o["rec_dbl"].view(np.uint64)), s
+    seeds = [1, 2, 3, 4, 5, 6, 7, 8]
+    summ, (ri, rd) = sa.run_chains(ds, seeds, burnin_calls=1, sample_calls=20, keep_records=True)
+
+    def one(s):
+        o = oracle_ref.run_chain(config5, s, 1, 20, maxs=0)
+        return o["rc"], o["rec_int"].copy(), o["rec_dbl"].copy()
+
+    with ThreadPoolExecutor(8) as ex:
+        ref = list(ex.map(one, seeds))
+    for k, (s, (rc, oi, od)) in enumerate(zip(seeds, ref)):
+        assert rc == 0
+        np.testing.assert_array_equal(ri[k], oi, err_msg="seed %d" % s)
+        assert np.array_equal(rd[k].view(np.uint64), od.view(np.uint64)), s
         assert summ[k]["consistent"] == 0

@@ -85,3 +85,30 @@ def test_parity_g2s2():
 
 def test_parity_synth_256x512():
     _compare_chains("synth_256x512.txt", [1, 2], tb=1, ts=3)
+
+
+def test_parity_config3_100_chains_200_calls():
+    """BASELINE config 3's workload (synthetic 256x512, 100 chains) for 200 saved calls (2000
+    sweeps) per chain: every saved sample of every chain against the oracle (run on 16 threads)."""
+    import hashlib
+    from concurrent.futures import ThreadPoolExecutor
+    text = _text("synth_256x512.txt")
+    ds = sa.Dataset.parse(text, maxs=0)
+    seeds = list(range(1, 101))
+    summ, (ri, rd) = sa.run_chains(ds, seeds, burnin_calls=0, sample_calls=200, keep_records=True)
+
+    def one(s):
+        o = oracle_ref.run_chain(text, s, 0, 200, maxs=0)
+        return (o["rc"], hashlib.sha256(np.ascontiguousarray(o["rec_int"], "<i4").tobytes()).hexdigest(),
+                o["rec_dbl"].copy())
+
+    with ThreadPoolExecutor(min(16, os.cpu_count() or 1)) as ex:
+        ref = list(ex.map(one, seeds))
+    bad = []
+    for k, (rc, dig, od) in enumerate(ref):
+        assert rc == 0
+        if hashlib.sha256(np.ascontiguousarray(ri[k], "<i4").tobytes()).hexdigest() != dig or \
+                not np.array_equal(rd[k].view(np.uint64), od.view(np.uint64)):
+            bad.append(k)
+        assert summ[k]["consistent"] == 0
+    assert not bad, "chains differing from the oracle: %s" % bad

@@ -70,6 +70,9 @@ typedef struct {
 #define SR_F_NO_CHECK 1      /* skip the closing mcmc_consistent check */
 #define SR_F_HBM_COLUMNS 2   /* force the HBM-column kernel variant (default: only when LDS is too small) */
 #define SR_F_LDS_COLUMNS 4   /* force the LDS-column variant (SR_EUNSUPPORTED if it does not fit) */
+#define SR_F_DEBUG_CHECK 8   /* the reference's MCMCDEBUG (mcmc.c:249-255): mcmc_consistent on every chain after
+                                every mcmc_sample call (one call per launch); SR_EINCONSISTENT on the first failure */
+#define SR_F_DEBUG_PRINT 16  /* with SR_F_DEBUG_CHECK: MCMCDEBUG's acceptance-rate line on stderr per chain and call */
 
 typedef struct {
   int32_t chain_id;
@@ -99,6 +102,18 @@ int sr_run_chains(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n_ch
  * under chains_root byte-for-byte as the reference's main() does. */
 int sr_run_to_dirs(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n_chains,
                    const sr_run_opts *opts, const char *chains_root, sr_chain_summary *out);
+
+/* Several GPUs from one call (the reference runs one process per chain, script.py:55-62):
+ * chains sharded contiguously over n_devices shards, shard k on HIP device devices[k] (an ordinal may
+ * repeat: those shards share the GPU), one host thread per shard.  Every output equals the
+ * sr_run_chains / sr_run_to_dirs one; the sink is serialised and receives global chain indices
+ * (samples in order per chain, chains of different shards interleaved).  opts->device is ignored. */
+int sr_run_chains_multi(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n_chains,
+                        const sr_run_opts *opts, const int32_t *devices, int32_t n_devices,
+                        sr_sample_sink_fn sink, void *sink_ctx, sr_chain_summary *out);
+int sr_run_to_dirs_multi(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n_chains,
+                         const sr_run_opts *opts, const int32_t *devices, int32_t n_devices,
+                         const char *chains_root, sr_chain_summary *out);
 
 /* ---- sessions: chains resident in HBM on one GPU, asynchronous launches ---- */
 typedef struct sr_session sr_session;

@@ -325,6 +325,7 @@ struct sr_session {
   sr_run_opts opts;
   srk_dev *dev;
   int rec_cap, nrec;
+  long debug_calls;         /* mcmc_sample calls checked by SR_F_DEBUG_CHECK */
 };
 
 static void state_free(sr_state_host *st)
@@ -455,13 +456,43 @@ SR_API int sr_session_set_stream(sr_session *s, void *hip_stream)
   return srk_set_stream(s->dev, hip_stream) ? SR_EDEVICE : SR_OK;
 }
 
+static int download(sr_session *s, sr_state_host *st);
+static int check_chain(const sr_dataset *ds, const sr_state_host *st, int c);
+
+/* SR_F_DEBUG_CHECK after one mcmc_sample call of every chain: the reference's MCMCDEBUG block
+ * (mcmc.c:249-255) -- the running acceptance rates on stderr (cumulative counters, as its static
+ * ones; one line per chain in chain order) and mcmc_consistent on the downloaded state. */
+static int debug_check(sr_session *s)
+{
+  sr_state_host st;
+  int rc = download(s, &st);
+  if (rc) return rc;
+  s->debug_calls++;
+  const double n = (double)s->debug_calls, M = (double)s->ds.M;
+  for (int c = 0; c < s->nchains && rc == SR_OK; c++) {
+    const uint64_t *a = st.acc + (size_t)c * SR_NACC;
+    if (s->opts.flags & SR_F_DEBUG_PRINT)
+      fprintf(stderr, "mcmc_sample: %f %f %f %f %f %f %f\n", a[0] / (10. * n), a[1] / (10. * n), a[2] / (20. * n * M),
+              a[3] / (10. * 5 * n), a[4] / (10. * 5 * n), a[5] / (10. * 5 * n), a[6] / (10. * 5 * n));
+    if (check_chain(&s->ds, &st, c)) rc = SR_EINCONSISTENT;
+  }
+  state_free(&st);
+  return rc;
+}
+
 SR_API int sr_session_run(sr_session *s, int32_t calls, int32_t save)
 {
   if (!s || calls < 0) return SR_EINVAL;
   if (save && s->nrec + calls > s->rec_cap) return SR_EINVAL;
-  int rc = srk_run(s->dev, calls, s->opts.sweeps_per_call, save ? 1 : 0, s->nrec);
-  if (rc) return rc == -1 ? SR_EINVAL : SR_EDEVICE;
-  if (save) s->nrec += calls;
+  const int dbg = (s->opts.flags & SR_F_DEBUG_CHECK) != 0;
+  for (int done = 0; done < calls;) {   /* debug: one call per launch, each followed by the check */
+    const int k = dbg ? 1 : calls;
+    int rc = srk_run(s->dev, k, s->opts.sweeps_per_call, save ? 1 : 0, s->nrec);
+    if (rc) return rc == -1 ? SR_EINVAL : SR_EDEVICE;
+    if (save) s->nrec += k;
+    done += k;
+    if (dbg && (rc = debug_check(s))) return rc;
+  }
   return SR_OK;
 }
 
@@ -928,9 +959,24 @@ static int run_common(const sr_dataset *ds, const sr_chain_spec *specs, int32_t 
   r.sums = (sr_sums *)calloc(n, sizeof(sr_sums));
   r.ra = (int32_t *)malloc((size_t)W * 4);
   if (!r.sums || !r.ra) { free(r.sums); free(r.ra); rc = SR_ENOMEM; goto fail; }
+  if (o.flags & SR_F_DEBUG_CHECK) {   /* checked call by call (sr_session_run), records consumed per call */
+    const size_t W2 = (size_t)W;
+    int16_t *ab = (int16_t *)malloc(W2 * n * sizeof(int16_t));
+    double *cd = (double *)malloc((size_t)3 * n * sizeof(double));
+    rc = (ab && cd) ? SR_OK : SR_ENOMEM;
+    for (int t = 0; t < o.sample_calls && rc == SR_OK; t++) {
+      sr_session_reset_records(s);
+      if ((rc = sr_session_run(s, 1, 1))) break;
+      if ((rc = sr_session_fetch_records(s, 0, 1, ab, cd))) break;
+      if (consume_batch(&r, t, 1, ab, cd)) rc = dir ? SR_EIO : SR_EINVAL;
+    }
+    free(ab); free(cd); free(r.ra);
+    if (rc) { free(r.sums); goto fail; }
+  } else {
   rc = srk_run_pipelined(s->dev, o.sample_calls, cpl, o.sweeps_per_call, consume_batch, &r);
   free(r.ra);
   if (rc) { free(r.sums); rc = (rc == -1) ? (dir ? SR_EIO : SR_EINVAL) : SR_EDEVICE; goto fail; }
+  }
   sr_state_host st;
   rc = download(s, &st);
   if (rc) { free(r.sums); goto fail; }
@@ -954,11 +1000,106 @@ fail:
   return rc;
 }
 
+/* ---- several devices from one call: chains sharded contiguously, one host thread per shard ----
+ * Shard k (of nd) owns chains [k n / nd, (k + 1) n / nd) and runs run_common on devices[k]; a chain's
+ * trajectory depends only on (dataset, seed), so every output equals the single-device run.  The
+ * caller's sink is called under a mutex with the global chain index; final states are merged. */
+typedef struct {
+  const sr_dataset *ds;
+  const sr_chain_spec *specs;
+  int n, off, rc;
+  sr_run_opts o;
+  sr_sample_sink_fn sink;
+  void *ctx;
+  pthread_mutex_t *mu;
+  dir_ctx dir;
+  int have_dir;
+  sr_chain_summary *out;
+  sr_state_host st;
+  int want_state;
+} shard_arg;
+
+static int shard_sink(void *ctx, int32_t ci, int32_t si, const sr_record *rec)
+{
+  shard_arg *a = (shard_arg *)ctx;
+  pthread_mutex_lock(a->mu);
+  const int rc = a->sink(a->ctx, a->off + ci, si, rec);
+  pthread_mutex_unlock(a->mu);
+  return rc;
+}
+
+static void *shard_main(void *va)
+{
+  shard_arg *a = (shard_arg *)va;
+  a->rc = run_common(a->ds, a->specs, a->n, &a->o, a->sink ? shard_sink : NULL, a, a->have_dir ? &a->dir : NULL,
+                     a->out, a->want_state ? &a->st : NULL);
+  return NULL;
+}
+
+static int run_multi(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n, const sr_run_opts *opts,
+                     const int32_t *devices, int32_t nd, sr_sample_sink_fn sink, void *ctx, dir_ctx *dir,
+                     sr_chain_summary *out, sr_state_host *final_state)
+{
+  if (nd <= 0 || nd > n || !devices) return SR_EINVAL;
+  sr_run_opts o;
+  if (opts) o = *opts; else sr_default_opts(&o);
+  if (nd == 1) { o.device = devices[0]; return run_common(ds, specs, n, &o, sink, ctx, dir, out, final_state); }
+  shard_arg *sa = (shard_arg *)calloc(nd, sizeof(shard_arg));
+  pthread_t *th = (pthread_t *)calloc(nd, sizeof(pthread_t));
+  int *started = (int *)calloc(nd, sizeof(int));
+  if (!sa || !th || !started) { free(sa); free(th); free(started); return SR_ENOMEM; }
+  pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
+  int rc = SR_OK;
+  for (int k = 0; k < nd; k++) {
+    shard_arg *a = &sa[k];
+    a->off = (int)((long)k * n / nd);
+    a->n = (int)((long)(k + 1) * n / nd) - a->off;
+    a->ds = ds; a->specs = specs + a->off; a->o = o; a->o.device = devices[k];
+    a->sink = sink; a->ctx = ctx; a->mu = &mu;
+    if (dir) { a->dir.f = dir->f + a->off; a->dir.M = dir->M; a->have_dir = 1; }
+    a->out = out ? out + a->off : NULL;
+    a->want_state = final_state != NULL;
+    a->rc = SR_EDEVICE;
+    if (pthread_create(&th[k], NULL, shard_main, a) != 0) { rc = SR_ENOMEM; break; }
+    started[k] = 1;
+  }
+  for (int k = 0; k < nd; k++) if (started[k]) pthread_join(th[k], NULL);
+  /* the first hard error wins; SR_EINCONSISTENT (every shard finished its run) only if none */
+  for (int k = 0; k < nd && rc == SR_OK; k++) if (sa[k].rc && sa[k].rc != SR_EINCONSISTENT) rc = sa[k].rc;
+  for (int k = 0; k < nd && rc == SR_OK; k++) if (sa[k].rc) rc = sa[k].rc;
+  if (final_state && (rc == SR_OK || rc == SR_EINCONSISTENT)) {
+    int r2 = state_alloc(final_state, ds->N, ds->M, ds->nh, n);
+    if (r2) rc = r2;
+    else {
+      ck_part dst[9], src[9];
+      const int np = ck_parts(final_state, dst);
+      for (int k = 0; k < nd; k++) {
+        ck_parts(&sa[k].st, src);
+        for (int q = 0; q < np; q++) {
+          const size_t per = dst[q].bytes / (size_t)n;
+          memcpy((char *)dst[q].p + per * sa[k].off, src[q].p, per * sa[k].n);
+        }
+      }
+    }
+  }
+  for (int k = 0; k < nd; k++) if (sa[k].want_state) state_free(&sa[k].st);
+  free(sa); free(th); free(started);
+  return rc;
+}
+
 SR_API int sr_run_chains(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n_chains, const sr_run_opts *opts,
                          sr_sample_sink_fn sink, void *sink_ctx, sr_chain_summary *out)
 {
   if (!ds || !specs || n_chains <= 0) return SR_EINVAL;
   return run_common(ds, specs, n_chains, opts, sink, sink_ctx, NULL, out, NULL);
+}
+
+SR_API int sr_run_chains_multi(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n_chains, const sr_run_opts *opts,
+                               const int32_t *devices, int32_t n_devices, sr_sample_sink_fn sink, void *sink_ctx,
+                               sr_chain_summary *out)
+{
+  if (!ds || !specs || n_chains <= 0) return SR_EINVAL;
+  return run_multi(ds, specs, n_chains, opts, devices, n_devices, sink, sink_ctx, NULL, out, NULL);
 }
 
 /* ------------------------------------------------------------ file output */
@@ -979,10 +1120,10 @@ static void chain_dir(char *buf, size_t n, const char *root, int id)
   else snprintf(buf, n, "%s/Chains/chain_%d", root, id);
 }
 
-SR_API int sr_run_to_dirs(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n, const sr_run_opts *opts,
-                          const char *root, sr_chain_summary *out)
+SR_API int sr_run_to_dirs_multi(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n, const sr_run_opts *opts,
+                                const int32_t *devices, int32_t n_devices, const char *root, sr_chain_summary *out)
 {
-  if (!ds || !specs || n <= 0 || !root) return SR_EINVAL;
+  if (!ds || !specs || n <= 0 || !root || !devices || n_devices <= 0 || n_devices > n) return SR_EINVAL;
   char path[4096], dir[4000];
   snprintf(path, sizeof path, "%s/mcmc_c.log", root);     /* mcmc.c:104 (never written) */
   FILE *lf = fopen(path, "a");
@@ -1004,7 +1145,7 @@ SR_API int sr_run_to_dirs(const sr_dataset *ds, const sr_chain_spec *specs, int3
   }
   sr_state_host st;
   memset(&st, 0, sizeof st);
-  if (!rc) rc = run_common(ds, specs, n, opts, NULL, NULL, &x, sum, &st);
+  if (!rc) rc = run_multi(ds, specs, n, opts, devices, n_devices, NULL, NULL, &x, sum, &st);
   for (int c = 0; c < n; c++) if (x.f[c]) fclose(x.f[c]);
   free(x.f);
   if (rc && rc != SR_EINCONSISTENT) { if (!out) free(sum); state_free(&st); return rc; }
@@ -1042,6 +1183,13 @@ SR_API int sr_run_to_dirs(const sr_dataset *ds, const sr_chain_spec *specs, int3
   state_free(&st);
   if (!out) free(sum);
   return rc;
+}
+
+SR_API int sr_run_to_dirs(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n, const sr_run_opts *opts,
+                          const char *root, sr_chain_summary *out)
+{
+  const int32_t dev = opts ? opts->device : 0;
+  return sr_run_to_dirs_multi(ds, specs, n, opts, &dev, 1, root, out);
 }
 
 /* ------------------------------------------------------ test / diagnostic hooks */

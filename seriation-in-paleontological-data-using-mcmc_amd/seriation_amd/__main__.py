@@ -6,7 +6,7 @@ whole job at once and writes the same ``Chains/chain_NN`` tree:
 
     python -m seriation_amd DATASET [--chains 100] [--burnin 1000] [--samples 1000] [--thin 10]
                                     [--seed-base S] [--devices 0,1] [--root .] [--select K]
-                                    [--no-save]
+                                    [--no-save] [--debug-check]
 
   --thin        sweeps per saved sample (the reference's mcmc_sample runs 10, mcmc.c:225)
   --seed-base   chain k gets seed S + k; omitted -> unique 1-byte urandom seeds like
@@ -14,6 +14,8 @@ whole job at once and writes the same ``Chains/chain_NN`` tree:
   --select K    after the run, the one-sigma selection of choose_chains (script.py:70-98) over
                 the written exp_data.csv files; prints the chosen chain indices
   --no-save     sample without writing files; prints one JSON summary per chain
+  --debug-check mcmc_consistent on every chain after every mcmc_sample call (the reference's
+                MCMCDEBUG build, mcmc.c:249-255); with --no-save
 
 Prints the wall time (seconds, 2 decimals) as script.py:67 does.  Exit status 1 when a chain
 fails its closing consistency check (mcmc.c:199-204).
@@ -38,6 +40,7 @@ def main(argv=None):
     ap.add_argument("--root", default=".")
     ap.add_argument("--select", type=int, default=0)
     ap.add_argument("--no-save", action="store_true")
+    ap.add_argument("--debug-check", action="store_true")
     a = ap.parse_args(argv)
     if a.chains < 1 or a.burnin < 0 or a.samples < 0 or a.thin < 1:
         ap.error("--chains and --thin must be >= 1, --burnin and --samples >= 0")
@@ -49,11 +52,13 @@ def main(argv=None):
         seeds = [launcher._unique_seed(old) for _ in range(a.chains)]
     else:
         seeds = [a.seed_base + k for k in range(a.chains)]
+    if a.debug_check and not a.no_save:
+        ap.error("--debug-check runs with --no-save")
     if a.no_save:
         ds = core.Dataset.load(a.dataset)
         t0 = time.perf_counter()
         summ, _ = core.run_chains(ds, seeds, burnin_calls=a.burnin, sample_calls=a.samples,
-                                  sweeps_per_call=a.thin, device=devices[0])
+                                  sweeps_per_call=a.thin, devices=devices[:len(seeds)], debug_check=a.debug_check)
         wall = time.perf_counter() - t0
         for s in summ:
             print(json.dumps(s))

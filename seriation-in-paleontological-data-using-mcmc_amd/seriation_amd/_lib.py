@@ -23,6 +23,8 @@ SR_MAXS = 2000
 SR_F_NO_CHECK = 1
 SR_F_HBM_COLUMNS = 2
 SR_F_LDS_COLUMNS = 4
+SR_F_DEBUG_CHECK = 8
+SR_F_DEBUG_PRINT = 16
 
 
 class SrError(RuntimeError):
@@ -74,7 +76,7 @@ SINK_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, ctypes
 PUBLIC_SYMBOLS = [
     "sr_parse_dataset", "sr_load_dataset", "sr_free_dataset", "sr_save_dataset_bin", "sr_load_dataset_bin",
     "sr_default_opts",
-    "sr_run_chains", "sr_run_to_dirs", "sr_session_create", "sr_session_set_stream",
+    "sr_run_chains", "sr_run_to_dirs", "sr_run_chains_multi", "sr_run_to_dirs_multi", "sr_session_create", "sr_session_set_stream",
     "sr_session_run", "sr_session_sync", "sr_session_records", "sr_session_record_capacity",
     "sr_session_fetch_records", "sr_session_reset_records", "sr_session_state",
     "sr_session_accept_counts", "sr_session_fallback_counts", "sr_session_last_kernel_ms", "sr_session_block_threads", "sr_session_variant",
@@ -105,6 +107,10 @@ def _lib():
                                   c_void_p, P(sr_chain_summary)]),
         "sr_run_to_dirs": (c_int, [P(sr_dataset), P(sr_chain_spec), c_i32, P(sr_run_opts),
                                    ctypes.c_char_p, P(sr_chain_summary)]),
+        "sr_run_chains_multi": (c_int, [P(sr_dataset), P(sr_chain_spec), c_i32, P(sr_run_opts), P(c_i32), c_i32,
+                                        SINK_FN, c_void_p, P(sr_chain_summary)]),
+        "sr_run_to_dirs_multi": (c_int, [P(sr_dataset), P(sr_chain_spec), c_i32, P(sr_run_opts), P(c_i32), c_i32,
+                                         ctypes.c_char_p, P(sr_chain_summary)]),
         "sr_session_create": (c_int, [P(sr_dataset), P(sr_chain_spec), c_i32, P(sr_run_opts), P(c_void_p)]),
         "sr_session_set_stream": (c_int, [c_void_p, c_void_p]),
         "sr_session_run": (c_int, [c_void_p, c_i32, c_i32]),

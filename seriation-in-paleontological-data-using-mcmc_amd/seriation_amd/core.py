@@ -73,8 +73,10 @@ class Dataset:
 
 
 def make_opts(burnin_calls=1000, sample_calls=1000, sweeps_per_call=10, device=0, block_threads=0,
-              calls_per_launch=0, check=True, columns="auto"):
-    """columns: "auto" (LDS when the layout fits, else HBM), "lds" or "hbm" (SR_F_*_COLUMNS)."""
+              calls_per_launch=0, check=True, columns="auto", debug_check=False, debug_print=False):
+    """columns: "auto" (LDS when the layout fits, else HBM), "lds" or "hbm" (SR_F_*_COLUMNS).
+    debug_check: mcmc_consistent after every mcmc_sample call (the reference's MCMCDEBUG,
+    mcmc.c:249-255; SR_F_DEBUG_CHECK), debug_print: its acceptance-rate lines on stderr."""
     o = L.sr_run_opts()
     L.lib().sr_default_opts(ctypes.byref(o))
     o.burnin_calls = burnin_calls
@@ -85,6 +87,8 @@ def make_opts(burnin_calls=1000, sample_calls=1000, sweeps_per_call=10, device=0
     o.calls_per_launch = calls_per_launch
     o.flags = (0 if check else L.SR_F_NO_CHECK) | {"auto": 0, "lds": L.SR_F_LDS_COLUMNS,
                                                    "hbm": L.SR_F_HBM_COLUMNS}[columns]
+    if debug_check:
+        o.flags |= L.SR_F_DEBUG_CHECK | (L.SR_F_DEBUG_PRINT if debug_print else 0)
     return o
 
 
@@ -102,12 +106,12 @@ class Session:
     ``calls`` mcmc_sample calls (mcmc.c:214-258) for every chain."""
 
     def __init__(self, dataset, seeds, device=0, sweeps_per_call=10, calls_per_launch=0, block_threads=0,
-                 chain_ids=None, columns="auto"):
+                 chain_ids=None, columns="auto", debug_check=False):
         self.ds = dataset
         self.n = len(seeds)
         self.specs = make_specs(seeds, chain_ids)
         self.opts = make_opts(sweeps_per_call=sweeps_per_call, device=device, block_threads=block_threads,
-                              calls_per_launch=calls_per_launch, columns=columns)
+                              calls_per_launch=calls_per_launch, columns=columns, debug_check=debug_check)
         h = ctypes.c_void_p()
         _check(L.lib().sr_session_create(ctypes.byref(dataset.c), self.specs, self.n, ctypes.byref(self.opts),
                                          ctypes.byref(h)), "sr_session_create")
@@ -228,14 +232,21 @@ class Session:
         self.close()
 
 
+def _devices(devices):
+    arr = (ctypes.c_int32 * len(devices))(*[int(d) for d in devices])
+    return arr, len(devices)
+
+
 def run_chains(dataset, seeds, burnin_calls=1000, sample_calls=1000, sweeps_per_call=10, device=0,
-               chain_ids=None, keep_records=False, calls_per_launch=0, block_threads=0, columns="auto"):
+               chain_ids=None, keep_records=False, calls_per_launch=0, block_threads=0, columns="auto",
+               devices=None, debug_check=False):
     """sr_run_chains: returns (summaries list of dicts, records or None).
-    records = (ab_pi int32 [n, ts, 2M+N], cdl [n, ts, 3]) when keep_records."""
+    records = (ab_pi int32 [n, ts, 2M+N], cdl [n, ts, 3]) when keep_records.
+    devices: a list of HIP ordinals (may repeat) -> sr_run_chains_multi, chains sharded over them."""
     n = len(seeds)
     specs = make_specs(seeds, chain_ids)
     opts = make_opts(burnin_calls, sample_calls, sweeps_per_call, device, block_threads=block_threads,
-                     calls_per_launch=calls_per_launch, columns=columns)
+                     calls_per_launch=calls_per_launch, columns=columns, debug_check=debug_check)
     out = (L.sr_chain_summary * n)()
     N, M = dataset.N, dataset.M
     recs = None
@@ -252,7 +263,11 @@ def run_chains(dataset, seeds, burnin_calls=1000, sample_calls=1000, sweeps_per_
         return 0
 
     cb = L.SINK_FN(sink) if keep_records else ctypes.cast(None, L.SINK_FN)
-    rc = L.lib().sr_run_chains(ctypes.byref(dataset.c), specs, n, ctypes.byref(opts), cb, None, out)
+    if devices:
+        darr, nd = _devices(devices)
+        rc = L.lib().sr_run_chains_multi(ctypes.byref(dataset.c), specs, n, ctypes.byref(opts), darr, nd, cb, None, out)
+    else:
+        rc = L.lib().sr_run_chains(ctypes.byref(dataset.c), specs, n, ctypes.byref(opts), cb, None, out)
     if rc not in (L.SR_OK, L.SR_EINCONSISTENT):
         raise L.SrError(rc, "sr_run_chains")
     summ = [dict(chain_id=o.chain_id, consistent=o.consistent, exp_loglik=o.exp_loglik, exp_c=o.exp_c,
@@ -261,15 +276,21 @@ def run_chains(dataset, seeds, burnin_calls=1000, sample_calls=1000, sweeps_per_
 
 
 def run_to_dirs(dataset, seeds, root=".", chain_ids=None, burnin_calls=1000, sample_calls=1000, device=0,
-                sweeps_per_call=10):
+                sweeps_per_call=10, devices=None):
     """sr_run_to_dirs: writes Chains/chain_NN/*.csv under root like the reference main().
-    sweeps_per_call is the thinning (the reference's mcmc_sample runs 10, mcmc.c:225)."""
+    sweeps_per_call is the thinning (the reference's mcmc_sample runs 10, mcmc.c:225).
+    devices: HIP ordinals (may repeat) -> sr_run_to_dirs_multi."""
     n = len(seeds)
     specs = make_specs(seeds, chain_ids)
     opts = make_opts(burnin_calls, sample_calls, sweeps_per_call, device)
     out = (L.sr_chain_summary * n)()
-    rc = L.lib().sr_run_to_dirs(ctypes.byref(dataset.c), specs, n, ctypes.byref(opts),
-                                os.fsencode(root), out)
+    if devices:
+        darr, nd = _devices(devices)
+        rc = L.lib().sr_run_to_dirs_multi(ctypes.byref(dataset.c), specs, n, ctypes.byref(opts), darr, nd,
+                                          os.fsencode(root), out)
+    else:
+        rc = L.lib().sr_run_to_dirs(ctypes.byref(dataset.c), specs, n, ctypes.byref(opts),
+                                    os.fsencode(root), out)
     if rc not in (L.SR_OK, L.SR_EINCONSISTENT):
         raise L.SrError(rc, "sr_run_to_dirs")
     return [dict(chain_id=o.chain_id, consistent=o.consistent, exp_loglik=o.exp_loglik, exp_c=o.exp_c,

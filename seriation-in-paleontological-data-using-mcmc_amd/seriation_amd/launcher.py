@@ -9,7 +9,6 @@ output depends only on (dataset, seed), never on the sharding.
 """
 import os
 import subprocess
-import threading
 import time
 
 import numpy as np
@@ -48,7 +47,8 @@ def run_all_chains(dataset, n_chains=100, seeds=None, devices=None, burnin_calls
 
     seeds: None -> unique 1-byte urandom seeds exactly like the reference (only 256 exist, so
     n_chains <= 256); otherwise an explicit list (deterministic runs).
-    devices: list of GPU ordinals to shard over (default: [0])."""
+    devices: list of GPU ordinals to shard over (default: [0]); the sharding is done by the C
+    library (sr_run_to_dirs_multi: one host thread and session per device)."""
     if seeds is None:
         old = []
         seeds = [_unique_seed(old) for _ in range(n_chains)]
@@ -57,29 +57,13 @@ def run_all_chains(dataset, n_chains=100, seeds=None, devices=None, burnin_calls
     ds = core.Dataset.load(str(dataset))
     os.makedirs(os.path.join(root, "Chains"), exist_ok=True)
     start = time.perf_counter()
-    shards = np.array_split(np.arange(len(seeds)), len(devices))
-    results = [None] * len(devices)
-    errors = []
-
-    def work(k, dev, idx):
-        try:
-            results[k] = core.run_to_dirs(ds, [seeds[i] for i in idx], root=root, chain_ids=list(idx),
-                                          burnin_calls=burnin_calls, sample_calls=sample_calls, device=dev,
-                                          sweeps_per_call=sweeps_per_call)
-        except Exception as e:  # re-raised below
-            errors.append(e)
-
-    threads = [threading.Thread(target=work, args=(k, d, s)) for k, (d, s) in enumerate(zip(devices, shards)) if len(s)]
-    for t in threads:
-        t.start()
-    for t in threads:
-        t.join()
-    if errors:
-        raise errors[0]
+    devices = devices[:len(seeds)]
+    summ = core.run_to_dirs(ds, seeds, root=root, chain_ids=list(range(len(seeds))), burnin_calls=burnin_calls,
+                            sample_calls=sample_calls, sweeps_per_call=sweeps_per_call, devices=devices)
     finish = time.perf_counter()
     if verbose:
         print(round(finish - start, 2))
-    return [r for part in results if part for r in part]
+    return summ
 
 
 def _read_exp_loglik(path):

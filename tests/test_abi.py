@@ -162,3 +162,39 @@ def test_restore_validates_chain_state(tmp_path):
     assert restore(damaged("rng", 0, pos + 624 * 20, "<u8")) == -2         # cursor beyond the ring
     if nh:
         assert restore(damaged("hp", 0, N + 3)) == -2                      # hard position out of range
+
+
+def test_hard_site_limit_boundary():
+    """The kernel holds at most SR_NHMAX = 32 hard sites (a 32-bit mask per taxon): 33 are refused
+    with SR_EUNSUPPORTED before any device call (the 32-site case runs in tests/test_gpu_edge.py
+    'nh32').  The reference has no such limit."""
+    def text(nh, N=40, M=6):
+        rows = ["%d %d" % (N, M)]
+        for i in range(N):
+            rows.append(" ".join("1" if (i + m) % 3 == 0 else "0" for m in range(M)) + (" *" if i < nh else ""))
+        return ("\n".join(rows) + "\n").encode()
+    ds33 = sa.Dataset.parse(text(33))
+    assert ds33.nh == 33
+    with pytest.raises(sa.SrError) as e:
+        sa.Session(ds33, [1])
+    assert e.value.code == L.SR_EUNSUPPORTED
+    out = (L.sr_chain_summary * 1)()
+    devs = (ctypes.c_int32 * 1)(0)
+    assert sa.lib().sr_run_chains_multi(ctypes.byref(ds33.c), sa.core.make_specs([1]), 1, None, devs, 1,
+                                        ctypes.cast(None, L.SINK_FN), None, out) == L.SR_EUNSUPPORTED
+    if not _gpu_present():
+        with pytest.raises(sa.SrError) as e:
+            sa.Session(sa.Dataset.parse(text(32)), [1])
+        assert e.value.code == L.SR_EDEVICE   # accepted by the limit check, then no device
+
+
+def test_multi_device_arguments_rejected():
+    lib = sa.lib()
+    ds = sa.Dataset.parse(b"3 2\n1 0\n1 1\n0 1\n")
+    out = (L.sr_chain_summary * 2)()
+    devs = (ctypes.c_int32 * 3)(0, 0, 0)
+    none = ctypes.cast(None, L.SINK_FN)
+    # more shards than chains, no device list, no shards
+    assert lib.sr_run_chains_multi(ctypes.byref(ds.c), sa.core.make_specs([1, 2]), 2, None, devs, 3, none, None, out) == L.SR_EINVAL
+    assert lib.sr_run_chains_multi(ctypes.byref(ds.c), sa.core.make_specs([1, 2]), 2, None, None, 1, none, None, out) == L.SR_EINVAL
+    assert lib.sr_run_to_dirs_multi(ctypes.byref(ds.c), sa.core.make_specs([1, 2]), 2, None, devs, 0, b"/tmp", out) == L.SR_EINVAL

@@ -134,7 +134,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=20, help="untimed steps first (the clocks ramp over the first ~10 launches)")
     ap.add_argument("--chains-per-gpu", type=int, default=100)
     ap.add_argument("--calls-per-step", type=int, default=10)
     ap.add_argument("--dataset", default=SYNTH)

@@ -73,6 +73,10 @@ typedef struct {
 #define SR_F_DEBUG_CHECK 8   /* the reference's MCMCDEBUG (mcmc.c:249-255): mcmc_consistent on every chain after
                                 every mcmc_sample call (one call per launch); SR_EINCONSISTENT on the first failure */
 #define SR_F_DEBUG_PRINT 16  /* with SR_F_DEBUG_CHECK: MCMCDEBUG's acceptance-rate line on stderr per chain and call */
+#define SR_F_RNG_PHILOX 32   /* opt-in: the sampling phase draws every word from a counter-based Philox4x32-10 stream
+                                keyed by the chain's seed instead of GSL's MT19937 (initialisation unchanged).  Not
+                                the reference's stream: statistically equivalent, not bit-equal.  A checkpoint
+                                keeps its stream kind; restoring it needs the same flag (else SR_EINVAL). */
 
 typedef struct {
   int32_t chain_id;

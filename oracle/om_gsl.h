@@ -39,7 +39,38 @@ typedef struct {
   uint32_t mt[OM_MT_N];
   int mti;
   uint64_t ndraw; /* words drawn so far (diagnostic) */
+  /* opt-in Philox mode (the product's SR_F_RNG_PHILOX; not the reference's generator):
+     word w = Philox4x32-10(key, counter w / 4)[w % 4] */
+  int philox;
+  uint32_t pkey[2], pbuf[4];
+  uint64_t pw;
 } om_rng;
+
+/* Philox4x32-10, restated from its publication (Salmon et al., "Parallel random numbers: as
+   easy as 1, 2, 3", SC'11; Random123 philox.h): 10 rounds of two 32x32->64 multiplies by
+   0xD2511F53 / 0xCD9E8D57 with the Weyl key schedule 0x9E3779B9 / 0xBB67AE85. */
+static inline void om_philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1)
+{
+  for (int round = 0; round < 10; round++) {
+    if (round) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+    const uint64_t a = (uint64_t)0xD2511F53u * c[0], b = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t n0 = (uint32_t)(b >> 32) ^ c[1] ^ k0, n2 = (uint32_t)(a >> 32) ^ c[3] ^ k1;
+    c[1] = (uint32_t)b;
+    c[3] = (uint32_t)a;
+    c[0] = n0;
+    c[2] = n2;
+  }
+}
+
+/* switch a generator to the Philox stream of `seed` (0 -> 4357), word 0 next */
+static inline void om_rng_philox(om_rng *r, unsigned long seed)
+{
+  uint64_t s = seed ? (uint64_t)seed : 4357u;
+  r->philox = 1;
+  r->pkey[0] = (uint32_t)s;
+  r->pkey[1] = (uint32_t)(s >> 32) ^ 0xA511E9B3u;
+  r->pw = 0;
+}
 
 static inline void om_rng_seed(om_rng *r, unsigned long s)
 {
@@ -51,10 +82,20 @@ static inline void om_rng_seed(om_rng *r, unsigned long s)
   }
   r->mti = OM_MT_N;
   r->ndraw = 0;
+  r->philox = 0;
 }
 
 static inline uint32_t om_rng_get(om_rng *r)
 {
+  if (r->philox) {
+    if ((r->pw & 3) == 0) {
+      const uint64_t ctr = r->pw >> 2;
+      r->pbuf[0] = (uint32_t)ctr; r->pbuf[1] = (uint32_t)(ctr >> 32); r->pbuf[2] = 0; r->pbuf[3] = 0;
+      om_philox4x32_10(r->pbuf, r->pkey[0], r->pkey[1]);
+    }
+    r->ndraw++;
+    return r->pbuf[r->pw++ & 3];
+  }
   uint32_t *mt = r->mt;
   if (r->mti >= OM_MT_N) {
     int kk;

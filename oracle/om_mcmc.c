@@ -705,6 +705,11 @@ OM_API int oracle_parse(const char *text, long len, int maxs, int *N, int *M, in
  *   check:   1 = verify mcmc_consistent (non-mutating) after every call
  * Returns 0, parse error (<0), or 1 if the final/check consistency test failed.
  */
+/* 1: the sampling phase of oracle_run_chain draws from the Philox stream (the product's opt-in
+ * SR_F_RNG_PHILOX mode), initialisation stays MT19937; 0: the reference's MT19937 throughout */
+static int g_rng_philox = 0;
+OM_API void oracle_set_rng(int philox) { g_rng_philox = philox ? 1 : 0; }
+
 OM_API int oracle_run_chain(const char *text, long len, int maxs, unsigned long seed, int manycd,
                             int tb, int ts, int sweeps, int check,
                             int32_t *init_out, double *init_dbl,
@@ -716,6 +721,7 @@ OM_API int oracle_run_chain(const char *text, long len, int maxs, unsigned long 
   if (rc) return rc;
   om_rng_seed(&x.rng, seed);
   om_randomize(&x);
+  if (g_rng_philox) om_rng_philox(&x.rng, seed);
   int bad = om_consistent(&x, 1, 0);
   const int N = x.N, M = x.M, W = 2 * M + N;
   if (init_out) {
@@ -747,6 +753,14 @@ OM_API int oracle_run_chain(const char *text, long len, int maxs, unsigned long 
   if (om_consistent(&x, 1, 1)) bad = 1;
   om_free(&x);
   return bad ? 1 : 0;
+}
+
+/* Philox4x32-10 block probe (known-answer tests) */
+OM_API void oracle_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4])
+{
+  uint32_t c[4] = {ctr[0], ctr[1], ctr[2], ctr[3]};
+  om_philox4x32_10(c, key[0], key[1]);
+  memcpy(out, c, sizeof c);
 }
 
 /* RNG probes for the unit tests. kind: 0 raw u32, 1 uniform, 2 uniform_pos,

@@ -53,6 +53,7 @@ struct KArgs {
   double *rec_cdl;
   unsigned long long *dbg;   /* SR_STAMPS builds: [chain][16] cycles per phase */
   uint16_t *gpre;            /* gm variant scratch, per chain: column prefix tables */
+  uint32_t *pkey;            /* [chain][2] Philox keys (SR_F_RNG_PHILOX), else null: MT19937 */
   double *gck, *glbuf, *gcbuf;   /* gm variant scratch: Gibbs checkpoints, logl terms, exact-delta terms */
 };
 
@@ -194,15 +195,31 @@ __device__ __forceinline__ void gsync()
 struct DRng {
   uint32_t *ring;   /* LDS, SR_RING blocks of 624 raw words */
   uint32_t blk, off, gen;   /* next word = block blk, index off; blocks [.., gen) exist */
+  uint32_t pk0, pk1;        /* Philox key (SR_F_RNG_PHILOX), */
+  bool ph;                  /* else the MT19937 recurrence */
 };
 
-/* generate block `gen` from block gen-1 (three dependency phases of the MT recurrence);
- * by-value arguments so the caller's cursor never escapes to scratch */
+/* generate block `gen` from block gen-1 (three dependency phases of the MT recurrence), or in
+ * the Philox mode from its counters alone (156 Philox4x32-10 calls, stored untempered so that
+ * every read site's tempering returns the Philox word); by-value arguments so the caller's
+ * cursor never escapes to scratch */
 template <bool WAVE>
-__device__ __noinline__ void rng_gen_block(uint32_t *ring, uint32_t gen, int t, int nthr)
+__device__ __noinline__ void rng_gen_block(uint32_t *ring, uint32_t gen, int t, int nthr, uint32_t pk0, uint32_t pk1, bool ph)
 {
   const uint32_t *prev = ring + ((gen - 1) & (SR_RING - 1)) * SR_MT_N;
   uint32_t *nxt = ring + (gen & (SR_RING - 1)) * SR_MT_N;
+  if (ph) {
+    for (int i = t; i < SR_MT_N / 4; i += nthr) {
+      const uint64_t cw = (uint64_t)gen * (SR_MT_N / 4) + (uint64_t)i;   /* word 4 cw + j of the stream */
+      const uint32_t ctr[4] = {(uint32_t)cw, (uint32_t)(cw >> 32), 0u, 0u}, key[2] = {pk0, pk1};
+      uint32_t o[4];
+      sr_philox4x32_10(ctr, key, o);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) nxt[4 * i + j] = sr_mt_untemper(o[j]);
+    }
+    gsync<WAVE>();
+    return;
+  }
   for (int k = t; k < 227; k += nthr) nxt[k] = sr_mt_mix(prev[k], prev[k + 1], prev[k + 397]);
   gsync<WAVE>();
   for (int k = 227 + t; k < 454; k += nthr) nxt[k] = sr_mt_mix(prev[k], prev[k + 1], nxt[k - 227]);
@@ -215,7 +232,7 @@ __device__ __noinline__ void rng_gen_block(uint32_t *ring, uint32_t gen, int t, 
 template <bool WAVE>
 __device__ __forceinline__ void rng_gen(DRng &r, int t, int nthr)
 {
-  rng_gen_block<WAVE>(r.ring, r.gen, t, nthr);
+  rng_gen_block<WAVE>(r.ring, r.gen, t, nthr, r.pk0, r.pk1, r.ph);
   r.gen++;
 }
 
@@ -532,9 +549,10 @@ struct BitWalk {
 
 /* mcmc_auxa + mcmc_logtop + mcmc_randompick for one limit of one taxon, in walk
  * coordinates (fwd: walk w = position w; rev: walk w = position N-1-w).  o = current limit,
- * entries w = 0..L.  Returns the picked entry and the count deltas dt0,df0,dt1,df1 there. */
+ * entries w = 0..L.  Returns the picked entry (the caller derives the count deltas there).
+ * Arguments by value and the result in a register: nothing of the caller lives in scratch. */
 __device__ __noinline__ int draw_exact(const uint32_t *Pm, int M, int N, bool rev, int o, int L, double u,
-                                      const CD &k, const sr_mtab &tb, int &dt0, int &df0, int &dt1, int &df1)
+                                      const CD k, const sr_mtab tb)
 {
   const int POo = rev ? ones_range(Pm, M, N - o, N) : ones_range(Pm, M, 0, o);
   auto q_at = [&](int w, int PO) -> double {
@@ -592,11 +610,6 @@ __device__ __noinline__ int draw_exact(const uint32_t *Pm, int M, int N, bool re
     long s = sr_run_sub(&r, pe, L - hi);
     res = (r <= 0.0) ? hi + (int)s : L;
   }
-  /* count deltas at the pick (the dt arrays of mcmc_auxa) */
-  const int POp = wprefix(res);
-  if (res == o) { dt0 = df0 = dt1 = df1 = 0; }
-  else if (res < o) { int O = POo - POp; int Z = (o - res) - O; dt0 = -Z; df0 = Z; dt1 = O; df1 = -O; }
-  else { int O = POp - POo; int Z = (res - o) - O; dt0 = Z; df0 = -Z; dt1 = -O; df1 = O; }
   return res;
 }
 
@@ -803,9 +816,10 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
 #ifdef SR_STAMPS
     if (!(S > 0.0)) atomicAdd((unsigned long long *)fbk + 3, 1ull);
 #endif
-    return draw_exact(Pm, M, N, rev, o, L, u, K, tb, dt0, df0, dt1, df1);
+    res = draw_exact(Pm, M, N, rev, o, L, u, K, tb);
   }
   GSTAMP(3);
+  /* count deltas at the pick (the dt arrays of mcmc_auxa) */
   const int POp = walk_prefix(Pm, M, N, NW, rev, res);
   if (res == o) { dt0 = df0 = dt1 = df1 = 0; }
   else if (res < o) { int O = POo - POp; int Z = (o - res) - O; dt0 = -Z; df0 = Z; dt1 = O; df1 = -O; }
@@ -1004,8 +1018,9 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
   }
   if (res < 0) {
     atomicAdd((unsigned long long *)fbk, 1ull);   /* exact-walk fallbacks (rare: counted always) */
-    return draw_exact(Pm, M, N, rev, o, L, u, K, tb, dt0, df0, dt1, df1);
+    res = draw_exact(Pm, M, N, rev, o, L, u, K, tb);
   }
+  /* count deltas at the pick (the dt arrays of mcmc_auxa) */
   const int POp = walk_prefix_s<NWM>(wk, res);
   if (res == o) { dt0 = df0 = dt1 = df1 = 0; }
   else if (res < o) { int O = POo - POp; int Z = (o - res) - O; dt0 = -Z; df0 = Z; dt1 = O; df1 = -O; }
@@ -1406,6 +1421,9 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
     R.blk = (uint32_t)(pos / SR_MT_N);
     R.off = (uint32_t)(pos % SR_MT_N);
     R.gen = (uint32_t)gen;
+    R.ph = A.pkey != nullptr;
+    R.pk0 = R.ph ? A.pkey[(size_t)chain * 2 + 0] : 0u;
+    R.pk1 = R.ph ? A.pkey[(size_t)chain * 2 + 1] : 0u;
   }
   if (tid == 0) for (int k = 0; k < 7; ++k) misc[MS_ACC + k] = 0;
   int rcur = 0;     /* current rpi buffer */
@@ -2238,7 +2256,7 @@ static int dev_alloc_copy(srk_dev *d, T **dst, const T *src, size_t n)
 }
 
 extern "C" int srk_create(const sr_state_host *st, int device, int block_threads, int rec_cap_calls, int gm_force,
-                          srk_dev **out)
+                          const uint32_t *pkey, srk_dev **out)
 {
   int ndev = srk_device_count();
   if (ndev <= 0 || device < 0 || device >= ndev) return -5;
@@ -2277,6 +2295,7 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
   rc |= dev_alloc_copy(d, &A.rec_abpi, (const int16_t *)nullptr, C * d->rec_cap * (2 * st->M + st->N));
   rc |= dev_alloc_copy(d, &A.rec_cdl, (const double *)nullptr, C * d->rec_cap * 3);
   rc |= dev_alloc_copy(d, &A.dbg, (const unsigned long long *)nullptr, C * 17 * 8);
+  if (pkey) rc |= dev_alloc_copy(d, &A.pkey, pkey, C * 2);
   if (d->gm) {
     rc |= dev_alloc_copy(d, &A.gpre, (const uint16_t *)nullptr, C * sr_gm_pre(st->M, st->NW));
     rc |= dev_alloc_copy(d, &A.gck, (const double *)nullptr, C * sr_gm_ck(st->N, st->M, TB));

@@ -431,13 +431,31 @@ static int session_new(const sr_dataset *ds, const sr_chain_spec *specs, int32_t
   sr_state_host st;
   int rc = state_alloc(&st, ds->N, ds->M, ds->nh, n_chains);
   if (rc) { sr_session_destroy(s); return rc; }
+  const int philox = (o.flags & SR_F_RNG_PHILOX) != 0;
   if (restore) rc = restore(restore_ctx, &st);
   else
-    for (int c = 0; c < n_chains && rc == SR_OK; c++) rc = init_chain(ds, specs[c].seed, &st, c);
+    for (int c = 0; c < n_chains && rc == SR_OK; c++) {
+      rc = init_chain(ds, specs[c].seed, &st, c);
+      if (philox) {   /* sampling draws from the chain's Philox stream, word 0 on (init stays GSL MT19937) */
+        st.rng[(size_t)c * 2 + 0] = 0;
+        st.rng[(size_t)c * 2 + 1] = 0;
+        st.cdl[(size_t)c * 4 + 3] = 1.0;   /* the stream kind travels with the state (checkpoints) */
+      }
+    }
+  /* a restored state keeps its stream: the caller's flag must name the same one */
+  for (int c = 0; c < n_chains && rc == SR_OK; c++)
+    if ((st.cdl[(size_t)c * 4 + 3] == 1.0) != philox) rc = SR_EINVAL;
+  uint32_t *pkey = NULL;
+  if (rc == SR_OK && philox) {
+    pkey = (uint32_t *)malloc(sizeof(uint32_t) * 2 * n_chains);
+    if (!pkey) rc = SR_ENOMEM;
+    for (int c = 0; c < n_chains && pkey; c++) sr_philox_key(specs[c].seed, pkey + 2 * c);
+  }
   if (rc) { state_free(&st); sr_session_destroy(s); return rc; }
   s->rec_cap = auto_calls_per_launch(&o);
   const int gm_force = (o.flags & SR_F_HBM_COLUMNS) ? 1 : ((o.flags & SR_F_LDS_COLUMNS) ? 0 : -1);
-  rc = srk_create(&st, o.device, o.block_threads, s->rec_cap, gm_force, &s->dev);
+  rc = srk_create(&st, o.device, o.block_threads, s->rec_cap, gm_force, pkey, &s->dev);
+  free(pkey);
   state_free(&st);
   if (rc) { sr_session_destroy(s); return rc == -6 ? SR_EUNSUPPORTED : SR_EDEVICE; }
   *out = s;
@@ -610,7 +628,9 @@ static int ck_validate(const sr_dataset *ds, const sr_state_host *st)
       if (hp[k] < 0 || hp[k] >= N || (k > 0 && hp[k] <= hp[k - 1]) || !ds->hard[rpi[hp[k]]]) return SR_EPARSE;
     const uint64_t pos = st->rng[(size_t)c * 2 + 0], gen = st->rng[(size_t)c * 2 + 1];
     const uint64_t blk = pos / SR_MT_N;
-    if (gen < 1 || blk > gen || gen - blk > SR_RING || gen > 0xffffffffULL) return SR_EPARSE;
+    const double kind = st->cdl[(size_t)c * 4 + 3];   /* 0 MT19937 (a seeded block exists), 1 Philox */
+    if ((kind != 0.0 && kind != 1.0) || (kind == 0.0 && gen < 1) || blk > gen || gen - blk > SR_RING || gen > 0xffffffffULL)
+      return SR_EPARSE;
   }
   return SR_OK;
 }
@@ -1209,6 +1229,13 @@ SR_API void sr_host_exp_log(const double *in, long n, double *out_exp, double *o
 }
 
 SR_API double sr_host_run_add(double x, double e, long L) { return sr_run_add(x, e, L); }
+
+/* the Philox mode's building blocks as the device uses them (sr_rng.h) */
+SR_API void sr_host_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) { sr_philox4x32_10(ctr, key, out); }
+SR_API void sr_host_mt_untemper(const uint32_t *in, long n, uint32_t *untempered, uint32_t *roundtrip)
+{
+  for (long k = 0; k < n; k++) { untempered[k] = sr_mt_untemper(in[k]); roundtrip[k] = sr_mt_temper(untempered[k]); }
+}
 SR_API long sr_host_run_sub(double *r, double p, long L) { return sr_run_sub(r, p, L); }
 
 /* initial chain state as the host builds it (a, b, pi after mcmc_randomize; c, d, loglik) */

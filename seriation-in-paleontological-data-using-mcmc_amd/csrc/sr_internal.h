@@ -40,8 +40,10 @@ extern "C" {
 #endif
 
 int srk_device_count(void);
-/* gm_force: -1 auto (LDS columns when they fit, else HBM columns), 0 LDS, 1 HBM */
-int srk_create(const sr_state_host *st, int device, int block_threads, int rec_cap_calls, int gm_force, srk_dev **out);
+/* gm_force: -1 auto (LDS columns when they fit, else HBM columns), 0 LDS, 1 HBM;
+ * pkey: [nchains][2] Philox keys (the SR_F_RNG_PHILOX stream), NULL = MT19937 */
+int srk_create(const sr_state_host *st, int device, int block_threads, int rec_cap_calls, int gm_force,
+               const uint32_t *pkey, srk_dev **out);
 int srk_set_stream(srk_dev *d, void *stream);
 /* calls*spc sweeps for all chains; save -> records appended at slot rec_base.. */
 int srk_run(srk_dev *d, int calls, int spc, int save, int rec_base);

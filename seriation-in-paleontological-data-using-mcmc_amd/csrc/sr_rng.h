@@ -37,6 +37,44 @@ SR_RHD uint32_t sr_mt_temper(uint32_t k)
   return k;
 }
 
+/* the inverse of sr_mt_temper: sr_mt_temper(sr_mt_untemper(x)) == x for every x (the Philox
+ * mode stores untempered words in the ring, so every read site keeps its tempering) */
+SR_RHD uint32_t sr_mt_untemper(uint32_t y)
+{
+  y ^= y >> 18;
+  y ^= (y << 15) & 0xefc60000u;
+  uint32_t x = y;
+  for (int i = 0; i < 4; ++i) x = y ^ ((x << 7) & 0x9d2c5680u);
+  return x ^ (x >> 11) ^ (x >> 22);
+}
+
+/* ---- opt-in counter-based stream (SR_F_RNG_PHILOX; north_star "Philox state per lane") ----
+ * Philox4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11; the generator rocRAND's philox4x32_10
+ * implements): word w of a chain's stream = philox(key, ctr = {w / 4 lo, w / 4 hi, 0, 0})[w % 4],
+ * key = {seed lo, seed hi ^ SR_PHILOX_KEY1}.  Any block of words is computable lane-parallel with
+ * no state but the counter.  Not the reference's stream: statistically equivalent, not bit-equal. */
+#define SR_PHILOX_KEY1 0xA511E9B3u
+SR_RHD void sr_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4])
+{
+  uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+  uint32_t k0 = key_in[0], k1 = key_in[1];
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0, h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
+    c0 = h1 ^ c1 ^ k0; c1 = l1; c2 = h0 ^ c3 ^ k1; c3 = l0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* a chain's Philox key from its GSL_RNG_SEED value (0 -> GSL's default 4357, as mt_set) */
+SR_RHD void sr_philox_key(uint64_t seed, uint32_t key[2])
+{
+  if (seed == 0) seed = 4357;
+  key[0] = (uint32_t)seed;
+  key[1] = (uint32_t)(seed >> 32) ^ SR_PHILOX_KEY1;
+}
+
 /* one recurrence step: y = upper(cur) | lower(next); far ^ (y >> 1) ^ mag(y) */
 SR_RHD uint32_t sr_mt_mix(uint32_t cur, uint32_t next, uint32_t far)
 {

@@ -25,6 +25,7 @@ SR_F_HBM_COLUMNS = 2
 SR_F_LDS_COLUMNS = 4
 SR_F_DEBUG_CHECK = 8
 SR_F_DEBUG_PRINT = 16
+SR_F_RNG_PHILOX = 32
 
 
 class SrError(RuntimeError):
@@ -137,6 +138,8 @@ def _lib():
         "sr_host_exp_log": (None, [P(c_double), ctypes.c_long, P(c_double), P(c_double)]),
         "sr_host_run_add": (c_double, [c_double, c_double, ctypes.c_long]),
         "sr_host_run_sub": (ctypes.c_long, [P(c_double), c_double, ctypes.c_long]),
+        "sr_host_philox": (None, [P(ctypes.c_uint32), P(ctypes.c_uint32), P(ctypes.c_uint32)]),
+        "sr_host_mt_untemper": (None, [P(ctypes.c_uint32), ctypes.c_long, P(ctypes.c_uint32), P(ctypes.c_uint32)]),
         "sr_host_initial_checkpoint": (c_int, [P(sr_dataset), P(sr_chain_spec), c_i32, ctypes.c_char_p]),
         "sr_host_init_chain": (c_int, [P(sr_dataset), ctypes.c_uint64, P(c_i32), P(c_i32), P(c_i32),
                                        P(c_double), P(ctypes.c_uint64)]),
@@ -144,6 +147,8 @@ def _lib():
         "sr_device_selftest_math": (c_int, [c_int, P(c_double), ctypes.c_long, P(c_double), P(c_double)]),
     }
     for name, (res, args) in sig.items():
+        if not hasattr(L, name):   # an older build (A/B variants); tests/test_abi.py checks the product's exports
+            continue
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

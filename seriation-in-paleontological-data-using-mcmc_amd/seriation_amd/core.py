@@ -73,10 +73,12 @@ class Dataset:
 
 
 def make_opts(burnin_calls=1000, sample_calls=1000, sweeps_per_call=10, device=0, block_threads=0,
-              calls_per_launch=0, check=True, columns="auto", debug_check=False, debug_print=False):
+              calls_per_launch=0, check=True, columns="auto", debug_check=False, debug_print=False, rng="mt"):
     """columns: "auto" (LDS when the layout fits, else HBM), "lds" or "hbm" (SR_F_*_COLUMNS).
     debug_check: mcmc_consistent after every mcmc_sample call (the reference's MCMCDEBUG,
-    mcmc.c:249-255; SR_F_DEBUG_CHECK), debug_print: its acceptance-rate lines on stderr."""
+    mcmc.c:249-255; SR_F_DEBUG_CHECK), debug_print: its acceptance-rate lines on stderr.
+    rng: "mt" (the reference's GSL MT19937 stream, bit-exact) or "philox" (opt-in SR_F_RNG_PHILOX:
+    counter-based Philox4x32-10 per chain for the sampling phase; statistically equivalent only)."""
     o = L.sr_run_opts()
     L.lib().sr_default_opts(ctypes.byref(o))
     o.burnin_calls = burnin_calls
@@ -89,6 +91,10 @@ def make_opts(burnin_calls=1000, sample_calls=1000, sweeps_per_call=10, device=0
                                                    "hbm": L.SR_F_HBM_COLUMNS}[columns]
     if debug_check:
         o.flags |= L.SR_F_DEBUG_CHECK | (L.SR_F_DEBUG_PRINT if debug_print else 0)
+    if rng not in ("mt", "philox"):
+        raise ValueError("rng must be 'mt' or 'philox'")
+    if rng == "philox":
+        o.flags |= L.SR_F_RNG_PHILOX
     return o
 
 
@@ -106,12 +112,12 @@ class Session:
     ``calls`` mcmc_sample calls (mcmc.c:214-258) for every chain."""
 
     def __init__(self, dataset, seeds, device=0, sweeps_per_call=10, calls_per_launch=0, block_threads=0,
-                 chain_ids=None, columns="auto", debug_check=False):
+                 chain_ids=None, columns="auto", debug_check=False, rng="mt"):
         self.ds = dataset
         self.n = len(seeds)
         self.specs = make_specs(seeds, chain_ids)
         self.opts = make_opts(sweeps_per_call=sweeps_per_call, device=device, block_threads=block_threads,
-                              calls_per_launch=calls_per_launch, columns=columns, debug_check=debug_check)
+                              calls_per_launch=calls_per_launch, columns=columns, debug_check=debug_check, rng=rng)
         h = ctypes.c_void_p()
         _check(L.lib().sr_session_create(ctypes.byref(dataset.c), self.specs, self.n, ctypes.byref(self.opts),
                                          ctypes.byref(h)), "sr_session_create")
@@ -123,12 +129,12 @@ class Session:
 
     @classmethod
     def restore(cls, dataset, path, device=0, sweeps_per_call=10, calls_per_launch=0, block_threads=0,
-                columns="auto"):
+                columns="auto", rng="mt"):
         """sr_session_restore: a session continuing the chains of a checkpoint over `dataset`."""
         self = cls.__new__(cls)
         self.ds = dataset
         self.opts = make_opts(sweeps_per_call=sweeps_per_call, device=device, block_threads=block_threads,
-                              calls_per_launch=calls_per_launch, columns=columns)
+                              calls_per_launch=calls_per_launch, columns=columns, rng=rng)
         h = ctypes.c_void_p()
         _check(L.lib().sr_session_restore(ctypes.byref(dataset.c), os.fsencode(path), ctypes.byref(self.opts),
                                           ctypes.byref(h)), "sr_session_restore")
@@ -239,14 +245,14 @@ def _devices(devices):
 
 def run_chains(dataset, seeds, burnin_calls=1000, sample_calls=1000, sweeps_per_call=10, device=0,
                chain_ids=None, keep_records=False, calls_per_launch=0, block_threads=0, columns="auto",
-               devices=None, debug_check=False):
+               devices=None, debug_check=False, rng="mt"):
     """sr_run_chains: returns (summaries list of dicts, records or None).
     records = (ab_pi int32 [n, ts, 2M+N], cdl [n, ts, 3]) when keep_records.
     devices: a list of HIP ordinals (may repeat) -> sr_run_chains_multi, chains sharded over them."""
     n = len(seeds)
     specs = make_specs(seeds, chain_ids)
     opts = make_opts(burnin_calls, sample_calls, sweeps_per_call, device, block_threads=block_threads,
-                     calls_per_launch=calls_per_launch, columns=columns, debug_check=debug_check)
+                     calls_per_launch=calls_per_launch, columns=columns, debug_check=debug_check, rng=rng)
     out = (L.sr_chain_summary * n)()
     N, M = dataset.N, dataset.M
     recs = None
@@ -276,13 +282,13 @@ def run_chains(dataset, seeds, burnin_calls=1000, sample_calls=1000, sweeps_per_
 
 
 def run_to_dirs(dataset, seeds, root=".", chain_ids=None, burnin_calls=1000, sample_calls=1000, device=0,
-                sweeps_per_call=10, devices=None):
+                sweeps_per_call=10, devices=None, rng="mt"):
     """sr_run_to_dirs: writes Chains/chain_NN/*.csv under root like the reference main().
     sweeps_per_call is the thinning (the reference's mcmc_sample runs 10, mcmc.c:225).
     devices: HIP ordinals (may repeat) -> sr_run_to_dirs_multi."""
     n = len(seeds)
     specs = make_specs(seeds, chain_ids)
-    opts = make_opts(burnin_calls, sample_calls, sweeps_per_call, device)
+    opts = make_opts(burnin_calls, sample_calls, sweeps_per_call, device, rng=rng)
     out = (L.sr_chain_summary * n)()
     if devices:
         darr, nd = _devices(devices)

@@ -47,6 +47,10 @@ def load(path):
     L.oracle_shuffle.argtypes = [ctypes.c_ulong, P(ctypes.c_int32), ctypes.c_long]
     L.oracle_choose.argtypes = [ctypes.c_ulong, P(ctypes.c_int32), ctypes.c_long, P(ctypes.c_int32), ctypes.c_long]
     L.oracle_exp_log.argtypes = [P(ctypes.c_double), ctypes.c_long, P(ctypes.c_double), P(ctypes.c_double)]
+    L.oracle_set_rng.restype = None
+    L.oracle_set_rng.argtypes = [ctypes.c_int]
+    L.oracle_philox.restype = None
+    L.oracle_philox.argtypes = [P(ctypes.c_uint32), P(ctypes.c_uint32), P(ctypes.c_uint32)]
     L.oracle_libm_mismatch.restype = None
     L.oracle_libm_mismatch.argtypes = [P(ctypes.c_double), ctypes.c_long, P(ctypes.c_long), P(ctypes.c_long)]
     return L
@@ -70,10 +74,12 @@ def parse(text, maxs=2000):
     return 0, X.reshape(N.value, M.value), h
 
 
-def run_chain(text, seed, tb, ts, sweeps=10, check=0, maxs=2000, want_init=False):
-    """Returns dict(rc, init (a,b,pi), init_cdl, rec_int [ts, 2M+N], rec_dbl [ts, 3], exp, acc, words)."""
+def run_chain(text, seed, tb, ts, sweeps=10, check=0, maxs=2000, want_init=False, rng="mt"):
+    """Returns dict(rc, init (a,b,pi), init_cdl, rec_int [ts, 2M+N], rec_dbl [ts, 3], exp, acc, words).
+    rng="philox": the sampling phase on the Philox stream (the product's SR_F_RNG_PHILOX)."""
     if isinstance(text, str):
         text = text.encode()
+    lib().oracle_set_rng(1 if rng == "philox" else 0)
     rc, X, h = parse(text, maxs)
     assert rc == 0, rc
     N, M = X.shape

@@ -10,6 +10,7 @@ each piece is pinned against an independent source:
   * gaussian_ziggurat / gamma / beta: distribution moments and a KS test (the exact
     GSL stream for these is "parity unpinned", see DESIGN.md "Oracle").
 """
+import ctypes
 import json
 import os
 
@@ -129,3 +130,49 @@ def test_beta_moments(a, b):
     assert ((x >= 0) & (x <= 1)).all()
     assert abs(x.mean() - mean) < 5 * np.sqrt(var / len(x)) + 1e-12
     assert stats.kstest(x, "beta", args=(a, b)).pvalue > 1e-3
+
+
+# ---- the opt-in Philox stream (SR_F_RNG_PHILOX) ----------------------------------------------
+# Philox4x32-10 known answers (Random123's published kat_vectors for philox4x32_10)
+PHILOX_KAT = [
+    ((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+    ((0xffffffff,) * 4, (0xffffffff, 0xffffffff), (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+    ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), (0xa4093822, 0x299f31d0),
+     (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1)),
+]
+
+
+def _u32(v):
+    return (ctypes.c_uint32 * len(v))(*v)
+
+
+def test_philox_known_answers_oracle_and_product():
+    import seriation_amd as sa
+    for ctr, key, want in PHILOX_KAT:
+        o1, o2 = (ctypes.c_uint32 * 4)(), (ctypes.c_uint32 * 4)()
+        oracle_ref.lib().oracle_philox(_u32(ctr), _u32(key), o1)
+        sa.lib().sr_host_philox(_u32(ctr), _u32(key), o2)
+        assert tuple(o1) == want and tuple(o2) == want
+
+
+def test_mt_untemper_inverts_tempering():
+    """The Philox mode stores untempered words in the MT ring (every read site tempers)."""
+    import seriation_amd as sa
+    x = np.random.default_rng(5).integers(0, 2 ** 32, 200000, dtype=np.uint64).astype(np.uint32)
+    x = np.concatenate([x, np.array([0, 1, 0xffffffff, 0x80000000], np.uint32)])
+    un, rt = np.zeros_like(x), np.zeros_like(x)
+    P = ctypes.POINTER(ctypes.c_uint32)
+    sa.lib().sr_host_mt_untemper(x.ctypes.data_as(P), len(x), un.ctypes.data_as(P), rt.ctypes.data_as(P))
+    assert np.array_equal(rt, x)
+    assert not np.array_equal(un, x)
+
+
+def test_oracle_philox_chain_runs_consistent_and_differs():
+    text = open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "datasets", "g5s5.txt"), "rb").read()
+    a = oracle_ref.run_chain(text, 3, 5, 5, check=1, rng="philox")
+    b = oracle_ref.run_chain(text, 3, 5, 5, check=1)
+    assert a["rc"] == 0 and b["rc"] == 0
+    assert np.array_equal(a["init"], b["init"])          # initialisation stays MT19937
+    assert not np.array_equal(a["rec_int"], b["rec_int"])
+    c = oracle_ref.run_chain(text, 3, 5, 5, rng="philox")
+    assert np.array_equal(a["rec_int"], c["rec_int"])    # deterministic per seed

@@ -27,14 +27,14 @@ TABLE1 = {
 BAND = (0.002, 0.03, 0.02)
 
 
-def run_row(name, chains=100, burnin=1000, samples=1000, seed_base=1):
+def run_row(name, chains=100, burnin=1000, samples=1000, seed_base=1, rng="mt"):
     import seriation_amd as sa
     from seriation_amd import analysis, launcher
     sel, pc, pd, pr = TABLE1[name]
     ds = sa.Dataset.load(os.path.join(ROOT, "tests", "golden", "datasets", name + ".txt"))
     t0 = time.perf_counter()
     summ, (ri, rd) = sa.run_chains(ds, list(range(seed_base, seed_base + chains)), burnin_calls=burnin,
-                                   sample_calls=samples, keep_records=True)
+                                   sample_calls=samples, keep_records=True, rng=rng)
     wall = time.perf_counter() - t0
     vals = {"chain_%02d" % k: s["exp_loglik"] for k, s in enumerate(summ)}
     chosen = launcher.choose_from_values(vals, sel)
@@ -42,13 +42,13 @@ def run_row(name, chains=100, burnin=1000, samples=1000, seed_base=1):
     corr = analysis.corr_mn_from_records([ri[k][:, 2 * ds.M:] for k in chosen])
     got = (float(ec), float(ed), float(corr))
     pub = (pc, pd, pr)
-    return {"dataset": name, "sites": ds.N, "taxa": ds.M, "chains": chains, "seed_base": seed_base, "selected": chosen,
+    return {"dataset": name, "rng": rng, "sites": ds.N, "taxa": ds.M, "chains": chains, "seed_base": seed_base, "selected": chosen,
             "E_c": got[0], "E_d": got[1], "CORRMN": got[2], "published": {"E_c": pc, "E_d": pd, "CORRMN": pr},
             "within_band": [bool(abs(g - p) < b) for g, p, b in zip(got, pub, BAND)],
             "wall_s": wall, "chain_iterations": chains * (burnin + samples) * 10}
 
 
-def run_row_spread(name, blocks=6, chains=100, burnin=1000, samples=1000):
+def run_row_spread(name, blocks=6, chains=100, burnin=1000, samples=1000, rng="mt"):
     """The Table 1 estimator (100 chains -> one-sigma selection -> E[c], E[d], CORRMN) repeated over
     `blocks` disjoint seed blocks (seeds 1..100, 101..200, ...).  The reference's own seeds are not
     published (script.py draws them at random), so its row is one draw of this estimator: with 2
@@ -56,7 +56,7 @@ def run_row_spread(name, blocks=6, chains=100, burnin=1000, samples=1000):
     checked against the estimator's measured distribution instead -- the published value must lie
     within max(band, 3 sd) of the block mean."""
     import numpy as np
-    rows = [run_row(name, chains, burnin, samples, seed_base=1 + b * chains) for b in range(blocks)]
+    rows = [run_row(name, chains, burnin, samples, seed_base=1 + b * chains, rng=rng) for b in range(blocks)]
     sel, pc, pd, pr = TABLE1[name]
     out = {"dataset": name, "blocks": rows, "published": {"E_c": pc, "E_d": pd, "CORRMN": pr}}
     ok = []
@@ -75,11 +75,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", default="g10s10,g5s5,g10s2")
     ap.add_argument("--spread", type=int, default=0, help="repeat each row over this many disjoint seed blocks")
+    ap.add_argument("--rng", default="mt", choices=("mt", "philox"), help="philox: the opt-in SR_F_RNG_PHILOX stream")
     args = ap.parse_args()
     if args.spread:
-        rows = [run_row_spread(r, args.spread) for r in args.rows.split(",")]
+        rows = [run_row_spread(r, args.spread, rng=args.rng) for r in args.rows.split(",")]
     else:
-        rows = [run_row(r) for r in args.rows.split(",")]
+        rows = [run_row(r, rng=args.rng) for r in args.rows.split(",")]
     print(json.dumps({"source": "Docs/Report.pdf Table 1 (p.7)", "band": BAND, "rows": rows}, indent=1), flush=True)
 
 

@@ -146,6 +146,8 @@ def main():
     ap.add_argument("--cpu-workers", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--block-threads", type=int, default=0)
+    ap.add_argument("--rng", default="mt", choices=("mt", "philox"), help="philox: the opt-in counter-based stream "
+                    "(SR_F_RNG_PHILOX; not the reference's, so never the headline line)")
     ap.add_argument("--no-save", action="store_true", help="sample without saving records (SURVEY.md 8(d) "
                     "asks for both; the default saves one record per call, as the reference's sampling phase)")
     args = ap.parse_args()
@@ -199,7 +201,7 @@ def main():
     chain_ids = list(sd.shard(C * world, world, rank))
     seeds = [i + 1 for i in chain_ids]
     sess = sa.Session(ds, seeds, device=local_rank, calls_per_launch=args.calls_per_step,
-                      block_threads=args.block_threads, chain_ids=chain_ids, columns=args.columns)
+                      block_threads=args.block_threads, chain_ids=chain_ids, columns=args.columns, rng=args.rng)
     stream = torch.cuda.current_stream()
     sess.set_stream(stream.cuda_stream)
     cps = args.calls_per_step
@@ -285,6 +287,7 @@ def main():
                            ds.N, ds.M, C, cps, sweeps_per_step),
             "sites": ds.N, "taxa": ds.M, "chains": total_chains, "chains_per_gpu": C,
             "sweeps_per_step": sweeps_per_step, "block_threads": sess.block_threads, "columns": sess.variant,
+            "rng": "GSL MT19937 (the reference's stream)" if args.rng == "mt" else "Philox4x32-10 (opt-in)",
             "parallelism": "chains sharded over %d GPU(s), RCCL all-gather at end" % world,
         },
         "roofline": {

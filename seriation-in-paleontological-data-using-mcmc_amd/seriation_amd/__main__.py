@@ -6,7 +6,7 @@ whole job at once and writes the same ``Chains/chain_NN`` tree:
 
     python -m seriation_amd DATASET [--chains 100] [--burnin 1000] [--samples 1000] [--thin 10]
                                     [--seed-base S] [--devices 0,1] [--root .] [--select K]
-                                    [--no-save] [--debug-check]
+                                    [--no-save] [--debug-check] [--rng mt|philox]
 
   --thin        sweeps per saved sample (the reference's mcmc_sample runs 10, mcmc.c:225)
   --seed-base   chain k gets seed S + k; omitted -> unique 1-byte urandom seeds like
@@ -14,6 +14,8 @@ whole job at once and writes the same ``Chains/chain_NN`` tree:
   --select K    after the run, the one-sigma selection of choose_chains (script.py:70-98) over
                 the written exp_data.csv files; prints the chosen chain indices
   --no-save     sample without writing files; prints one JSON summary per chain
+  --rng         mt: GSL MT19937 as the reference (default); philox: the opt-in counter-based
+                Philox4x32-10 stream for sampling (statistically equivalent, not bit-equal)
   --debug-check mcmc_consistent on every chain after every mcmc_sample call (the reference's
                 MCMCDEBUG build, mcmc.c:249-255); with --no-save
 
@@ -41,6 +43,7 @@ def main(argv=None):
     ap.add_argument("--select", type=int, default=0)
     ap.add_argument("--no-save", action="store_true")
     ap.add_argument("--debug-check", action="store_true")
+    ap.add_argument("--rng", default="mt", choices=("mt", "philox"))
     a = ap.parse_args(argv)
     if a.chains < 1 or a.burnin < 0 or a.samples < 0 or a.thin < 1:
         ap.error("--chains and --thin must be >= 1, --burnin and --samples >= 0")
@@ -58,7 +61,8 @@ def main(argv=None):
         ds = core.Dataset.load(a.dataset)
         t0 = time.perf_counter()
         summ, _ = core.run_chains(ds, seeds, burnin_calls=a.burnin, sample_calls=a.samples,
-                                  sweeps_per_call=a.thin, devices=devices[:len(seeds)], debug_check=a.debug_check)
+                                  sweeps_per_call=a.thin, devices=devices[:len(seeds)], debug_check=a.debug_check,
+                                  rng=a.rng)
         wall = time.perf_counter() - t0
         for s in summ:
             print(json.dumps(s))
@@ -66,7 +70,7 @@ def main(argv=None):
     else:
         summ = launcher.run_all_chains(a.dataset, n_chains=a.chains, seeds=seeds, devices=devices,
                                        burnin_calls=a.burnin, sample_calls=a.samples, root=a.root,
-                                       sweeps_per_call=a.thin)
+                                       sweeps_per_call=a.thin, rng=a.rng)
         if a.select:
             print("selected:", " ".join(str(k) for k in launcher.choose_chains(a.select, a.root)))
     return 1 if any(s.get("consistent", 0) for s in summ) else 0

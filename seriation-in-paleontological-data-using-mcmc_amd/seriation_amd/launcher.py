@@ -42,7 +42,7 @@ def run_chain(chain_index, old_seeds, dataset, burnin_calls=1000, sample_calls=1
 
 
 def run_all_chains(dataset, n_chains=100, seeds=None, devices=None, burnin_calls=1000, sample_calls=1000,
-                   root=".", verbose=True, sweeps_per_call=10):
+                   root=".", verbose=True, sweeps_per_call=10, rng="mt"):
     """script.py:48-67: run all chains and print the wall time (seconds, 2 decimals).
 
     seeds: None -> unique 1-byte urandom seeds exactly like the reference (only 256 exist, so
@@ -59,7 +59,7 @@ def run_all_chains(dataset, n_chains=100, seeds=None, devices=None, burnin_calls
     start = time.perf_counter()
     devices = devices[:len(seeds)]
     summ = core.run_to_dirs(ds, seeds, root=root, chain_ids=list(range(len(seeds))), burnin_calls=burnin_calls,
-                            sample_calls=sample_calls, sweeps_per_call=sweeps_per_call, devices=devices)
+                            sample_calls=sample_calls, sweeps_per_call=sweeps_per_call, devices=devices, rng=rng)
     finish = time.perf_counter()
     if verbose:
         print(round(finish - start, 2))

@@ -53,7 +53,8 @@ def main():
     ap.add_argument("run")
     ap.add_argument("prefix")
     ap.add_argument("--warmup", type=int, default=1, help="untimed launches at the start of each PMC pass")
-    ap.add_argument("--trace-warmup", type=int, default=3, help="untimed launches in the kernel-trace run")
+    ap.add_argument("--trace-timed", type=int, default=20, help="timed launches of the kernel-trace run: its last N "
+                    "sr_sweep_kernel launches (bench.py --steps; the warm-up launches come first)")
     args = ap.parse_args()
 
     res = {"kernel": None, "source": args.run,
@@ -67,10 +68,25 @@ def main():
     if trace:
         durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(trace))
                 if KERNEL in r["Kernel_Name"]]
-        timed = durs[args.trace_warmup:]
+        timed = durs[-args.trace_timed:]
         res["trace"] = {"launches": len(durs), "timed_launches": len(timed),
                         "avg_ns_timed": statistics.mean(timed) if timed else None,
+                        "min_ns_timed": min(timed) if timed else None, "max_ns_timed": max(timed) if timed else None,
                         "avg_ns_all": statistics.mean(durs) if durs else None}
+        # the bench line printed by the profiled run itself (same command as the bench)
+        plog = os.path.join(args.run, "prof.log")
+        if os.path.exists(plog):
+            for ln in open(plog):
+                if ln.startswith("{") and '"metric"' in ln:
+                    b = json.loads(ln)
+                    res["trace"]["profiled_run_bench"] = {"value": b["value"], "ms_per_step": b["ms_per_step"],
+                                                          "kernel_ms_hip_events": b["roofline"]["kernel_ms"]}
+        if timed:
+            with open(args.prefix + "_kernel_stats_timed.csv", "w") as fh:
+                fh.write('"Name","Calls","AverageNs","MinNs","MaxNs","StdDev","Note"\n')
+                fh.write('"%s",%d,%.1f,%d,%d,%.1f,"the %d timed launches of the profiled bench run (warm-up dropped)"\n'
+                         % (KERNEL, len(timed), statistics.mean(timed), min(timed), max(timed),
+                            statistics.pstdev(timed), len(timed)))
     fetch = find(os.path.join(args.run, "pmc_fetch"), "counter_collection.csv")
     write = find(os.path.join(args.run, "pmc_write"), "counter_collection.csv")
     if fetch and write:

@@ -1427,8 +1427,11 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   }
   if (tid == 0) for (int k = 0; k < 7; ++k) misc[MS_ACC + k] = 0;
   int rcur = 0;     /* current rpi buffer */
-  uint32_t hbc = 0;       /* own taxon's column bits at the hard positions (one-taxon kernels), */
-  bool hb_dirty = true;   /* recomputed after an accepted pi1 / pi2 (block-uniform flag) */
+  /* own taxon's column bits at the hard sites, bit k = hard site k in position order (one-taxon
+     kernels).  Invariant for the whole run: every move that would change the hard sites' relative
+     order is vetoed (mcmc.c:1153-1160, 1343-1348; pi3 moves non-hard sites only), so position hp[k]
+     always holds the same site and its bits travel with it. */
+  uint32_t hbc = 0;
   int par = 0;      /* parity of the double-buffered totals */
   int bpar = 0;     /* parity of the double-buffered proposal count sums */
   int xpar = 0;     /* parity of the double-buffered exact-delta term lists */
@@ -1436,6 +1439,10 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 
   build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane);
   for (int m = tid; m < M; m += TB) col_pre_build(pre + m, P + m, M, NW);   /* own columns */
+  {
+    const int hl0 = (lane < nh) ? hp[lane] : 0;   /* loaded with every lane active */
+    if (M <= TB && tid < M) hbc = hard_bits_col(P + tid, M, hl0, nh);
+  }
   const double ec = sr_exp_m(SR_LOGEPSILON, &tb);
   const uint32_t nhard = (uint32_t)nh;
   const UDivM mdN = make_udivm((uint32_t)N), mdN1 = make_udivm((uint32_t)(N - 1)), md2 = make_udivm(2u);
@@ -1620,22 +1627,28 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           const uint32_t rgen = __builtin_amdgcn_readfirstlane(R.gen);
           const int avail = min((int)((rgen - rblk) * SR_MT_N - roff), 128);   /* resident words, <= 2 per lane */
           const uint32_t base = (rblk & (SR_RING - 1)) * SR_MT_N + roff;
-          /* the batch's next 128 tempered words: word k in lane k & 63 of vw[k >> 6] */
-          uint32_t vw0, vw1;
-          {
+          /* the batch's next 128 tempered words for the scalar path (word k in lane k & 63 of
+             vw[k >> 6]), loaded only when a proposal takes that path: the swap batch, or a fast-path
+             stop (block-uniform flag) */
+          uint32_t vw0 = 0u, vw1 = 0u;
+          bool vw_ok = false;
+          auto need_vw = [&]() {
+            if (vw_ok) return;
             uint32_t i0 = base + (uint32_t)lane, i1 = base + 64u + (uint32_t)lane;
             i0 = (i0 >= SR_RING * SR_MT_N) ? i0 - SR_RING * SR_MT_N : i0;
             i1 = (i1 >= SR_RING * SR_MT_N) ? i1 - SR_RING * SR_MT_N : i1;
             i1 = (i1 >= SR_RING * SR_MT_N) ? i1 - SR_RING * SR_MT_N : i1;
             vw0 = sr_mt_temper(ring[i0]);
             vw1 = sr_mt_temper(ring[i1]);
-          }
+            vw_ok = true;
+          };
           FST(14);
           STAMP_D(3);
           int off = 0, pend = p0;
           /* one proposal drawn by block-uniform scalar code at word offset `off` (false: not enough
              resident words) */
           auto scalar_one = [&](int p) -> bool {
+              need_vw();
               const int kind = prop_kind(p);
               bool bad = false;
               auto word = [&](void) -> uint32_t {
@@ -1846,7 +1859,6 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           /* own taxon's limits and hard-site bits, fixed for the batch (one taxon per thread) */
           const bool one = M <= TB;
           int a1 = 0, b1 = 0;
-          if (hb_dirty && one) { if (tid < M) hbc = hard_bits_col(P + tid, M, hl, nh); hb_dirty = false; }
           const uint32_t hb1 = hbc;
           if (one && tid < M) { a1 = sab[tid]; b1 = sab[M + tid]; }
           FST(13);
@@ -2132,10 +2144,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             rcur ^= 1;
           }
           FST(10);
-          /* the hard tables only when a hard site moved; the columns' hard-site bits after any
-             pi1 / pi2 (the bits at the hard positions move with the sites) */
+          /* the hard tables only when a hard site moved (the columns' hard-site bits never change) */
           if (hmoved) { wsync(); build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane); }
-          if (kind != PK_PI3) hb_dirty = true;
           FST(9);
           wsync();
           STAMP(7);

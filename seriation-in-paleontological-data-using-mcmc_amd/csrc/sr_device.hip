@@ -59,7 +59,7 @@ struct KArgs {
 
 /* ---------------------------------------------------------------- LDS carve */
 struct Lay {
-  size_t tab, cbuf, lbuf, mt, P, rpi0, rpi1, ht, ck, ccnt, sab, scnt, hpw, hbw, t4, t8, pre, part, tot, xs, misc, total;
+  size_t tab, cbuf, lbuf, mt, P, rpi0, rpi1, ht, ck, ccnt, sab, scnt, hpw, hbw, t4, t8, pre, part, tot, xs, ptab, misc, total;
 };
 __host__ __device__ static inline size_t sr_al16(size_t x) { return (x + 15) & ~(size_t)15; }
 /* walk words held in registers by the register-column kernels (NWM template argument): 9 for
@@ -100,6 +100,7 @@ __host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB, bo
   L.part = o;  o = sr_al16(o + (size_t)2 * 16 * NWV * 8 * 4);         /* [2][proposal][wave] count sums */
   L.tot = o;   o = sr_al16(o + (size_t)2 * NWV * 4 * 4);               /* [2][wave] t0, f0, t1, f1 */
   L.xs = o;    o = sr_al16(o + (size_t)NWV * sizeof(double));          /* per-wave broadcast slot */
+  L.ptab = o;  o = sr_al16(o + 4 * 128 * 4);                          /* lane-parallel proposal tables (shared) */
   L.misc = o;  o = sr_al16(o + 64 * 8);
   L.total = o;
   return L;
@@ -1386,6 +1387,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   int *tot = (int *)(smem + L.tot);
   double *xs = (double *)(smem + L.xs) + wave;
   uint64_t *misc = (uint64_t *)(smem + L.misc);
+  uint32_t *ptab = (uint32_t *)(smem + L.ptab);   /* [4][128]: pi1, pi2, pi3 records and pi3 ranks per word offset */
 
   /* ---- load tables and state */
   for (int i = tid; i < 256; i += TB) {
@@ -1618,6 +1620,11 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       {
         int vi = 0, vj = 0, vfl = 4, vkn = 0, vuw = 1, vnd = 0, voff = 0, vr0 = 0;   /* lane p: proposal p */
         int p0 = 0;
+        /* the lane-parallel proposal tables (ptab) hold "a proposal of each kind starting at word o"
+           for the 128 words from stream position (tblk, toff); a later batch of the sweep reuses them
+           while its proposals stay inside those words and no hard site moved (block-uniform state) */
+        uint32_t tblk = 0u, toff = 0u;
+        bool tvalid = false;
         while (p0 < 16) {
           p0 = __builtin_amdgcn_readfirstlane(p0);   /* block-uniform: keep the control flow scalar */
           const int hl = (lane < nh) ? hp[lane] : 0;  /* lane k: hard position k */
@@ -1717,61 +1724,62 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           if (p0 == 0) (void)scalar_one(0);
           if (p0 > 0) {
             /* Lane-parallel draws: lane l evaluates "a pi1 / pi2 / pi3 proposal starting at word
-               offset o" for o = l and o = l + 64 (words o..o+4); the scan below then walks the
-               batch's actual offsets reading those results.  ok = no GSL rejection and a nonzero
-               uniform_pos word (else the scalar path below takes over at that proposal). */
-            uint32_t rA1[2] = {0u, 0u}, rA2[2] = {0u, 0u}, rA3[2] = {0u, 0u}, rB3[2] = {0u, 0u}, rU1[2] = {0u, 0u},
-                     rU2[2] = {0u, 0u};
-            /* the second 64 offsets only when the batch's proposals can reach them (<= 5 words each) */
-            const int nh2 = (5 * (16 - p0) + 5 <= 64) ? 1 : 2;
+               offset o" for o = l and o = l + 64 (words o..o+4) into ptab; the scan below then walks
+               the batch's actual offsets reading those results.  ok = no GSL rejection and a nonzero
+               uniform_pos word (else the scalar path below takes over at that proposal).  The tables
+               are shared by the waves: every wave writes the same values (block-uniform inputs), and
+               no wave reads them past the batch barrier that every wave's next write follows. */
+            int delta = tvalid ? (int)((rblk - tblk) * SR_MT_N + roff) - (int)toff : 0;
+            if (!tvalid || delta + 5 * (16 - p0) + 5 > 128) {
+              delta = 0;
+              tblk = rblk; toff = roff; tvalid = true;
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              if (h >= nh2) break;
-              const int o = lane + 64 * h;
-              uint32_t w[5];
+              for (int h = 0; h < 2; ++h) {
+                const int o = lane + 64 * h;
+                uint32_t w[5];
 #pragma unroll
-              for (int k = 0; k < 5; ++k) {
-                uint32_t idx = base + (uint32_t)min(o + k, avail - 1);
-                idx = (idx >= SR_RING * SR_MT_N) ? idx - SR_RING * SR_MT_N : idx;
-                w[k] = sr_mt_temper(ring[idx]);
+                for (int k = 0; k < 5; ++k) {
+                  uint32_t idx = base + (uint32_t)min(o + k, avail - 1);
+                  idx = (idx >= SR_RING * SR_MT_N) ? idx - SR_RING * SR_MT_N : idx;
+                  w[k] = sr_mt_temper(ring[idx]);
+                }
+                const bool in = o + 5 <= avail;
+                const uint32_t qN = udivm_v(w[0], mdN.m, mdN.l), qN1 = udivm_v(w[1], mdN1.m, mdN1.l);
+                const uint32_t qa = udivm_v(w[2], md2.m, md2.l), qb = udivm_v(w[3], md2.m, md2.l);
+                const bool okN = in && qN < mdN.n && qN1 < mdN1.n;
+                const bool okab = qa < 2u && qb < 2u;
+                /* pi1 (mcmc.c:1133-1160): words o, o+1, uniform_pos at o+2 */
+                {
+                  const int i = (int)qN, j = (int)qN1 + ((int)qN1 >= (int)qN ? 1 : 0);
+                  const int ic = min(i, N - 1), jc = min(j, N - 1);
+                  const bool veto = (hcnt[ic + 1] != hcnt[ic]) && (hcnt[max(ic, jc) + 1] - hcnt[min(ic, jc)] > 1);
+                  const bool ok = okN && (veto || w[2] != 0u);
+                  ptab[o] = (uint32_t)ic | ((uint32_t)jc << 11) | (veto ? 1u << 22 : 0u) | (ok ? 1u << 23 : 0u);
+                }
+                /* pi2 (mcmc.c:1317-1364): words o, o+1, [o+2, o+3 inc], uniform_pos at o+4 */
+                {
+                  int i = (int)qN, j = (int)qN1;
+                  if (j >= i) j++; else { const int t = i; i = j; j = t; }
+                  const int ic = min(i, N - 1), jc = min(j, N - 1);
+                  const bool veto = hcnt[jc + 1] - hcnt[ic] > 1;
+                  const bool ok = okN && (veto || (okab && w[4] != 0u));
+                  ptab[128 + o] = (uint32_t)ic | ((uint32_t)jc << 11) | (veto ? 1u << 22 : 0u) | (ok ? 1u << 23 : 0u) |
+                                  (qa << 24) | (qb << 25);
+                }
+                /* pi3 (mcmc.c:1495-1565): words o..o+3, uniform_pos at o+4 */
+                {
+                  const uint32_t qH = udivm_v(w[0], mdH.m, mdH.l), qH1 = udivm_v(w[1], mdH1.m, mdH1.l);
+                  int ri, rj;
+                  if ((int)qH <= (int)qH1) { ri = (int)qH; rj = (int)qH1 + 1; } else { ri = (int)qH1; rj = (int)qH; }
+                  const int NH = N - nh;
+                  ri = min(ri, max(NH - 1, 0)); rj = min(rj, max(NH - 1, 0));
+                  const int i = nhall[ri], j = nhall[rj];
+                  const bool ok = in && NH >= 2 && qH < mdH.n && qH1 < mdH1.n && okab && w[4] != 0u;
+                  ptab[256 + o] = (uint32_t)i | ((uint32_t)j << 11) | (ok ? 1u << 23 : 0u) | (qa << 24) | (qb << 25);
+                  ptab[384 + o] = (uint32_t)ri | ((uint32_t)(rj - ri + 1) << 16);
+                }
               }
-              const bool in = o + 5 <= avail;
-              const uint32_t qN = udivm_v(w[0], mdN.m, mdN.l), qN1 = udivm_v(w[1], mdN1.m, mdN1.l);
-              const uint32_t qa = udivm_v(w[2], md2.m, md2.l), qb = udivm_v(w[3], md2.m, md2.l);
-              const bool okN = in && qN < mdN.n && qN1 < mdN1.n;
-              const bool okab = qa < 2u && qb < 2u;
-              /* pi1 (mcmc.c:1133-1160): words o, o+1, uniform_pos at o+2 */
-              {
-                const int i = (int)qN, j = (int)qN1 + ((int)qN1 >= (int)qN ? 1 : 0);
-                const int ic = min(i, N - 1), jc = min(j, N - 1);
-                const bool veto = (hcnt[ic + 1] != hcnt[ic]) && (hcnt[max(ic, jc) + 1] - hcnt[min(ic, jc)] > 1);
-                const bool ok = okN && (veto || w[2] != 0u);
-                rA1[h] = (uint32_t)ic | ((uint32_t)jc << 11) | (veto ? 1u << 22 : 0u) | (ok ? 1u << 23 : 0u);
-                rU1[h] = w[2];
-              }
-              /* pi2 (mcmc.c:1317-1364): words o, o+1, [o+2, o+3 inc], uniform_pos at o+4 */
-              {
-                int i = (int)qN, j = (int)qN1;
-                if (j >= i) j++; else { const int t = i; i = j; j = t; }
-                const int ic = min(i, N - 1), jc = min(j, N - 1);
-                const bool veto = hcnt[jc + 1] - hcnt[ic] > 1;
-                const bool ok = okN && (veto || (okab && w[4] != 0u));
-                rA2[h] = (uint32_t)ic | ((uint32_t)jc << 11) | (veto ? 1u << 22 : 0u) | (ok ? 1u << 23 : 0u) |
-                         (qa << 24) | (qb << 25);
-                rU2[h] = w[4];
-              }
-              /* pi3 (mcmc.c:1495-1565): words o..o+3, uniform_pos at o+4 */
-              {
-                const uint32_t qH = udivm_v(w[0], mdH.m, mdH.l), qH1 = udivm_v(w[1], mdH1.m, mdH1.l);
-                int ri, rj;
-                if ((int)qH <= (int)qH1) { ri = (int)qH; rj = (int)qH1 + 1; } else { ri = (int)qH1; rj = (int)qH; }
-                const int NH = N - nh;
-                ri = min(ri, max(NH - 1, 0)); rj = min(rj, max(NH - 1, 0));
-                const int i = nhall[ri], j = nhall[rj];
-                const bool ok = in && NH >= 2 && qH < mdH.n && qH1 < mdH1.n && okab && w[4] != 0u;
-                rA3[h] = (uint32_t)i | ((uint32_t)j << 11) | (ok ? 1u << 23 : 0u) | (qa << 24) | (qb << 25);
-                rB3[h] = (uint32_t)ri | ((uint32_t)(rj - ri + 1) << 16);
-              }
+              wsync();
             }
             FST(15);
             /* scan, two steps.  (1) the offset chain: proposal p starts where p-1 ended; a 5-bit
@@ -1782,9 +1790,12 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             uint32_t lent = 0;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-              const uint32_t e = ((rA1[h] >> 23) & 1u) | ((((rA1[h] >> 22) & 1u) ^ 1u) << 1) | (((rA2[h] >> 23) & 1u) << 2) |
-                                 (((rA2[h] >> 22) & 1u) << 3) | (((rA3[h] >> 23) & 1u) << 4);
-              lent |= e << (16 * h);
+              const int t = delta + lane + 64 * h;   /* table index of batch offset lane + 64 h */
+              const int tc = min(t, 127);
+              const uint32_t a1 = ptab[tc], a2 = ptab[128 + tc], a3 = ptab[256 + tc];
+              const uint32_t e = ((a1 >> 23) & 1u) | ((((a1 >> 22) & 1u) ^ 1u) << 1) | (((a2 >> 23) & 1u) << 2) |
+                                 (((a2 >> 22) & 1u) << 3) | (((a3 >> 23) & 1u) << 4);
+              lent |= (t < 128 ? e : 0u) << (16 * h);   /* past the tables: not ok (scalar path) */
             }
             const int sstart = pend;
             int vstart = 0;
@@ -1804,17 +1815,14 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               pend = sI + 1;
             }
             {
-              const int o = vstart, src = o & 63;
-              const bool hi = o >= 64;
+              const int o = vstart;
               const int kind = prop_kind(lane & 15);
-              auto g = [&](const uint32_t (&t)[2]) -> uint32_t {
-                const uint32_t a = (uint32_t)__shfl((int)t[0], src), b = (uint32_t)__shfl((int)t[1], src);
-                return hi ? b : a;
-              };
-              const uint32_t g1 = g(rA1), g2 = g(rA2), g3 = g(rA3), gb = g(rB3), gu1 = g(rU1), gu2 = g(rU2);
-              const uint32_t ra = (kind == PK_PI1) ? g1 : (kind == PK_PI2) ? g2 : g3;
-              const uint32_t rb = (kind == PK_PI3) ? gb : 0u;
-              const uint32_t ru = (kind == PK_PI1) ? gu1 : gu2;
+              const int tc = min(delta + o, 127);
+              const uint32_t ra = ptab[(kind == PK_PI1 ? 0 : (kind == PK_PI2 ? 128 : 256)) + tc];
+              const uint32_t rb = (kind == PK_PI3) ? ptab[384 + tc] : 0u;
+              uint32_t iu = base + (uint32_t)min(o + (kind == PK_PI1 ? 2 : 4), avail - 1);   /* the uniform_pos word */
+              iu = (iu >= SR_RING * SR_MT_N) ? iu - SR_RING * SR_MT_N : iu;
+              const uint32_t ru = sr_mt_temper(ring[iu]);
               const bool veto = (ra >> 22) & 1u;
               const int nd = o + (kind == PK_PI1 ? 2 : (kind == PK_PI2 ? (veto ? 2 : 4) : 4));
               if (lane >= sstart && lane < pend) {
@@ -1839,6 +1847,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           STAMP_D(4);
           if (pend == p0) {   /* not enough resident words for one proposal: make more, retry */
             rng_ensure(R, min(avail + 256, (SR_RING - 1) * SR_MT_N - (SR_MT_N - 1)), tid, TB);
+            tvalid = false;
             continue;
           }
           auto load_prop = [&](int p) -> Prop {
@@ -2145,7 +2154,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           }
           FST(10);
           /* the hard tables only when a hard site moved (the columns' hard-site bits never change) */
-          if (hmoved) { wsync(); build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane); }
+          if (hmoved) { wsync(); build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane); tvalid = false; }
           FST(9);
           wsync();
           STAMP(7);

@@ -53,9 +53,10 @@ def algorithmic_bytes_per_iter(N, M):
 
 
 def measured_traffic(N, M, chains, sweeps_per_step):
-    """HBM bytes per sweep-kernel launch from the newest PMC summary in profiles/ whose workload
+    """HBM bytes per sweep-kernel launch from the latest round's PMC summary in profiles/ whose workload
     matches (tools/pmc_summary.py: 2*FETCH_SIZE + WRITE_SIZE from separate rocprofv3 --pmc passes
-    over this bench).  None when no matching PMC pass exists."""
+    over this bench; rounds are ordered by file name, r01c < ... < r02g, not by mtime, which a checkout
+    or a copy to the GPU box does not keep).  None when no matching PMC pass exists."""
     import glob
     best = None
     for p in glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")):
@@ -66,8 +67,8 @@ def measured_traffic(N, M, chains, sweeps_per_step):
             if (w.get("sites"), w.get("taxa"), w.get("chains_per_gpu"), w.get("sweeps_per_step")) != \
                     (N, M, chains, sweeps_per_step) or "traffic_bytes_per_launch" not in t:
                 continue
-            if best is None or os.path.getmtime(p) > best[0]:
-                best = (os.path.getmtime(p), p, t)
+            if best is None or os.path.basename(p) > best[0]:
+                best = (os.path.basename(p), p, t)
         except (OSError, ValueError):
             continue
     if best is None:

@@ -901,8 +901,11 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
      Byte steps: T8[byte] = {sum of the byte's 8 prefix products, their product}; T8[256] =
      {0, 1} is the dead entry, read for every byte outside the window or not wholly inside the
      walk (it leaves S and y unchanged), so no step needs a select.  A word's 4 entries are read
-     together (one LDS round trip per word).  The walk's partial last byte ((L + 1) mod 8
-     entries) follows from the 4-entry tables (T4 rows c = 0..4). */
+     together (one LDS round trip per word) and summed in Horner form, W = s0 + p0 (s1 + p1 (s2 +
+     p2 s3)), y *= (p0 p1)(p2 p3): the y chain takes one multiply per word (dead entries are
+     trailing, so W and the product stay exact for them); each entry's value keeps at most as many
+     roundings as the byte-by-byte chain it replaces, inside REL.  The walk's partial last byte
+     ((L + 1) mod 8 entries) follows from the 4-entry tables (T4 rows c = 0..4). */
   const double y0 = exp2_split(qlo);
   double S = 0.0;
   double ckr[NWM], yst[NWM];
@@ -924,10 +927,13 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
     for (int k = 0; k < NWM; ++k) {
       if (k + 1 < NWM) wload(k + 1, tn);   /* next word's reads in flight while this word is summed */
       yst[k] = y;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        S = __builtin_fma(y, t[g].x, S);
-        y = y * t[g].y;
+      {   /* the word's 4 byte steps in Horner form: one multiply on the y chain per word */
+        const double w23 = __builtin_fma(t[2].y, t[3].x, t[2].x);
+        const double w13 = __builtin_fma(t[1].y, w23, t[1].x);
+        const double W = __builtin_fma(t[0].y, w13, t[0].x);
+        const double pw = (t[0].y * t[1].y) * (t[2].y * t[3].y);
+        S = __builtin_fma(y, W, S);
+        y = y * pw;
       }
       ckr[k] = S;
 #pragma unroll
@@ -1892,7 +1898,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 int dt0 = 0, dt1 = 0;
                 if (tid < M) taxon_dt(prop_kind(sI), q, a1, b1, P + tid, pre + tid, M, hb1, hcnt, nhall, dt0, dt1);
                 d0s[sI] = dt0; d1s[sI] = dt1;
-                nzs[sI] = __popcll(__ballot((dt0 | dt1) != 0));
+                if (prop_kind(sI) != PK_PI1) nzs[sI] = __popcll(__ballot((dt0 | dt1) != 0));
               }
             }
             FST(3);
@@ -1901,10 +1907,11 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               const int fl = __builtin_amdgcn_readlane(vfl, sI);
               if (sI >= p0 && sI < pend && !(fl & 4)) {
                 int X0, X1, Y0, Y1;
-                if (prop_kind(sI) == PK_PI1) {   /* pi1: dt in {-1, 0, 1}: |dt| sums are ballot counts */
-                  const uint32_t u1 = (uint32_t)wave_sum_i32((int)((uint32_t)(d0s[sI] + 1) | ((uint32_t)(d1s[sI] + 1) << 16)));
-                  X0 = (int)(u1 & 0xffffu) - 64; X1 = (int)(u1 >> 16) - 64;
-                  Y0 = (int)__popcll(__ballot(d0s[sI] != 0)); Y1 = (int)__popcll(__ballot(d1s[sI] != 0));
+                if (prop_kind(sI) == PK_PI1) {   /* pi1: dt in {-1, 0, 1} and dt0 dt1 = 0: every sum is a ballot count */
+                  const int cp0 = (int)__popcll(__ballot(d0s[sI] > 0)), cn0 = (int)__popcll(__ballot(d0s[sI] < 0));
+                  const int cp1 = (int)__popcll(__ballot(d1s[sI] > 0)), cn1 = (int)__popcll(__ballot(d1s[sI] < 0));
+                  X0 = cp0 - cn0; X1 = cp1 - cn1; Y0 = cp0 + cn0; Y1 = cp1 + cn1;
+                  nzs[sI] = Y0 + Y1;
                 } else if (pack) {   /* per-wave sums of (dt + N) and |dt| fit 16-bit fields (N < 512) */
                   const uint32_t u1 = (uint32_t)wave_sum_i32((int)((uint32_t)(d0s[sI] + N) | ((uint32_t)(d1s[sI] + N) << 16)));
                   const uint32_t u2 = (uint32_t)wave_sum_i32((int)((uint32_t)abs(d0s[sI]) | ((uint32_t)abs(d1s[sI]) << 16)));

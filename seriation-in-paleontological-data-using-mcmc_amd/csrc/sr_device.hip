@@ -864,18 +864,26 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
 {
   const int POo = walk_prefix_s<NWM>(wk, o);
   const int nk = (L >> 5) + 1;
-  /* pass 0: window of words that can hold mass above 2^-40 relative to entry o */
+  /* pass 0: window of words that can hold mass above 2^-40 relative to entry o.  q at a word
+     start w0 is F(o) - F(w0), F(w) = zeros before w * vA + ones before w * vB = w vA + O(w) (vB - vA)
+     (the window only bounds the skipped mass: the pick is certified independently of it). */
   int klo = NWM, khi = -1;
   double qlo = 0.0;
   {
-    int O = 0;
+    const double dv = vB - vA;
+    const double Fo = __builtin_fma((double)POo, dv, (double)o * vA);
+    int O = 0;   /* ones among walk entries [0, 32k) */
 #pragma unroll
     for (int k = 0; k < NWM; ++k) {
       const int nb = min(32, L + 1 - 32 * k);
       const uint32_t vm = (nb >= 32) ? 0xffffffffu : ((nb > 0) ? ((1u << nb) - 1u) : 0u);
-      const int w0 = 32 * k;
-      const double qs = (w0 <= o) ? ((double)((o - w0) - (POo - O)) * vA + (double)(POo - O) * vB)
-                                  : -((double)((w0 - o) - (O - POo)) * vA + (double)(O - POo) * vB);
+      double qs;
+      if constexpr (NWM <= 9) qs = Fo - __builtin_fma((double)O, dv, (double)(32 * k) * vA);
+      else {   /* the 17-word walks keep the two-sided form: the F form spills there (+9 % kernel time at N = 400) */
+        const int w0 = 32 * k;
+        qs = (w0 <= o) ? ((double)((o - w0) - (POo - O)) * vA + (double)(POo - O) * vB)
+                       : -((double)((w0 - o) - (O - POo)) * vA + (double)(O - POo) * vB);
+      }
       const int ones = __popc(wk[k] & vm);
       const double ub = qs - (double)(nb - ones) * vA;
       const bool in = (k < nk) && ub > -SR_WIN_T;

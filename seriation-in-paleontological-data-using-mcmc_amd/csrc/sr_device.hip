@@ -858,11 +858,11 @@ __device__ __forceinline__ int walk_prefix_s(const uint32_t (&wk)[NWM], int w)
  * Same approximation and certification as draw_fast; fallback to draw_exact on failure. */
 template <int NWM>
 __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint32_t *Pm, int M, int N, bool rev, int o,
-                                           int L, double u, const CD &K, const sr_mtab &tb, double vA, double vB,
+                                           int L, int POo, double u, const CD &K, const sr_mtab &tb, double vA, double vB,
                                            const double *T4, const double *T8, uint64_t *fbk, int &dt0, int &df0, int &dt1,
                                            int &df1)
 {
-  const int POo = walk_prefix_s<NWM>(wk, o);
+  /* POo: ones among walk entries [0, o), from the caller's column prefix table */
   const int nk = (L >> 5) + 1;
   /* pass 0: window of words that can hold mass above 2^-40 relative to entry o.  q at a word
      start w0 is F(o) - F(w0), F(w) = zeros before w * vA + ones before w * vB = w vA + O(w) (vB - vA)
@@ -961,7 +961,7 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
     S = __builtin_fma(y * tlo.y, shi, S);
   }
   /* pass 2: locate the word, then the group and entry where u falls; certify */
-  int res = -1;
+  int res = -1, POp = 0;   /* the pick and the ones among walk entries [0, pick) */
   if (S > 0.0 && S < 0x1p1000) {
     const double inv = 1.0 / S;
     const double REL = (double)(N + 33) * 0x1p-50;   /* + the byte tables' own rounding (<= 16 ulp per entry) */
@@ -971,10 +971,12 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
     for (int k = 0; k < NWM; ++k) j += (k >= klo && k < khi && ckr[k] * inv < u) ? 1 : 0;
     double Sp0 = 0.0, y = yst[0];
     uint32_t ww = wk[0];
+    [[maybe_unused]] int Oj = 0, Ok = 0;   /* ones among walk entries [0, 32 j) (9-word walks) */
 #pragma unroll
     for (int k = 0; k < NWM; ++k) {
-      if (k == j) { y = yst[k]; ww = wk[k]; }
+      if (k == j) { y = yst[k]; ww = wk[k]; Oj = Ok; }
       if (k + 1 == j && j > klo) Sp0 = ckr[k];
+      if constexpr (NWM <= 9) Ok += __popc(wk[k]);
     }
     const int w0 = 32 * j;
     const int nb = min(32, L + 1 - w0);
@@ -1026,7 +1028,11 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
     const bool prev_ok = (w == 0) || (tprev > eprev);
     const bool here_ok = (w == L) || (t < -e);
 #ifndef SR_FORCE_EXACT
-    if (prev_ok && here_ok) res = w;
+    if (prev_ok && here_ok) {
+      res = w;
+      if constexpr (NWM <= 9) POp = Oj + __popc(ww & ((1u << (w & 31)) - 1u));
+      else POp = walk_prefix_s<NWM>(wk, res);   /* (the tracked form spills in the 17-word kernel) */
+    }
 #else   /* test build: every Gibbs draw takes the exact three-pass walk */
     (void)prev_ok; (void)here_ok; (void)w;
 #endif
@@ -1034,9 +1040,9 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
   if (res < 0) {
     atomicAdd((unsigned long long *)fbk, 1ull);   /* exact-walk fallbacks (rare: counted always) */
     res = draw_exact(Pm, M, N, rev, o, L, u, K, tb);
+    POp = walk_prefix_s<NWM>(wk, res);
   }
   /* count deltas at the pick (the dt arrays of mcmc_auxa) */
-  const int POp = walk_prefix_s<NWM>(wk, res);
   if (res == o) { dt0 = df0 = dt1 = df1 = 0; }
   else if (res < o) { int O = POo - POp; int Z = (o - res) - O; dt0 = -Z; df0 = Z; dt1 = O; df1 = -O; }
   else { int O = POp - POo; int Z = (res - o) - O; dt0 = Z; df0 = -Z; dt1 = -O; df1 = O; }
@@ -1568,6 +1574,11 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           if constexpr (NWM > 0) {   /* column in registers, branch-free draws */
             uint32_t wk[NWM];   /* forward walk words, then (second trip) the reversed ones */
             load_fwd<NWM>(Pm, M, NW, wk);
+            /* ones before each trip's start entry from the column prefix table: forward, positions
+               [0, a0); reversed, walk entries [0, N - b0) = positions [b0, N) */
+            const uint16_t *prem = pre + m;
+            const int POa = col_pre(prem, Pm, M, a0);
+            const int POb = (int)prem[NW * M] - col_pre(prem, Pm, M, b0);
             for (int pass = 0; pass < 2; ++pass) {
               int d0, e0, d1, e1;
               const bool rev = pass != 0;
@@ -1577,8 +1588,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 #pragma unroll
                 for (int k = 0; k < NWM; ++k) wk[k] = rw[k];
               }
-              const int res = draw_fast_s<NWM>(wk, Pm, M, N, rev, rev ? N - b0 : a0, rev ? N - na : b0, rev ? ub : ua, K,
-                                               tb, vA, vB, T4w, T8w, &misc[MS_FBK], d0, e0, d1, e1);
+              const int res = draw_fast_s<NWM>(wk, Pm, M, N, rev, rev ? N - b0 : a0, rev ? N - na : b0, rev ? POb : POa,
+                                               rev ? ub : ua, K, tb, vA, vB, T4w, T8w, &misc[MS_FBK], d0, e0, d1, e1);
               t0 += d0; f0 += e0; t1 += d1; f1 += e1;
               if (rev) nb = N - res; else na = res;
             }

@@ -960,7 +960,8 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
     S = __builtin_fma(y, tlo.x, S);
     S = __builtin_fma(y * tlo.y, shi, S);
   }
-  /* pass 2: locate the word, then the group and entry where u falls; certify */
+  /* pass 2: locate the word, then the byte, nibble and entry where u falls (the searches compare
+     against u S; the pick is certified below, independently of how it was found) */
   int res = -1, POp = 0;   /* the pick and the ones among walk entries [0, pick) */
   if (S > 0.0 && S < 0x1p1000) {
     const double inv = 1.0 / S;
@@ -979,46 +980,46 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
       if constexpr (NWM <= 9) Ok += __popc(wk[k]);
     }
     const int w0 = 32 * j;
-    const int nb = min(32, L + 1 - w0);
-    const int nvg = (nb + 3) >> 2;
-    double gsum[8], gy[8];
-    int ng = 0;
+    const int nb = min(32, L + 1 - w0);   /* walk entries in word j */
+    const double uS = u * S;
+    /* byte level: the word's whole bytes from the 8-entry tables (the walk's partial last byte,
+       if any, is the last candidate: its end is S itself); then the nibble, then the entry */
+    const int nfb = nb >> 3, nlb = (nb + 7) >> 3;
+    double2 tb8[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) tb8[g] = *reinterpret_cast<const double2 *>(T8 + 2 * ((ww >> (8 * g)) & 255u));
+    double Bg[4], Yg[4];
+    int nbc = 0;
     {
-      double yy = y, acc = Sp0;
+      double acc = Sp0, yy = y;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {   /* 4 table entries per LDS round trip */
-        double2 tt[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const uint32_t nib = (ww >> (4 * (4 * h + g))) & 15u;
-          const int c = min(max(nb - 4 * (4 * h + g), 0), 4);
-          tt[g] = t4sp(T4, c, nib);
-        }
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          gy[4 * h + g] = yy;
-          acc = __builtin_fma(yy, tt[g].x, acc);
-          gsum[4 * h + g] = acc;
-          yy = yy * tt[g].y;
-        }
-        __builtin_amdgcn_sched_barrier(0);
+      for (int g = 0; g < 4; ++g) {
+        Yg[g] = yy;
+        acc = __builtin_fma(yy, tb8[g].x, acc);
+        Bg[g] = acc;
+        yy = yy * tb8[g].y;
+        nbc += (g < nfb && acc < uS) ? 1 : 0;
       }
-#pragma unroll
-      for (int g = 0; g < 8; ++g) ng += (g < nvg && gsum[g] * inv < u) ? 1 : 0;
     }
-    const int gsel = min(ng, nvg - 1);
-    double base = Sp0, ys = y;
+    const int bsel = min(nbc, nlb - 1);
+    double base_b = Sp0, y_b = y;
 #pragma unroll
-    for (int g = 0; g < 8; ++g) {
-      if (g == gsel) ys = gy[g];
-      if (g + 1 == gsel) base = gsum[g];
+    for (int g = 0; g < 4; ++g) {
+      if (g == bsel) y_b = Yg[g];
+      if (g + 1 == bsel) base_b = Bg[g];
     }
-    const uint32_t nibs = (ww >> (4 * gsel)) & 15u;
-    const int cmax = min(nb - 4 * gsel, 4);
+    const uint32_t bv = (ww >> (8 * bsel)) & 255u;
+    const int ce = min(nb - 8 * bsel, 8), c_lo = min(ce, 4), c_hi = ce - c_lo;
+    const double2 tlo = t4sp(T4, c_lo, bv & 15u);
+    const double N0 = __builtin_fma(y_b, tlo.x, base_b);
+    const bool nsel = c_hi > 0 && N0 < uS;
+    const int gsel = 2 * bsel + (nsel ? 1 : 0);
+    const double base = nsel ? N0 : base_b, ys = nsel ? y_b * tlo.y : y_b;
+    const uint32_t nibs = nsel ? (bv >> 4) : (bv & 15u);
+    const int cmax = nsel ? c_hi : c_lo;
     const double P1 = __builtin_fma(ys, t4s(T4, 1, nibs), base), P2 = __builtin_fma(ys, t4s(T4, 2, nibs), base);
     const double P3 = __builtin_fma(ys, t4s(T4, 3, nibs), base), P4 = __builtin_fma(ys, t4s(T4, 4, nibs), base);
-    const int nc = ((cmax > 1 && P1 * inv < u) ? 1 : 0) + ((cmax > 2 && P2 * inv < u) ? 1 : 0) +
-                   ((cmax > 3 && P3 * inv < u) ? 1 : 0);
+    const int nc = ((cmax > 1 && P1 < uS) ? 1 : 0) + ((cmax > 2 && P2 < uS) ? 1 : 0) + ((cmax > 3 && P3 < uS) ? 1 : 0);
     const double Ph = (nc == 0) ? P1 : (nc == 1) ? P2 : (nc == 2) ? P3 : P4;
     const double Pp = (nc == 0) ? base : (nc == 1) ? P1 : (nc == 2) ? P2 : P3;
     const int w = w0 + 4 * gsel + nc;

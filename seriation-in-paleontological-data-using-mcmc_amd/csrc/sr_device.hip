@@ -967,21 +967,23 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
     const double inv = 1.0 / S;
     const double REL = (double)(N + 33) * 0x1p-50;   /* + the byte tables' own rounding (<= 16 ulp per entry) */
     const double ABS = (double)(N + 1) * 0x1p-39;
-    int j = klo;
+    /* the words before the window hold S = 0 (< u S), so counting k < khi finds the word */
+    const double uS = u * S;
+    int j = 0;
 #pragma unroll
-    for (int k = 0; k < NWM; ++k) j += (k >= klo && k < khi && ckr[k] * inv < u) ? 1 : 0;
+    for (int k = 0; k < NWM; ++k) j += (k < khi && ckr[k] < uS) ? 1 : 0;
+    j = max(j, klo);   /* (u = 0) */
     double Sp0 = 0.0, y = yst[0];
     uint32_t ww = wk[0];
     [[maybe_unused]] int Oj = 0, Ok = 0;   /* ones among walk entries [0, 32 j) (9-word walks) */
 #pragma unroll
     for (int k = 0; k < NWM; ++k) {
       if (k == j) { y = yst[k]; ww = wk[k]; Oj = Ok; }
-      if (k + 1 == j && j > klo) Sp0 = ckr[k];
+      if (k + 1 == j) Sp0 = ckr[k];   /* ckr[klo - 1] = 0 */
       if constexpr (NWM <= 9) Ok += __popc(wk[k]);
     }
     const int w0 = 32 * j;
     const int nb = min(32, L + 1 - w0);   /* walk entries in word j */
-    const double uS = u * S;
     /* byte level: the word's whole bytes from the 8-entry tables (the walk's partial last byte,
        if any, is the last candidate: its end is S itself); then the nibble, then the entry */
     const int nfb = nb >> 3, nlb = (nb + 7) >> 3;

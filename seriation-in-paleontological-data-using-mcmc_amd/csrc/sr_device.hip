@@ -873,10 +873,13 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
     const double dv = vB - vA;
     const double Fo = __builtin_fma((double)POo, dv, (double)o * vA);
     int O = 0;   /* ones among walk entries [0, 32k) */
+    const int kl = L >> 5, nbl = (L & 31) + 1;   /* the walk's last word and its entries */
+    const uint32_t lastm = (2u << (L & 31)) - 1u;
 #pragma unroll
     for (int k = 0; k < NWM; ++k) {
-      const int nb = min(32, L + 1 - 32 * k);
-      const uint32_t vm = (nb >= 32) ? 0xffffffffu : ((nb > 0) ? ((1u << nb) - 1u) : 0u);
+      const bool full = k < kl;   /* (words past kl are outside the walk: not in the window) */
+      const int nb = full ? 32 : nbl;
+      const uint32_t vm = full ? 0xffffffffu : lastm;
       double qs;
       if constexpr (NWM <= 9) qs = Fo - __builtin_fma((double)O, dv, (double)(32 * k) * vA);
       else {   /* the 17-word walks keep the two-sided form: the F form spills there (+9 % kernel time at N = 400) */

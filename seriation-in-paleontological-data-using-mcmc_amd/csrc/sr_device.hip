@@ -869,11 +869,12 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
      (the window only bounds the skipped mass: the pick is certified independently of it). */
   int klo = NWM, khi = -1;
   double qlo = 0.0;
+  const int kl = L >> 5, nbl = (L & 31) + 1;   /* the walk's last word and its entries */
+  uint32_t wl = 0u;                              /* word kl */
   {
     const double dv = vB - vA;
     const double Fo = __builtin_fma((double)POo, dv, (double)o * vA);
     int O = 0;   /* ones among walk entries [0, 32k) */
-    const int kl = L >> 5, nbl = (L & 31) + 1;   /* the walk's last word and its entries */
     const uint32_t lastm = (2u << (L & 31)) - 1u;
 #pragma unroll
     for (int k = 0; k < NWM; ++k) {
@@ -895,6 +896,7 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
       klo = first ? k : klo;
       khi = in ? k : khi;
       O += __popc(wk[k]);
+      if constexpr (NWM <= 9) wl = (k == kl) ? wk[k] : wl;
     }
   }
 #ifdef SR_STAMP_FINE
@@ -925,7 +927,9 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
     /* word k's 4 entries (whole bytes of the walk inside the window; the dead entry otherwise) */
     auto wload = [&](int k, double2 (&t)[4]) {
       const bool inw = k >= klo && k <= khi;
-      const int nfk = inw ? min(max((L + 1 - 32 * k) >> 3, 0), 4) : 0;
+      int nfk;   /* whole bytes of the walk in word k (khi <= kl) */
+      if constexpr (NWM <= 9) nfk = inw ? ((k < kl) ? 4 : (nbl >> 3)) : 0;
+      else nfk = inw ? min(max((L + 1 - 32 * k) >> 3, 0), 4) : 0;   /* (the form above is 1.8 % slower here) */
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const uint32_t e = (g < nfk) ? ((wk[k] >> (8 * g)) & 255u) : 256u;
@@ -954,9 +958,11 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
     /* the partial byte (c8 entries) when its word lies in the window */
     const int nfull = (L + 1) >> 3, c8 = (L + 1) & 7, kb = nfull >> 2;
     const bool actb = c8 > 0 && kb >= klo && kb <= khi;
-    uint32_t wb = 0u;   /* word kb by masks (a select at a runtime index becomes a scratch array) */
+    uint32_t wb = wl;   /* word kb = kl when c8 > 0 (the 17-word kernel selects it here: tracking spills there) */
+    if constexpr (NWM > 9) {
 #pragma unroll
-    for (int k = 0; k < NWM; ++k) wb |= wk[k] & (0u - (uint32_t)(k == kb));
+      for (int k = 0; k < NWM; ++k) wb |= wk[k] & (0u - (uint32_t)(k == kb));
+    }
     const uint32_t eb = (wb >> (8 * (nfull & 3))) & 255u;
     const double2 tlo = t4sp(T4, actb ? min(c8, 4) : 0, eb & 15u);
     const double shi = t4s(T4, actb ? max(c8 - 4, 0) : 0, eb >> 4);

@@ -1919,17 +1919,16 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             /* one taxon per thread: all 16 proposal slots unrolled; slot s has the compile-time
                kind prop_kind(s), so each copy holds one kind's code and the slots' loads, ALU
                and reductions are independent */
-            int d0s[16], d1s[16], nzs[16];
+            int d0s[16], d1s[16];
 #pragma unroll
             for (int sI = 0; sI < 16; ++sI) {
-              d0s[sI] = 0; d1s[sI] = 0; nzs[sI] = 0;
+              d0s[sI] = 0; d1s[sI] = 0;
               const int fl = __builtin_amdgcn_readlane(vfl, sI);
               if (sI >= p0 && sI < pend && !(fl & 4)) {
                 const Prop q = load_prop(sI);
                 int dt0 = 0, dt1 = 0;
                 if (tid < M) taxon_dt(prop_kind(sI), q, a1, b1, P + tid, pre + tid, M, hb1, hcnt, nhall, dt0, dt1);
                 d0s[sI] = dt0; d1s[sI] = dt1;
-                if (prop_kind(sI) != PK_PI1) nzs[sI] = __popcll(__ballot((dt0 | dt1) != 0));
               }
             }
             FST(3);
@@ -1942,7 +1941,6 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                   const int cp0 = (int)__popcll(__ballot(d0s[sI] > 0)), cn0 = (int)__popcll(__ballot(d0s[sI] < 0));
                   const int cp1 = (int)__popcll(__ballot(d1s[sI] > 0)), cn1 = (int)__popcll(__ballot(d1s[sI] < 0));
                   X0 = cp0 - cn0; X1 = cp1 - cn1; Y0 = cp0 + cn0; Y1 = cp1 + cn1;
-                  nzs[sI] = Y0 + Y1;
                 } else if (pack) {   /* per-wave sums of (dt + N) and |dt| fit 16-bit fields (N < 512) */
                   const uint32_t u1 = (uint32_t)wave_sum_i32((int)((uint32_t)(d0s[sI] + N) | ((uint32_t)(d1s[sI] + N) << 16)));
                   const uint32_t u2 = (uint32_t)wave_sum_i32((int)((uint32_t)abs(d0s[sI]) | ((uint32_t)abs(d1s[sI]) << 16)));
@@ -1954,7 +1952,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 }
                 if (lane == 0) {
                   int *o = pw + (sI * NWV + wave) * 8;
-                  o[0] = X0; o[1] = X1; o[2] = Y0; o[3] = Y1; o[4] = nzs[sI];
+                  o[0] = X0; o[1] = X1; o[2] = Y0; o[3] = Y1;
                 }
               }
             }
@@ -1964,7 +1962,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             if (__builtin_amdgcn_readlane(vfl, p) & 4) continue;
             const int kind = prop_kind(p);
             const Prop q = load_prop(p);
-            int x0 = 0, x1 = 0, y0 = 0, y1 = 0, nzc = 0;
+            int x0 = 0, x1 = 0, y0 = 0, y1 = 0;
             for (int m0 = wave * 64; m0 < M; m0 += TB) {
               const int m = m0 + lane;
               int dt0 = 0, dt1 = 0;
@@ -1972,12 +1970,11 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 taxon_dt(kind, q, sab[m], sab[M + m], P + m, pre + m, M, kind == PK_PI3 ? hard_bits_col(P + m, M, hl, nh) : 0u,
                          hcnt, nhall, dt0, dt1);
               x0 += dt0; x1 += dt1; y0 += abs(dt0); y1 += abs(dt1);
-              nzc += __popcll(__ballot((dt0 | dt1) != 0));
             }
             const int X0 = wave_sum_i32(x0), X1 = wave_sum_i32(x1), Y0 = wave_sum_i32(y0), Y1 = wave_sum_i32(y1);
             if (lane == 0) {
               int *o = pw + (p * NWV + wave) * 8;
-              o[0] = X0; o[1] = X1; o[2] = Y0; o[3] = Y1; o[4] = nzc;
+              o[0] = X0; o[1] = X1; o[2] = Y0; o[3] = Y1;
             }
             STAMP_K(kind);
           }
@@ -1990,7 +1987,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
              X = sum dt, Y = sum |dt| (exact integers), S = X0 (cc - d) + X1 (dd - c) is the exact
              sum of the exact per-taxon terms and B = Y0 (|cc|+|d|) + Y1 (|dd|+|c|) bounds their
              magnitudes; the reference's rounded terms and sequential sum stay within
-             (K + 7) 2^-53 B of S, K = #nonzero terms <= Knz, so Eb = (Knz + 16) 2^-52 B decides
+             (K + 7) 2^-53 B of S, K = #nonzero terms <= Knz = Y0 + Y1, so Eb = (Knz + 16) 2^-52 B decides
              delta >= 0 and delta > log u whenever the true value is farther than Eb.  log u is
              first taken in f32 (error << 2^-16 (1 + |log u|)), exactly only when that is too close.
              cls: 0 rejected, 1 accepted, 2 needs the exact delta or the exact log. */
@@ -2006,10 +2003,11 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 #pragma unroll
                 for (int w = 0; w < NWV; ++w) {
                   const int *o = pw + (p * NWV + w) * 8;
-                  X0 += o[0]; X1 += o[1]; Y0 += o[2]; Y1 += o[3]; Knz += o[4];
+                  X0 += o[0]; X1 += o[1]; Y0 += o[2]; Y1 += o[3];
                 }
                 Sp = ((double)X0 * K.cc - (double)X0 * K.d) + ((double)X1 * K.dd - (double)X1 * K.c);
                 const double B = (double)Y0 * aC + (double)Y1 * aD;
+                Knz = Y0 + Y1;   /* >= the number of nonzero terms: each has |dt0| + |dt1| >= 1 */
                 Ebp = ((double)Knz + 16.0) * 0x1p-52 * B;
                 uwp = (uint32_t)vuw;
 #ifdef SR_FORCE_EXACT   /* test build: every decision by the exact sequential delta */

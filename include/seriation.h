@@ -143,6 +143,9 @@ int sr_session_accept_counts(sr_session *s, int32_t chain, int64_t *acc7);
    mcmc.c; every fallback is bit-exact): fb3 = {proposals decided by the exact sequential delta,
    Gibbs draws by the exact three-pass walk, c/d draws by the sequential GSL path}. */
 int sr_session_fallback_counts(sr_session *s, int32_t chain, int64_t *fb3);
+/* SR_F_DEBUG_CHECK: 1 if the chain failed mcmc_consistent after some mcmc_sample call of this
+   session (the check of mcmc.c:254; sticky), 0 if not or without the flag. */
+int sr_session_debug_flagged(const sr_session *s, int32_t chain);
 /* Device time of the last sr_session_run (ms, HIP events on the session stream; syncs). */
 double sr_session_last_kernel_ms(sr_session *s);
 int32_t sr_session_block_threads(const sr_session *s);

@@ -325,7 +325,10 @@ struct sr_session {
   sr_run_opts opts;
   srk_dev *dev;
   int rec_cap, nrec;
-  long debug_calls;         /* mcmc_sample calls checked by SR_F_DEBUG_CHECK */
+  long debug_calls;         /* mcmc_sample calls checked by SR_F_DEBUG_CHECK in this session */
+  uint64_t *acc0;           /* SR_F_DEBUG_CHECK: acceptance counters at session creation (a restored
+                               state carries its counters over; the rates cover this session's calls) */
+  uint8_t *dbg_bad;         /* SR_F_DEBUG_CHECK: chain failed mcmc_consistent after some call (sticky) */
 };
 
 static void state_free(sr_state_host *st)
@@ -452,6 +455,12 @@ static int session_new(const sr_dataset *ds, const sr_chain_spec *specs, int32_t
     for (int c = 0; c < n_chains && pkey; c++) sr_philox_key(specs[c].seed, pkey + 2 * c);
   }
   if (rc) { state_free(&st); sr_session_destroy(s); return rc; }
+  if (o.flags & SR_F_DEBUG_CHECK) {
+    s->acc0 = (uint64_t *)malloc(sizeof(uint64_t) * SR_NACC * n_chains);
+    s->dbg_bad = (uint8_t *)calloc(n_chains, 1);
+    if (!s->acc0 || !s->dbg_bad) { state_free(&st); free(pkey); sr_session_destroy(s); return SR_ENOMEM; }
+    memcpy(s->acc0, st.acc, sizeof(uint64_t) * SR_NACC * n_chains);
+  }
   s->rec_cap = auto_calls_per_launch(&o);
   const int gm_force = (o.flags & SR_F_HBM_COLUMNS) ? 1 : ((o.flags & SR_F_LDS_COLUMNS) ? 0 : -1);
   rc = srk_create(&st, o.device, o.block_threads, s->rec_cap, gm_force, pkey, &s->dev);
@@ -478,21 +487,27 @@ static int download(sr_session *s, sr_state_host *st);
 static int check_chain(const sr_dataset *ds, const sr_state_host *st, int c);
 
 /* SR_F_DEBUG_CHECK after one mcmc_sample call of every chain: the reference's MCMCDEBUG block
- * (mcmc.c:249-255) -- the running acceptance rates on stderr (cumulative counters, as its static
- * ones; one line per chain in chain order) and mcmc_consistent on the downloaded state. */
+ * (mcmc.c:249-255) -- the running acceptance rates on stderr (counters and calls of this session,
+ * as its static ones count the process's calls; sweeps_per_call sweeps per call where the
+ * reference hard-codes 10; one line per chain in chain order) and mcmc_consistent on the
+ * downloaded state.  Like the reference (which ignores that check's result there and runs on), a
+ * failing chain does not stop the run: it is flagged (dbg_bad, sticky) and SR_EINCONSISTENT
+ * returned after every chain was checked. */
 static int debug_check(sr_session *s)
 {
   sr_state_host st;
   int rc = download(s, &st);
   if (rc) return rc;
   s->debug_calls++;
-  const double n = (double)s->debug_calls, M = (double)s->ds.M;
-  for (int c = 0; c < s->nchains && rc == SR_OK; c++) {
-    const uint64_t *a = st.acc + (size_t)c * SR_NACC;
+  const double n = (double)s->debug_calls, M = (double)s->ds.M, spc = (double)s->opts.sweeps_per_call;
+  for (int c = 0; c < s->nchains; c++) {
+    const uint64_t *a = st.acc + (size_t)c * SR_NACC, *a0 = s->acc0 + (size_t)c * SR_NACC;
+    double r[7];
+    for (int k = 0; k < 7; k++) r[k] = (double)(a[k] - a0[k]);
     if (s->opts.flags & SR_F_DEBUG_PRINT)
-      fprintf(stderr, "mcmc_sample: %f %f %f %f %f %f %f\n", a[0] / (10. * n), a[1] / (10. * n), a[2] / (20. * n * M),
-              a[3] / (10. * 5 * n), a[4] / (10. * 5 * n), a[5] / (10. * 5 * n), a[6] / (10. * 5 * n));
-    if (check_chain(&s->ds, &st, c)) rc = SR_EINCONSISTENT;
+      fprintf(stderr, "mcmc_sample: %f %f %f %f %f %f %f\n", r[0] / (spc * n), r[1] / (spc * n), r[2] / (2. * spc * n * M),
+              r[3] / (spc * 5 * n), r[4] / (spc * 5 * n), r[5] / (spc * 5 * n), r[6] / (spc * 5 * n));
+    if (check_chain(&s->ds, &st, c)) { s->dbg_bad[c] = 1; rc = SR_EINCONSISTENT; }
   }
   state_free(&st);
   return rc;
@@ -503,15 +518,25 @@ SR_API int sr_session_run(sr_session *s, int32_t calls, int32_t save)
   if (!s || calls < 0) return SR_EINVAL;
   if (save && s->nrec + calls > s->rec_cap) return SR_EINVAL;
   const int dbg = (s->opts.flags & SR_F_DEBUG_CHECK) != 0;
+  int bad = 0;
   for (int done = 0; done < calls;) {   /* debug: one call per launch, each followed by the check */
     const int k = dbg ? 1 : calls;
     int rc = srk_run(s->dev, k, s->opts.sweeps_per_call, save ? 1 : 0, s->nrec);
     if (rc) return rc == -1 ? SR_EINVAL : SR_EDEVICE;
     if (save) s->nrec += k;
     done += k;
-    if (dbg && (rc = debug_check(s))) return rc;
+    if (dbg && (rc = debug_check(s))) {
+      if (rc != SR_EINCONSISTENT) return rc;
+      bad = 1;   /* flagged; the calls still run (mcmc.c:254 ignores the check's result) */
+    }
   }
-  return SR_OK;
+  return bad ? SR_EINCONSISTENT : SR_OK;
+}
+
+SR_API int sr_session_debug_flagged(const sr_session *s, int32_t chain)
+{
+  if (!s || chain < 0 || chain >= s->nchains) return SR_EINVAL;
+  return (s->dbg_bad && s->dbg_bad[chain]) ? 1 : 0;
 }
 
 SR_API int sr_session_sync(sr_session *s) { return (!s) ? SR_EINVAL : (srk_sync(s->dev) ? SR_EDEVICE : SR_OK); }
@@ -780,6 +805,8 @@ SR_API void sr_session_destroy(sr_session *s)
   if (s->dev) srk_destroy(s->dev);
   sr_free_dataset(&s->ds);
   free(s->specs);
+  free(s->acc0);
+  free(s->dbg_bad);
   free(s);
 }
 
@@ -955,7 +982,8 @@ static int writer_threads(int n)
 }
 
 static int run_common(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n, const sr_run_opts *opts,
-                      sr_sample_sink_fn sink, void *ctx, dir_ctx *dir, sr_chain_summary *out, sr_state_host *final_state)
+                      sr_sample_sink_fn sink, void *ctx, dir_ctx *dir, int wthr, sr_chain_summary *out,
+                      sr_state_host *final_state)
 {
   sr_run_opts o;
   if (opts) o = *opts; else sr_default_opts(&o);
@@ -966,9 +994,11 @@ static int run_common(const sr_dataset *ds, const sr_chain_spec *specs, int32_t 
   sr_session *s = NULL;
   int rc = sr_session_create(ds, specs, n, &o2, &s);
   if (rc) return rc;
+  /* SR_F_DEBUG_CHECK: a chain failing the per-call check is flagged in the session (dbg_bad) and
+     the run goes on (mcmc.c:254); its summary reports it at the end */
   for (int done = 0; done < o.burnin_calls;) {
     int k = o.burnin_calls - done < cpl ? o.burnin_calls - done : cpl;
-    if ((rc = sr_session_run(s, k, 0))) goto fail;
+    if ((rc = sr_session_run(s, k, 0)) && rc != SR_EINCONSISTENT) goto fail;
     done += k;
   }
   const int N = ds->N, M = ds->M, W = 2 * M + N;
@@ -976,6 +1006,7 @@ static int run_common(const sr_dataset *ds, const sr_chain_spec *specs, int32_t 
   memset(&r, 0, sizeof r);
   r.n = n; r.N = N; r.M = M; r.sink = sink; r.ctx = ctx; r.dir = dir;
   r.nthr = dir ? writer_threads(n) : 1;
+  if (wthr > 0 && r.nthr > wthr) r.nthr = wthr;   /* a shard's share of the writer threads */
   r.sums = (sr_sums *)calloc(n, sizeof(sr_sums));
   r.ra = (int32_t *)malloc((size_t)W * 4);
   if (!r.sums || !r.ra) { free(r.sums); free(r.ra); rc = SR_ENOMEM; goto fail; }
@@ -986,7 +1017,8 @@ static int run_common(const sr_dataset *ds, const sr_chain_spec *specs, int32_t 
     rc = (ab && cd) ? SR_OK : SR_ENOMEM;
     for (int t = 0; t < o.sample_calls && rc == SR_OK; t++) {
       sr_session_reset_records(s);
-      if ((rc = sr_session_run(s, 1, 1))) break;
+      if ((rc = sr_session_run(s, 1, 1)) && rc != SR_EINCONSISTENT) break;
+      rc = SR_OK;   /* a flagged chain (dbg_bad) keeps sampling */
       if ((rc = sr_session_fetch_records(s, 0, 1, ab, cd))) break;
       if (consume_batch(&r, t, 1, ab, cd)) rc = dir ? SR_EIO : SR_EINVAL;
     }
@@ -1006,15 +1038,17 @@ static int run_common(const sr_dataset *ds, const sr_chain_spec *specs, int32_t 
       out[c].exp_loglik = r.sums[c].ls / 1000;      /* print_exp_data divides by 1000 (mcmc.c:62-64) */
       out[c].exp_c = r.sums[c].cs / 1000;
       out[c].exp_d = r.sums[c].ds / 1000;
-      out[c].consistent = (o.flags & SR_F_NO_CHECK) ? 0 : check_chain(ds, &st, c);
+      out[c].consistent = ((o.flags & SR_F_NO_CHECK) ? 0 : check_chain(ds, &st, c)) | (s->dbg_bad ? s->dbg_bad[c] : 0);
     }
   }
   free(r.sums);
+  int bad = 0;
+  for (int c = 0; c < n && s->dbg_bad; c++) bad |= s->dbg_bad[c];
   if (final_state) *final_state = st; else state_free(&st);
   sr_session_destroy(s);
   if (out && !(o.flags & SR_F_NO_CHECK))
     for (int c = 0; c < n; c++) if (out[c].consistent) return SR_EINCONSISTENT;
-  return SR_OK;
+  return bad ? SR_EINCONSISTENT : SR_OK;
 fail:
   sr_session_destroy(s);
   return rc;
@@ -1037,6 +1071,7 @@ typedef struct {
   sr_chain_summary *out;
   sr_state_host st;
   int want_state;
+  int wthr;                 /* this shard's share of the chain_data.csv writer threads */
 } shard_arg;
 
 static int shard_sink(void *ctx, int32_t ci, int32_t si, const sr_record *rec)
@@ -1052,7 +1087,7 @@ static void *shard_main(void *va)
 {
   shard_arg *a = (shard_arg *)va;
   a->rc = run_common(a->ds, a->specs, a->n, &a->o, a->sink ? shard_sink : NULL, a, a->have_dir ? &a->dir : NULL,
-                     a->out, a->want_state ? &a->st : NULL);
+                     a->wthr, a->out, a->want_state ? &a->st : NULL);
   return NULL;
 }
 
@@ -1063,13 +1098,15 @@ static int run_multi(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n
   if (nd <= 0 || nd > n || !devices) return SR_EINVAL;
   sr_run_opts o;
   if (opts) o = *opts; else sr_default_opts(&o);
-  if (nd == 1) { o.device = devices[0]; return run_common(ds, specs, n, &o, sink, ctx, dir, out, final_state); }
+  if (nd == 1) { o.device = devices[0]; return run_common(ds, specs, n, &o, sink, ctx, dir, 0, out, final_state); }
   shard_arg *sa = (shard_arg *)calloc(nd, sizeof(shard_arg));
   pthread_t *th = (pthread_t *)calloc(nd, sizeof(pthread_t));
   int *started = (int *)calloc(nd, sizeof(int));
   if (!sa || !th || !started) { free(sa); free(th); free(started); return SR_ENOMEM; }
   pthread_mutex_t mu = PTHREAD_MUTEX_INITIALIZER;
   int rc = SR_OK;
+  /* the host's writer threads are shared by the shards, not started per shard */
+  const int wtot = dir ? writer_threads(n) : 1, wshare = wtot / nd > 0 ? wtot / nd : 1;
   for (int k = 0; k < nd; k++) {
     shard_arg *a = &sa[k];
     a->off = (int)((long)k * n / nd);
@@ -1079,6 +1116,7 @@ static int run_multi(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n
     if (dir) { a->dir.f = dir->f + a->off; a->dir.M = dir->M; a->have_dir = 1; }
     a->out = out ? out + a->off : NULL;
     a->want_state = final_state != NULL;
+    a->wthr = wshare;
     a->rc = SR_EDEVICE;
     if (pthread_create(&th[k], NULL, shard_main, a) != 0) { rc = SR_ENOMEM; break; }
     started[k] = 1;
@@ -1087,6 +1125,10 @@ static int run_multi(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n
   /* the first hard error wins; SR_EINCONSISTENT (every shard finished its run) only if none */
   for (int k = 0; k < nd && rc == SR_OK; k++) if (sa[k].rc && sa[k].rc != SR_EINCONSISTENT) rc = sa[k].rc;
   for (int k = 0; k < nd && rc == SR_OK; k++) if (sa[k].rc) rc = sa[k].rc;
+  /* a shard that returned SR_EINCONSISTENT finished its run and left its final state; any shard
+     without one (it failed before) makes the merge impossible */
+  for (int k = 0; k < nd && final_state && (rc == SR_OK || rc == SR_EINCONSISTENT); k++)
+    if (!sa[k].st.ab) rc = SR_EDEVICE;
   if (final_state && (rc == SR_OK || rc == SR_EINCONSISTENT)) {
     int r2 = state_alloc(final_state, ds->N, ds->M, ds->nh, n);
     if (r2) rc = r2;
@@ -1111,7 +1153,7 @@ SR_API int sr_run_chains(const sr_dataset *ds, const sr_chain_spec *specs, int32
                          sr_sample_sink_fn sink, void *sink_ctx, sr_chain_summary *out)
 {
   if (!ds || !specs || n_chains <= 0) return SR_EINVAL;
-  return run_common(ds, specs, n_chains, opts, sink, sink_ctx, NULL, out, NULL);
+  return run_common(ds, specs, n_chains, opts, sink, sink_ctx, NULL, 0, out, NULL);
 }
 
 SR_API int sr_run_chains_multi(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n_chains, const sr_run_opts *opts,

@@ -17,6 +17,7 @@ one-sigma selection input) -- the only collective.
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -72,8 +73,8 @@ def measured_traffic(N, M, chains, sweeps_per_step):
         except (OSError, ValueError):
             continue
     if best is None:
-        return None, None
-    return best[2]["traffic_bytes_per_launch"], os.path.relpath(best[1], ROOT)
+        return None, None, {}
+    return best[2]["traffic_bytes_per_launch"], os.path.relpath(best[1], ROOT), best[2]
 
 
 def _cpu_worker(args):
@@ -117,8 +118,14 @@ def cpu_baseline(path, calls, workers, variant="O2"):
     oracle_ref.lib()  # build/load before forking
     ctx = mp.get_context("fork")
     t0 = time.perf_counter()
-    with ctx.Pool(workers) as pool:
+    pool = ctx.Pool(workers)
+    try:
         res = pool.map(_cpu_worker, [(text, s + 1, calls, variant) for s in range(workers)])
+    finally:
+        # close + join: the workers exit on their own (a Pool context exit terminate()s them with
+        # SIGTERM, which a profiler's signal handler reports as an abort)
+        pool.close()
+        pool.join()
     wall = time.perf_counter() - t0
     assert all(rc == 0 for _, rc in res)
     iters = workers * calls * 10
@@ -137,7 +144,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=20, help="untimed steps first (the clocks ramp over the first ~10 launches)")
     ap.add_argument("--chains-per-gpu", type=int, default=100)
-    ap.add_argument("--calls-per-step", type=int, default=10)
+    ap.add_argument("--calls-per-step", type=int, default=50,
+                    help="mcmc_sample calls per step: 50 (500 sweeps) makes the driver's --steps 20 --warmup 5 time "
+                         "SURVEY 8(d)'s 10 000 sweeps after 2 500 warm-up sweeps, saving 1000 records per chain")
     ap.add_argument("--dataset", default=SYNTH)
     ap.add_argument("--sites", type=int, default=0, help="synthetic N x M instead of --dataset "
                     "(seed 20261015 for 256x512, 20261016 otherwise: SURVEY.md 8(d) configs 3 and 5)")
@@ -190,7 +199,7 @@ def main():
 
     dist = None
     torch.cuda.set_device(local_rank)
-    if world > 1:
+    if "WORLD_SIZE" in os.environ:   # under a launcher: the RCCL path, also at world 1
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         assert dist.get_world_size() == args.gpus, "RCCL world does not match --gpus"
@@ -201,18 +210,20 @@ def main():
     # weak scaling: C chains per rank, rank r owns chains [r*C, (r+1)*C) (sd.shard), seed = id + 1
     chain_ids = list(sd.shard(C * world, world, rank))
     seeds = [i + 1 for i in chain_ids]
-    sess = sa.Session(ds, seeds, device=local_rank, calls_per_launch=args.calls_per_step,
+    cps = args.calls_per_step
+    # records of every timed step are kept (steps x calls-per-step saved samples per chain: 1000 at the
+    # driver's --steps 20, the reference's sampling window ts = 1000, mcmc.c:180-185)
+    sess = sa.Session(ds, seeds, device=local_rank, calls_per_launch=max(1, args.steps * cps),
                       block_threads=args.block_threads, chain_ids=chain_ids, columns=args.columns, rng=args.rng)
     stream = torch.cuda.current_stream()
     sess.set_stream(stream.cuda_stream)
-    cps = args.calls_per_step
 
     def step():
-        sess.reset_records()
         sess.run(cps, save=not args.no_save)
 
     for _ in range(args.warmup):
-        step()
+        sess.run(cps, save=False)
+    sess.reset_records()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -222,26 +233,30 @@ def main():
         evs[k][0].record(stream)
         step()
         evs[k][1].record(stream)
-    # the one collective: every rank's per-chain summary record (exp_data payload of the
-    # last step's saved samples) all-gathered, then the one-sigma selection on every rank
     if args.no_save:   # summaries from the final state (c, d, loglik) when no records were kept
         sess.reset_records()
         sess.run(1, save=True)
     stream.synchronize()
     t_kernels = time.perf_counter()
-    # the end of the run: summaries all-gathered -> one-sigma selection on every
-    # rank -> the selected chains' saved samples gathered from their owners
-    ab_pi, cdl = sess.fetch_records()
-    rows = sd.summaries_from_records(chain_ids, cdl)
+    # the end of the run: each chain's exp_data summary over its saved samples
+    # (compute_exp_data, mcmc.c:53-67, in C) -> ONE all-gather of the summaries -> the one-sigma
+    # selection on every rank -> the selected chains' saved samples gathered from their owners
+    rows = sess.summaries()
+    nrec = int(sess.fetch_cdl().shape[1]) if args.no_save else args.steps * cps
     if dist:
         gathered = sd.gather_summaries(rows, C * world, device="cuda")
     else:
         gathered = rows
     selected = sd.select_chains(gathered, CHAINS_SELECTED)
+    mine = [c for c in selected if c in set(chain_ids)]
+    loc = [sess.fetch_chain_records(chain_ids.index(c)) for c in mine]
+    W = 2 * ds.M + ds.N
+    loc_ab = np.stack([a for a, _ in loc]) if loc else np.zeros((0, nrec, W), np.int16)
+    loc_cd = np.stack([c for _, c in loc]) if loc else np.zeros((0, nrec, 3))
     if dist:
-        sel_ab, sel_cdl = sd.gather_selected_records(selected, C * world, chain_ids, ab_pi, cdl, device="cuda")
+        sel_ab, sel_cdl = sd.gather_selected_records(selected, C * world, mine, loc_ab, loc_cd, device="cuda")
     else:
-        sel_ab, sel_cdl = ab_pi[selected], cdl[selected]
+        sel_ab, sel_cdl = loc_ab, loc_cd
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -264,7 +279,14 @@ def main():
     B = algorithmic_bytes_per_iter(ds.N, ds.M)
     launch_bytes = C * sweeps_per_step * B
     achieved = launch_bytes / (kernel_ms / 1e3) / 1e9
-    traffic, traffic_src = measured_traffic(ds.N, ds.M, C, sweeps_per_step)
+    traffic, traffic_src, prof = measured_traffic(ds.N, ds.M, C, sweeps_per_step)
+    # what bounds the kernel, from the same PMC summary (SQ counters): the LDS-resident variant is
+    # bound by per-wave issue and latency (its HBM traffic is the state and the records); the
+    # HBM-column variant (columns too large for LDS, config 5) re-reads its columns from L2 / HBM
+    limiter = dict(prof.get("limiter") or {})
+    limiter["bound"] = ("issue / latency (working set in LDS; HBM carries only chain state and records)"
+                        if sess.variant == "lds" else "HBM / L2 (occurrence columns re-read from HBM every sweep)")
+    limiter["source"] = traffic_src
     out = {
         "metric": "chain-iterations/sec (100 chains, 256x512 matrix) at 1/2/4/8 MI355X",
         "value": value,
@@ -305,6 +327,7 @@ def main():
             "bytes_per_chain_iteration": B,
             "launch_bytes": launch_bytes,
         },
+        "limiter": limiter,
         "cpu_baseline": cpu,
         "cpu_baseline_O0": cpu_o0,
         "timing": {"kernel_ms_per_step": kernel_ms, "gather_select_ms": tail_ms,
@@ -312,7 +335,11 @@ def main():
                            "one-sigma selection and the gather of the selected chains' records (inside the "
                            "timed region)"},
         "selection": {"chains_selected": selected, "exp_c": ec, "exp_d": ed, "corr_mn": corr,
-                      "note": "script.py:70-152 over the last step's saved samples of the selected chains"},
+                      "samples_per_chain": nrec,
+                      "records_sha256": hashlib.sha256(np.ascontiguousarray(sel_ab).tobytes() +
+                                                       np.ascontiguousarray(sel_cdl).tobytes()).hexdigest(),
+                      "note": "script.py:70-152 over every timed step's saved samples of the selected chains (the "
+                              "reference divides by 1000: exact means at --steps 20 x 50 calls = 1000 samples)"},
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

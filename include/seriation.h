@@ -77,6 +77,9 @@ typedef struct {
                                 keyed by the chain's seed instead of GSL's MT19937 (initialisation unchanged).  Not
                                 the reference's stream: statistically equivalent, not bit-equal.  A checkpoint
                                 keeps its stream kind; restoring it needs the same flag (else SR_EINVAL). */
+#define SR_F_DIAG 64         /* the reference's stderr diagnostics during initialisation: "mcmc_initab: zero column
+                                at %d, continuing." per all-zero column, from mcmc_readmodel's and mcmc_randomize's
+                                mcmc_initab (mcmc.c:457); the drop-in CLI sets it */
 
 typedef struct {
   int32_t chain_id;
@@ -134,6 +137,14 @@ int32_t sr_session_record_capacity(const sr_session *s);
    either may be NULL (not fetched) */
 int sr_session_fetch_records(sr_session *s, int32_t first, int32_t count, int16_t *ab_pi, double *cdl);
 int sr_session_reset_records(sr_session *s);
+/* One chain's buffered records [first, first + count): ab_pi [count][2M+N] int16, cdl [count][3]
+   (either may be NULL). */
+int sr_session_fetch_chain_records(sr_session *s, int32_t chain, int32_t first, int32_t count, int16_t *ab_pi,
+                                   double *cdl);
+/* compute_exp_data / print_exp_data (mcmc.c:53-67) of every chain over its buffered records [first,
+   first + count): out[c] = {chain_id, 0, sum(-loglik) / 1000, sum(e^c) / 1000, sum(e^d) / 1000}, sums in
+   sample order, the reference's hard-coded divisor (exact means when count = 1000). */
+int sr_session_summaries(sr_session *s, int32_t first, int32_t count, sr_chain_summary *out);
 /* Current state of one chain (any pointer may be NULL); counts = t0,f0,t1,f1 (4*M). */
 int sr_session_state(sr_session *s, int32_t chain, int32_t *a, int32_t *b, int32_t *pi,
                      double *c_d_loglik, int32_t *counts);

@@ -30,6 +30,7 @@
 #include <stdint.h>
 #include <stddef.h>
 #include <string.h>
+#include <math.h>
 #include "om_libm.h"
 
 #define OM_MT_N 624
@@ -211,8 +212,27 @@ static inline double om_gamma(om_rng *r, double a, double b)
   return b * d * v;
 }
 
+/* gsl_ran_beta (GSL 2.6 randist/beta.c, restated from its published algorithm): Johnk's method
+ * when both shapes are <= 1, else the ratio of two gammas.  The sampler's shapes are 1 + count
+ * (mcmc.c:757), so the Johnk branch is reached exactly when both counts are 0 (e.g. every taxon
+ * spans every site: t0a = f1a = 0 for c); then a = b = 1 and pow(U, 1/1) = U exactly.  Other
+ * shapes <= 1 use libm pow/log/exp (never reached by the sampler; not bit-pinned). */
 static inline double om_beta(om_rng *r, double a, double b)
 {
+  if (a <= 1.0 && b <= 1.0) {
+    for (;;) {
+      const double U = om_uniform_pos(r), V = om_uniform_pos(r);
+      const double X = (a == 1.0) ? U : pow(U, 1.0 / a), Y = (b == 1.0) ? V : pow(V, 1.0 / b);
+      if (X + Y <= 1.0) {
+        if (X + Y > 0) return X / (X + Y);
+        double logX = log(U) / a, logY = log(V) / b;
+        const double logM = logX > logY ? logX : logY;
+        logX -= logM;
+        logY -= logM;
+        return exp(logX - log(exp(logX) + exp(logY)));
+      }
+    }
+  }
   double x1 = om_gamma(r, a, 1.0);
   double x2 = om_gamma(r, b, 1.0);
   return x1 / (x1 + x2);

@@ -138,13 +138,15 @@ static int om_readmodel(om_model *x, const char *text, size_t len, int maxs, int
   return 0;
 }
 
-/* mcmc_initab, mcmc.c:440-474 */
+/* mcmc_initab, mcmc.c:440-474 (its stderr line, mcmc.c:457, in the CLI build: om_diag) */
+static int om_diag = 0;
 static void om_initab(om_model *x)
 {
   for (int m = 0; m < x->M; m++) {
     int n = 0;
     while (n < x->N && !X_(x, x->rpi[n], m)) n++;
     if (n == x->N) {
+      if (om_diag) fprintf(stderr, "mcmc_initab: zero column at %d, continuing.\n", m);
       x->a[m] = 0; x->b[m] = x->N;
     } else {
       x->a[m] = n;
@@ -870,6 +872,7 @@ int main(int argc, char *argv[])
     if (len == cap) { cap *= 2; text = (char *)realloc(text, cap); }
   }
   om_model x;
+  om_diag = 1;
   int rc = om_readmodel(&x, text, len, OM_MAXS, manycd);
   free(text);
   if (rc == -2) { fprintf(stderr, "mcmc_readmodel: read error at header.\n"); return 1; }

@@ -49,6 +49,7 @@ int main(int argc, char *argv[])
   o.burnin_calls = tb;
   o.sample_calls = ts;
   o.manycd = manycd;
+  o.flags |= SR_F_DIAG;   /* mcmc_initab's "zero column" lines on stderr, as the reference */
   const char *dev = getenv("SR_DEVICE");
   if (dev) o.device = atoi(dev);
   /* reference naming: index > 9 uses its first two characters, else "0" + first char */

@@ -423,10 +423,20 @@ template <bool WAVE>
 __device__ __forceinline__ double d_samplebeta(DRng &r, double x, double a, double b, double low, double high, int lane,
                                                int nthr, const sr_mtab &tb)
 {
-  double g[2];
-  for (int k = 0; k < 2; ++k) g[k] = d_gamma<WAVE>(r, 1. + (k ? b : a), lane, nthr, tb);   /* one inlined copy */
-  const double x1 = g[0], x2 = g[1];
-  double y = x1 / (x1 + x2);
+  double y;
+  if (a == 0. && b == 0.) {
+    /* gsl_ran_beta's Johnk branch (both shapes <= 1; here both are exactly 1 + 0): pow(U, 1/1) = U,
+       so X = U, Y = V, and X + Y > 0 always (oracle/om_gsl.h om_beta) */
+    for (;;) {
+      const double U = rng_uniform_pos<WAVE>(r, lane, nthr), V = rng_uniform_pos<WAVE>(r, lane, nthr);
+      if (U + V <= 1.0) { y = U / (U + V); break; }
+    }
+  } else {
+    double g[2];
+    for (int k = 0; k < 2; ++k) g[k] = d_gamma<WAVE>(r, 1. + (k ? b : a), lane, nthr, tb);   /* one inlined copy */
+    const double x1 = g[0], x2 = g[1];
+    y = x1 / (x1 + x2);
+  }
   if (y > 0.) {
     y = sr_log_m(y, &tb);
     if (low <= y && y <= high) x = y;
@@ -457,6 +467,7 @@ __device__ __forceinline__ bool draw_cd_fast(DRng &r, double &c, double &d, int 
   return false;
 #endif
   if (r.blk + (r.off + 7) / SR_MT_N >= r.gen) return false;
+  if ((f1 == 0 && t0 == 0) || (f0 == 0 && t1 == 0)) return false;   /* a Johnk beta: the sequential path */
   const uint32_t base = (r.blk & (SR_RING - 1)) * SR_MT_N + r.off;
   const int g = lane & 3;
   uint32_t i0 = base + 2 * g, i1 = base + 2 * g + 1;
@@ -2441,6 +2452,19 @@ extern "C" int srk_fetch_records(srk_dev *d, int first, int count, int16_t *ab_p
       HIPCHK(hipMemcpy(cdl + (size_t)c * count * 3, d->args.rec_cdl + ((size_t)c * d->rec_cap + first) * 3,
                        rows * 3 * sizeof(double), hipMemcpyDeviceToHost));
   }
+  return 0;
+}
+
+/* one chain's rows [first, first + count) of its record slab */
+extern "C" int srk_fetch_chain_records(srk_dev *d, int chain, int first, int count, int16_t *ab_pi, double *cdl)
+{
+  if (chain < 0 || chain >= d->nchains || first < 0 || count < 0 || first + count > d->rec_cap) return -1;
+  HIPCHK(hipSetDevice(d->device));
+  HIPCHK(hipStreamSynchronize(d->stream));
+  if (count == 0) return 0;
+  const size_t W = 2 * (size_t)d->M + d->N, row = (size_t)chain * d->rec_cap + first;
+  if (ab_pi) HIPCHK(hipMemcpy(ab_pi, d->args.rec_abpi + row * W, (size_t)count * W * sizeof(int16_t), hipMemcpyDeviceToHost));
+  if (cdl) HIPCHK(hipMemcpy(cdl, d->args.rec_cdl + row * 3, (size_t)count * 3 * sizeof(double), hipMemcpyDeviceToHost));
   return 0;
 }
 

@@ -226,6 +226,7 @@ typedef struct {
   int32_t *pi, *rpi, *a, *b, *t0, *f0, *t1, *f1;
   int t0a, f0a, t1a, f1a;
   double c, d, loglik;
+  int diag;                 /* SR_F_DIAG: the reference's stderr diagnostics */
 } hmodel;
 
 static void h_initab(hmodel *x)                       /* mcmc_initab, mcmc.c:440-474 */
@@ -233,7 +234,10 @@ static void h_initab(hmodel *x)                       /* mcmc_initab, mcmc.c:440
   for (int m = 0; m < x->M; m++) {
     int n = 0;
     while (n < x->N && !x->X[(size_t)x->rpi[n] * x->M + m]) n++;
-    if (n == x->N) { x->a[m] = 0; x->b[m] = x->N; }
+    if (n == x->N) {
+      if (x->diag) fprintf(stderr, "mcmc_initab: zero column at %d, continuing.\n", m);   /* mcmc.c:457 */
+      x->a[m] = 0; x->b[m] = x->N;
+    }
     else {
       x->a[m] = n;
       n = x->N - 1;
@@ -359,11 +363,12 @@ static int state_alloc(sr_state_host *st, int N, int M, int nh, int C)
 }
 
 /* initialise one chain exactly as main() does before the burn-in (mcmc.c:127-135) */
-static int init_chain(const sr_dataset *ds, uint64_t seed, sr_state_host *st, int c)
+static int init_chain(const sr_dataset *ds, uint64_t seed, sr_state_host *st, int c, int diag)
 {
   hmodel x;
   int rc = hmodel_alloc(&x, ds);
   if (rc) return rc;
+  x.diag = diag;
   const int N = ds->N, M = ds->M, NW = st->NW;
   for (int i = 0; i < N; i++) x.pi[i] = x.rpi[i] = i;      /* mcmc.c:405-407 */
   h_initab(&x);
@@ -438,7 +443,7 @@ static int session_new(const sr_dataset *ds, const sr_chain_spec *specs, int32_t
   if (restore) rc = restore(restore_ctx, &st);
   else
     for (int c = 0; c < n_chains && rc == SR_OK; c++) {
-      rc = init_chain(ds, specs[c].seed, &st, c);
+      rc = init_chain(ds, specs[c].seed, &st, c, (o.flags & SR_F_DIAG) != 0);
       if (philox) {   /* sampling draws from the chain's Philox stream, word 0 on (init stays GSL MT19937) */
         st.rng[(size_t)c * 2 + 0] = 0;
         st.rng[(size_t)c * 2 + 1] = 0;
@@ -552,6 +557,41 @@ SR_API int sr_session_fetch_records(sr_session *s, int32_t first, int32_t count,
   return srk_fetch_records(s->dev, first, count, ab_pi, cdl) ? SR_EDEVICE : SR_OK;
 }
 
+SR_API int sr_session_fetch_chain_records(sr_session *s, int32_t chain, int32_t first, int32_t count, int16_t *ab_pi,
+                                         double *cdl)
+{
+  if (!s || chain < 0 || chain >= s->nchains || first < 0 || count < 0 || first + count > s->nrec) return SR_EINVAL;
+  return srk_fetch_chain_records(s->dev, chain, first, count, ab_pi, cdl) ? SR_EDEVICE : SR_OK;
+}
+
+/* compute_exp_data + print_exp_data (mcmc.c:53-67) over the buffered records [first, first + count)
+ * of every chain: sums of -loglik, e^c, e^d in sample order (C library exp, as the reference),
+ * divided by the reference's hard-coded 1000.  consistent is left 0 (no check is run). */
+SR_API int sr_session_summaries(sr_session *s, int32_t first, int32_t count, sr_chain_summary *out)
+{
+  if (!s || !out || first < 0 || count < 0 || first + count > s->nrec) return SR_EINVAL;
+  double *cd = (double *)malloc(sizeof(double) * 3 * ((size_t)count > 0 ? (size_t)count : 1) * s->nchains);
+  if (!cd) return SR_ENOMEM;
+  int rc = count ? srk_fetch_records(s->dev, first, count, NULL, cd) : 0;
+  if (rc) { free(cd); return SR_EDEVICE; }
+  for (int c = 0; c < s->nchains; c++) {
+    double ls = 0., cs = 0., ds = 0.;
+    for (int t = 0; t < count; t++) {
+      const double *r = cd + ((size_t)c * count + t) * 3;
+      ls += -(r[2]);
+      cs += exp(r[0]);
+      ds += exp(r[1]);
+    }
+    out[c].chain_id = s->specs[c].chain_id;
+    out[c].consistent = 0;
+    out[c].exp_loglik = ls / 1000;
+    out[c].exp_c = cs / 1000;
+    out[c].exp_d = ds / 1000;
+  }
+  free(cd);
+  return SR_OK;
+}
+
 SR_API int sr_session_reset_records(sr_session *s)
 {
   if (!s) return SR_EINVAL;
@@ -629,7 +669,7 @@ SR_API int sr_host_initial_checkpoint(const sr_dataset *ds, const sr_chain_spec 
   sr_state_host st;
   int rc = state_alloc(&st, ds->N, ds->M, ds->nh, n_chains);
   if (rc) return rc;
-  for (int c = 0; c < n_chains && rc == SR_OK; c++) rc = init_chain(ds, specs[c].seed, &st, c);
+  for (int c = 0; c < n_chains && rc == SR_OK; c++) rc = init_chain(ds, specs[c].seed, &st, c, 0);
   if (rc == SR_OK) rc = ck_write(path, ds, specs, n_chains, &st);
   state_free(&st);
   return rc;
@@ -1287,7 +1327,7 @@ SR_API int sr_host_init_chain(const sr_dataset *ds, uint64_t seed, int32_t *a, i
   sr_state_host st;
   int rc = state_alloc(&st, ds->N, ds->M, ds->nh, 1);
   if (rc) return rc;
-  rc = init_chain(ds, seed, &st, 0);
+  rc = init_chain(ds, seed, &st, 0, 0);
   if (!rc) {
     if (a) memcpy(a, st.ab, ds->M * 4);
     if (b) memcpy(b, st.ab + ds->M, ds->M * 4);

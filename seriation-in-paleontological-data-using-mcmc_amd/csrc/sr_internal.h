@@ -53,6 +53,7 @@ int srk_block_threads(const srk_dev *d);
 int srk_variant(const srk_dev *d);   /* 0 LDS columns, 1 HBM columns */
 int srk_fetch_dbg(srk_dev *d, unsigned long long *out);
 int srk_fetch_records(srk_dev *d, int first, int count, int16_t *ab_pi, double *cdl);
+int srk_fetch_chain_records(srk_dev *d, int chain, int first, int count, int16_t *ab_pi, double *cdl);
 int srk_download_state(srk_dev *d, sr_state_host *st);
 int srk_run_pipelined(srk_dev *d, int total_calls, int cpl, int spc,
                       int (*consume)(void *, int, int, const int16_t *, const double *), void *ctx);

@@ -26,6 +26,7 @@ SR_F_LDS_COLUMNS = 4
 SR_F_DEBUG_CHECK = 8
 SR_F_DEBUG_PRINT = 16
 SR_F_RNG_PHILOX = 32
+SR_F_DIAG = 64
 
 
 class SrError(RuntimeError):
@@ -79,7 +80,8 @@ PUBLIC_SYMBOLS = [
     "sr_default_opts",
     "sr_run_chains", "sr_run_to_dirs", "sr_run_chains_multi", "sr_run_to_dirs_multi", "sr_session_create", "sr_session_set_stream",
     "sr_session_run", "sr_session_sync", "sr_session_records", "sr_session_record_capacity",
-    "sr_session_fetch_records", "sr_session_reset_records", "sr_session_state",
+    "sr_session_fetch_records", "sr_session_reset_records", "sr_session_fetch_chain_records", "sr_session_summaries",
+    "sr_session_state",
     "sr_session_accept_counts", "sr_session_fallback_counts", "sr_session_debug_flagged", "sr_session_last_kernel_ms", "sr_session_block_threads", "sr_session_variant",
     "sr_session_checkpoint", "sr_session_restore",
     "sr_session_destroy", "sr_posterior", "sr_session_posterior", "sr_strerror", "sr_device_count", "sr_version",
@@ -120,6 +122,8 @@ def _lib():
         "sr_session_record_capacity": (c_i32, [c_void_p]),
         "sr_session_fetch_records": (c_int, [c_void_p, c_i32, c_i32, P(ctypes.c_int16), P(c_double)]),
         "sr_session_reset_records": (c_int, [c_void_p]),
+        "sr_session_fetch_chain_records": (c_int, [c_void_p, c_i32, c_i32, c_i32, P(ctypes.c_int16), P(c_double)]),
+        "sr_session_summaries": (c_int, [c_void_p, c_i32, c_i32, P(sr_chain_summary)]),
         "sr_session_state": (c_int, [c_void_p, c_i32, P(c_i32), P(c_i32), P(c_i32), P(c_double), P(c_i32)]),
         "sr_session_accept_counts": (c_int, [c_void_p, c_i32, P(ctypes.c_int64)]),
         "sr_session_fallback_counts": (c_int, [c_void_p, c_i32, P(ctypes.c_int64)]),

@@ -192,6 +192,29 @@ class Session:
                                                     cdl.ctypes.data_as(ctypes.POINTER(ctypes.c_double))), "fetch")
         return cdl
 
+    def fetch_chain_records(self, chain, first=0, count=None):
+        """One chain's buffered records: (ab_pi int16 [count, 2M+N], cdl float64 [count, 3])."""
+        k = L.lib().sr_session_records(self.h)
+        count = k - first if count is None else count
+        N, M = self.ds.N, self.ds.M
+        ab = np.zeros((count, 2 * M + N), np.int16)
+        cdl = np.zeros((count, 3), np.float64)
+        if count:
+            _check(L.lib().sr_session_fetch_chain_records(self.h, chain, first, count,
+                                                          ab.ctypes.data_as(ctypes.POINTER(ctypes.c_int16)),
+                                                          cdl.ctypes.data_as(ctypes.POINTER(ctypes.c_double))),
+                   "fetch_chain_records")
+        return ab, cdl
+
+    def summaries(self, first=0, count=None):
+        """sr_session_summaries: exp_data rows (chain_id, exp_loglik, exp_c, exp_d) [n, 4] of every chain
+        over its buffered records (mcmc.c:53-67; divisor 1000 as the reference)."""
+        k = L.lib().sr_session_records(self.h)
+        count = k - first if count is None else count
+        out = (L.sr_chain_summary * self.n)()
+        _check(L.lib().sr_session_summaries(self.h, first, count, out), "sr_session_summaries")
+        return np.array([(o.chain_id, o.exp_loglik, o.exp_c, o.exp_d) for o in out], np.float64).reshape(self.n, 4)
+
     def state(self, chain):
         N, M = self.ds.N, self.ds.M
         a = np.zeros(M, np.int32)

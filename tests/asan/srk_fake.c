@@ -100,6 +100,15 @@ int srk_fetch_records(srk_dev *d, int first, int count, int16_t *ab_pi, double *
   return 0;
 }
 
+int srk_fetch_chain_records(srk_dev *d, int chain, int first, int count, int16_t *ab_pi, double *cdl)
+{
+  if (chain < 0 || chain >= d->st.nchains || first < 0 || count < 0 || first + count > d->rec_cap) return -1;
+  const size_t W = 2 * (size_t)d->st.M + d->st.N, row = (size_t)chain * d->rec_cap + first;
+  if (ab_pi) memcpy(ab_pi, d->rec + row * W, (size_t)count * W * 2);
+  if (cdl) memcpy(cdl, d->rcd + row * 3, (size_t)count * 24);
+  return 0;
+}
+
 int srk_download_state(srk_dev *d, sr_state_host *st)
 {
   const size_t C = (size_t)d->st.nchains;

@@ -86,6 +86,24 @@ def _compare(tmp_path, dataset, args, seed, chain_dir):
     for f in FILES:
         assert fa[f] == fb[f], f
     assert os.path.exists(os.path.join(b, "mcmc_c.log"))
+    # the reference's own stderr lines (GSL_RNG_SEED=..., mcmc_initab's zero-column notes, mcmc.c:457)
+    # in the same order; the HIP runtime may add lines of its own
+    assert ref_lines(pa.stderr) == ref_lines(pb.stderr)
+
+
+def ref_lines(err):
+    txt = err.decode() if isinstance(err, bytes) else err
+    return [l for l in txt.splitlines() if l.startswith(("GSL_RNG_SEED=", "mcmc_"))]
+
+
+def test_oracle_cli_zero_column_notes(tmp_path):
+    """g2s2 has 3 all-zero columns: mcmc_readmodel's and mcmc_randomize's mcmc_initab
+    (0 < nh < N) each print "mcmc_initab: zero column at %d, continuing." for them (mcmc.c:457)."""
+    p = run_cli(ORACLE_CLI, str(tmp_path), "g2s2.txt", ["0", "1", "1"], 4, "chain_00")
+    assert p.returncode == 0, p.stderr
+    notes = [l for l in ref_lines(p.stderr) if l.startswith("mcmc_initab")]
+    assert len(notes) == 6 and notes[:3] == notes[3:]
+    assert all(l.startswith("mcmc_initab: zero column at ") and l.endswith(", continuing.") for l in notes)
 
 
 @pytest.mark.gpu
@@ -104,3 +122,17 @@ def test_product_cli_four_argument_form(tmp_path):
 def test_product_cli_g2s2_reference_defaults(tmp_path):
     """BASELINE config 1: g2s2, 1 chain, CLI defaults (1000 burn-in + 1000 saved calls)."""
     _compare(tmp_path, "g2s2.txt", ["7"], 1, "chain_07")
+
+
+def test_product_cli_stderr_lines_on_fake_device(tmp_path):
+    """The product CLI's initialisation runs on the host, so its reference stderr lines can be
+    checked without a GPU: built against the host-memory fake device (tests/asan/srk_fake.c), it
+    prints what the oracle CLI prints (GSL_RNG_SEED=..., the six zero-column notes of g2s2)."""
+    pkg = os.path.join(ROOT, "seriation-in-paleontological-data-using-mcmc_amd")
+    r = subprocess.run(["make", "-s", "-C", pkg, "build/fake/mcmc"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    pa = run_cli(ORACLE_CLI, str(tmp_path / "o"), "g2s2.txt", ["0", "1", "1"], 3, "chain_00")
+    pb = run_cli(os.path.join(pkg, "build", "fake", "mcmc"), str(tmp_path / "p"), "g2s2.txt", ["0", "1", "1"], 3,
+                 "chain_00")
+    assert pa.returncode == 0 and pb.returncode == 0, pb.stderr
+    assert ref_lines(pa.stderr) == ref_lines(pb.stderr) and len(ref_lines(pb.stderr)) == 7

@@ -30,14 +30,15 @@ def test_config5_variant_is_hbm(config5):
 
 
 def test_config5_parity(config5):
-    """8 chains x (1 burn-in + 20 saved calls) against the oracle, bit for bit."""
+    """8 chains x (1 burn-in + 100 saved calls) = 1010 sweeps each against the oracle, bit for bit
+    (oracle on 8 threads, ~25 s)."""
     from concurrent.futures import ThreadPoolExecutor
     ds = sa.Dataset.parse(config5, maxs=0)
     seeds = [1, 2, 3, 4, 5, 6, 7, 8]
-    summ, (ri, rd) = sa.run_chains(ds, seeds, burnin_calls=1, sample_calls=20, keep_records=True)
+    summ, (ri, rd) = sa.run_chains(ds, seeds, burnin_calls=1, sample_calls=100, keep_records=True)
 
     def one(s):
-        o = oracle_ref.run_chain(config5, s, 1, 20, maxs=0)
+        o = oracle_ref.run_chain(config5, s, 1, 100, maxs=0)
         return o["rc"], o["rec_int"].copy(), o["rec_dbl"].copy()
 
     with ThreadPoolExecutor(8) as ex:

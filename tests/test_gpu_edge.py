@@ -108,3 +108,25 @@ def test_checkpoint_resume_continues_exactly(tmp_path):
         r.close()
     assert np.array_equal(ab_full[:, 10:], ab2)
     assert np.array_equal(cdl_full[:, 10:].view(np.uint64), cdl2.view(np.uint64))
+
+
+def _all_ones_text(N, M, hard_rows):
+    lines = ["%d %d" % (N, M)] + [" ".join("1" * M) + (" *" if i in hard_rows else "") for i in range(N)]
+    return ("\n".join(lines) + "\n").encode()
+
+
+@pytest.mark.parametrize("columns", ["lds", "hbm"])
+def test_johnk_beta_branch(columns):
+    """An all-ones matrix: every taxon spans every site (a = 0, b = N), so t0a = f1a = 0 and
+    mcmc_samplec's gsl_ran_beta(1 + 0, 1 + 0) takes GSL's Johnk branch (both shapes <= 1), not the
+    gamma ratio -- every word it consumes must match the oracle's restatement (oracle/om_gsl.h)."""
+    text = _all_ones_text(40, 24, {5, 17, 30})
+    ds = sa.Dataset.parse(text, maxs=0)
+    seeds = [2, 9, 31]
+    summ, (ri, rd) = sa.run_chains(ds, seeds, burnin_calls=3, sample_calls=6, keep_records=True, columns=columns)
+    for k, s in enumerate(seeds):
+        o = oracle_ref.run_chain(text, s, 3, 6, maxs=0)
+        assert o["rc"] == 0
+        np.testing.assert_array_equal(ri[k], o["rec_int"], err_msg="seed %d" % s)
+        assert np.array_equal(rd[k].view(np.uint64), o["rec_dbl"].view(np.uint64)), s
+        assert summ[k]["consistent"] == 0

@@ -112,3 +112,33 @@ def test_parity_config3_100_chains_200_calls():
             bad.append(k)
         assert summ[k]["consistent"] == 0
     assert not bad, "chains differing from the oracle: %s" % bad
+
+
+def test_parity_config3_reference_protocol():
+    """The reference CLI's own protocol (tb = 1000 burn-in calls, then ts = 1000 saved calls, mcmc.c:
+    140-185) at BASELINE config 3's size (synthetic 256x512): 16 chains, i.e. 20 000 sweeps each, well
+    into the converged regime; every one of the 1000 saved samples of every chain and its exp_data
+    summary against the oracle, bit for bit (oracle on 16 threads, ~30 s)."""
+    import hashlib
+    from concurrent.futures import ThreadPoolExecutor
+    text = _text("synth_256x512.txt")
+    ds = sa.Dataset.parse(text, maxs=0)
+    seeds = list(range(201, 217))
+    summ, (ri, rd) = sa.run_chains(ds, seeds, burnin_calls=1000, sample_calls=1000, keep_records=True)
+
+    def one(s):
+        o = oracle_ref.run_chain(text, s, 1000, 1000, maxs=0)
+        return (o["rc"], hashlib.sha256(np.ascontiguousarray(o["rec_int"], "<i4").tobytes()).hexdigest(),
+                o["rec_dbl"].copy(), np.asarray(o["exp"]).copy())
+
+    with ThreadPoolExecutor(min(16, os.cpu_count() or 1)) as ex:
+        ref = list(ex.map(one, seeds))
+    bad = []
+    for k, (rc, dig, od, oexp) in enumerate(ref):
+        assert rc == 0
+        if hashlib.sha256(np.ascontiguousarray(ri[k], "<i4").tobytes()).hexdigest() != dig or \
+                not np.array_equal(rd[k].view(np.uint64), od.view(np.uint64)) or \
+                not np.array_equal(np.array([summ[k]["exp_loglik"], summ[k]["exp_c"], summ[k]["exp_d"]]), oexp):
+            bad.append(k)
+        assert summ[k]["consistent"] == 0
+    assert not bad, "chains differing from the oracle: %s" % bad

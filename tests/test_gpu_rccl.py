@@ -1,0 +1,60 @@
+"""The multi-GPU path's collectives on real hardware (RCCL = torch.distributed "nccl" on ROCm).
+
+The box has one GPU, so the RCCL world is 1: the all-gathers still run through RCCL on cuda
+tensors, and bench.py under torch.distributed.run (--nproc-per-node 1) must give
+the single-process result bit for bit: the same selected chains, the same E[c] / E[d] / CORRMN and
+the same gathered records (script.py:55-99).  Each run is a fresh child process."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--gpus", "1", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--chains-per-gpu", "24",
+        "--calls-per-step", "20"]
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _env():
+    e = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        e.pop(k, None)
+    return e
+
+
+def _bench_line(cmd):
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=_env())
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{") and '"metric"' in l]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_rccl_collectives_world1():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "rccl_child.py")], capture_output=True, text=True,
+                       timeout=240, env=_env())
+    assert r.returncode == 0 and "rccl ok" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def test_bench_under_launcher_equals_single_process():
+    single = _bench_line([sys.executable, "bench.py"] + ARGS)
+    port = _port()
+    launched = _bench_line([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                            "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py"] + ARGS)
+    assert single["n_gpus"] == launched["n_gpus"] == 1
+    a, b = single["selection"], launched["selection"]
+    assert a["chains_selected"] == b["chains_selected"] and len(a["chains_selected"]) >= 1
+    assert a["records_sha256"] == b["records_sha256"]
+    for k in ("exp_c", "exp_d", "corr_mn"):
+        assert a[k] == b[k], k
+    assert a["samples_per_chain"] == b["samples_per_chain"] == 40

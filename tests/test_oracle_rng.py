@@ -132,6 +132,29 @@ def test_beta_moments(a, b):
     assert stats.kstest(x, "beta", args=(a, b)).pvalue > 1e-3
 
 
+def test_beta_johnk_branch_exact():
+    """gsl_ran_beta takes Johnk's method when both shapes are <= 1 (GSL 2.6 randist/beta.c); the
+    sampler reaches it with shapes (1, 1) (both counts 0).  Then pow(U, 1) = U, so the draw is
+    U / (U + V) for the first uniform_pos pair with U + V <= 1 -- restated here over the raw stream."""
+    count = 3000
+    x, words = oracle_ref.rng_stream(31, 6, count, 1.0, 1.0)
+    stream = iter(raw(31, words + 4))
+
+    def upos():
+        while True:
+            w = int(next(stream))
+            if w:
+                return w / 4294967296.0
+    exp = []
+    for _ in range(count):
+        while True:
+            u, v = upos(), upos()
+            if u + v <= 1.0:
+                exp.append(u / (u + v))
+                break
+    np.testing.assert_array_equal(x, np.array(exp))
+
+
 # ---- the opt-in Philox stream (SR_F_RNG_PHILOX) ----------------------------------------------
 # Philox4x32-10 known answers (Random123's published kat_vectors for philox4x32_10)
 PHILOX_KAT = [

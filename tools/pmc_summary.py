@@ -55,16 +55,22 @@ def main():
     ap.add_argument("--warmup", type=int, default=1, help="untimed launches at the start of each PMC pass")
     ap.add_argument("--trace-timed", type=int, default=20, help="timed launches of the kernel-trace run: its last N "
                     "sr_sweep_kernel launches (bench.py --steps; the warm-up launches come first)")
+    ap.add_argument("--tag", default="", help="directory prefix of another workload's passes in the same run "
+                    "(e.g. c5_: c5_prof, c5_fetch, c5_write, c5_sq*)")
+    ap.add_argument("--bench-json", default="", help="bench line of the workload (default <run>/bench.json)")
     args = ap.parse_args()
+    t = args.tag
+    D = {"prof": t + "prof" if t else "prof", "fetch": t + "fetch" if t else "pmc_fetch",
+         "write": t + "write" if t else "pmc_write", "sq": t + "sq" if t else "pmc_sq"}
 
     res = {"kernel": None, "source": args.run,
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over bench.py; "
                      "KiB -> bytes; FETCH_SIZE doubled (gfx950 correction, MI355X_MICROARCH.md HBM); "
                      "traffic = 2*FETCH + WRITE per sr_sweep_kernel launch, warm-up launches dropped"}
-    stats = find(os.path.join(args.run, "prof"), "kernel_stats.csv")
+    stats = find(os.path.join(args.run, D["prof"]), "kernel_stats.csv")
     if stats:
         shutil.copy(stats, args.prefix + "_kernel_stats.csv")
-    trace = find(os.path.join(args.run, "prof"), "kernel_trace.csv")
+    trace = find(os.path.join(args.run, D["prof"]), "kernel_trace.csv")
     if trace:
         durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(trace))
                 if KERNEL in r["Kernel_Name"]]
@@ -74,7 +80,7 @@ def main():
                         "min_ns_timed": min(timed) if timed else None, "max_ns_timed": max(timed) if timed else None,
                         "avg_ns_all": statistics.mean(durs) if durs else None}
         # the bench line printed by the profiled run itself (same command as the bench)
-        plog = os.path.join(args.run, "prof.log")
+        plog = os.path.join(args.run, D["prof"] + ".log")
         if os.path.exists(plog):
             for ln in open(plog):
                 if ln.startswith("{") and '"metric"' in ln:
@@ -87,8 +93,8 @@ def main():
                 fh.write('"%s",%d,%.1f,%d,%d,%.1f,"the %d timed launches of the profiled bench run (warm-up dropped)"\n'
                          % (KERNEL, len(timed), statistics.mean(timed), min(timed), max(timed),
                             statistics.pstdev(timed), len(timed)))
-    fetch = find(os.path.join(args.run, "pmc_fetch"), "counter_collection.csv")
-    write = find(os.path.join(args.run, "pmc_write"), "counter_collection.csv")
+    fetch = find(os.path.join(args.run, D["fetch"]), "counter_collection.csv")
+    write = find(os.path.join(args.run, D["write"]), "counter_collection.csv")
     if fetch and write:
         f, name = per_dispatch(fetch)
         w, _ = per_dispatch(write)
@@ -102,14 +108,35 @@ def main():
         res["write_bytes"] = wb
         res["traffic_bytes_per_launch"] = 2.0 * fb + wb
         res["launches"] = len(fk)
-    sq = find(os.path.join(args.run, "pmc_sq"), "counter_collection.csv")
-    if sq:
-        s, _ = per_dispatch(sq)
-        res["sq"] = {k: statistics.mean(v[args.warmup:]) for k, v in s.items()}
-        if "SQ_INSTS_LDS" in res["sq"] and res["sq"]["SQ_INSTS_LDS"]:
-            res["sq"]["lds_bank_conflict_cycles_per_lds_inst"] = (res["sq"].get("SQ_LDS_BANK_CONFLICT", 0.0) /
-                                                                   res["sq"]["SQ_INSTS_LDS"])
-    bench = os.path.join(args.run, "bench.json")
+    # every SQ pass (<sq>, <sq>_b, <sq>_c ...: one --pmc run each), merged per counter
+    sqd = {}
+    for d in sorted(os.listdir(args.run)):
+        if d.startswith(D["sq"]) and os.path.isdir(os.path.join(args.run, d)):
+            f = find(os.path.join(args.run, d), "counter_collection.csv")
+            if f:
+                sv, _ = per_dispatch(f)
+                for k, v in sv.items():
+                    sqd.setdefault(k, statistics.mean(v[args.warmup:]))
+    if sqd:
+        res["sq"] = sqd
+        q = sqd
+        if q.get("SQ_INSTS_LDS"):
+            q["lds_bank_conflict_cycles_per_lds_inst"] = q.get("SQ_LDS_BANK_CONFLICT", 0.0) / q["SQ_INSTS_LDS"]
+        wc = q.get("SQ_WAVE_CYCLES")
+        if wc:   # quad-cycle counters over the waves' lifetime (MI355X_MICROARCH.md, rocprofv3 PMC slots)
+            res["limiter"] = {k: q[c] / wc for k, c in (("issue_frac", "SQ_ACTIVE_INST_ANY"),
+                                                         ("valu_issue_frac", "SQ_ACTIVE_INST_VALU"),
+                                                         ("salu_issue_frac", "SQ_ACTIVE_INST_SCA"),
+                                                         ("lds_issue_frac", "SQ_ACTIVE_INST_LDS"),
+                                                         ("issue_stall_frac", "SQ_WAIT_INST_ANY"),
+                                                         ("parked_frac", "SQ_WAIT_ANY")) if c in q}
+            if "lds_bank_conflict_cycles_per_lds_inst" in q:
+                res["limiter"]["lds_bank_conflict_cycles_per_lds_inst"] = q["lds_bank_conflict_cycles_per_lds_inst"]
+            res["limiter"]["definition"] = ("fractions of SQ_WAVE_CYCLES (per-wave lifetime, quad-cycles): issue = "
+                                            "SQ_ACTIVE_INST_ANY, parked = SQ_WAIT_ANY (s_waitcnt / barrier), issue "
+                                            "stall = SQ_WAIT_INST_ANY; a wave issues at most one instruction per "
+                                            "quad-cycle")
+    bench = args.bench_json or os.path.join(args.run, "bench.json")
     if os.path.exists(bench):
         try:
             b = json.loads(open(bench).read().strip().splitlines()[-1])

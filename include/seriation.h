@@ -160,8 +160,10 @@ int sr_session_debug_flagged(const sr_session *s, int32_t chain);
 /* Device time of the last sr_session_run (ms, HIP events on the session stream; syncs). */
 double sr_session_last_kernel_ms(sr_session *s);
 int32_t sr_session_block_threads(const sr_session *s);
-/* Kernel variant the session runs: 0 = occurrence columns in LDS, 1 = columns in HBM
- * (chosen when the LDS layout exceeds 160 KB, e.g. 1024 sites x 2048 taxa). */
+/* Kernel variant the session runs: 0 = occurrence columns in LDS, one thread per taxon; 1 = columns
+ * in HBM (chosen when the LDS layout exceeds 160 KB, e.g. 1024 sites x 2048 taxa); 2 = columns in
+ * LDS, two lanes per taxon (the pair kernel: walks of <= 9 words and 257..512 taxa; opt-in with
+ * SR_KERNEL=pair in the environment and block_threads unset -- slower than variant 0). */
 int32_t sr_session_variant(const sr_session *s);
 /* Checkpoint / resume (the reference has none): the full chain state (columns, pi,
    limits, counts, c/d/loglik, MT19937 ring and cursor, acceptance counters) to a file; restoring

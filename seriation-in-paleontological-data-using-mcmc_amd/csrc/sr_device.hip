@@ -27,6 +27,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
 #define SR_TABLES_NO_ARRAYS
 #include "sr_tables.h"
 #include "sr_math.h"
@@ -73,29 +75,33 @@ __host__ __device__ static inline int sr_ckstride(int M, int TB) { return M >= T
 /* gm: the global-memory variant (columns too large for LDS, e.g. 1024 x 2048): the per-taxon
  * arrays (P, pre, ck, a/b, counts, logl terms, exact-delta terms) live in HBM (chain-private,
  * owner-thread access, L2/MALL-resident) and get no LDS slot */
-__host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB, bool gm)
+/* taxa per exact-delta chunk (one wave's taxa): 64, or 32 in the pair kernels (two lanes per taxon) */
+__host__ __device__ static inline int sr_chunk(bool pr) { return pr ? 32 : 64; }
+__host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB, bool gm, bool pr = false)
 {
   Lay L;
   size_t o = 0;
-  const int KT = (M + 63) / 64, NWV = TB / 64;
+  const int CH = sr_chunk(pr), KT = (M + CH - 1) / CH, NWV = TB / 64;
   const size_t g = gm ? 0 : 1;
+  /* step tables: one copy per wave, or one shared copy behind a barrier (pair kernels: 16 waves) */
+  const size_t NT = pr ? 1 : NWV;
   L.tab = o;   o = sr_al16(o + 512 * sizeof(double));   /* glibc exp/log tables */
-  L.cbuf = o;  o = sr_al16(o + g * 2 * KT * 64 * sizeof(double));       /* [2][KT*64] by proposal parity */
+  L.cbuf = o;  o = sr_al16(o + g * 2 * KT * CH * sizeof(double));       /* [2][KT*CH] by proposal parity */
   L.lbuf = o;  o = sr_al16(o + g * M * sizeof(double));
   L.mt = o;    o = sr_al16(o + (size_t)SR_RING * SR_MT_N * 4);
   L.P = o;     o = sr_al16(o + g * NW * M * 4);
   L.rpi0 = o;  o = sr_al16(o + (size_t)N * 4);
   L.rpi1 = o;  o = sr_al16(o + (size_t)N * 4);
   L.ht = o;    o = sr_al16(o + (size_t)NWV * (2 * N + 2) * 2);           /* per wave: hcnt[N+1], nhall[N] (int16) */
-  const size_t rw = sr_regwalk(N, TB, gm) ? 1 : 0;   /* register walks: byte tables instead of LDS checkpoints */
+  const size_t rw = (pr || sr_regwalk(N, TB, gm)) ? 1 : 0;   /* register walks (pair kernels too): byte tables instead of LDS checkpoints */
   L.ck = o;    o = sr_al16(o + g * (1 - rw) * ((N >> 5) + 1) * sr_ckstride(M, TB) * sizeof(double));
   L.ccnt = o;  o = sr_al16(o + (size_t)2 * KT * 4);
   L.sab = o;   o = sr_al16(o + g * 2 * M * 4);
   L.scnt = o;  o = sr_al16(o + g * 4 * M * 4);
   L.hpw = o;   o = sr_al16(o + (size_t)NWV * SR_NHMAX * 4);           /* per wave: hard positions */
   L.hbw = o;   o = sr_al16(o + (size_t)NWV * NW * 4);                 /* per wave: hard bitmap */
-  L.t4 = o;    o = sr_al16(o + (size_t)NWV * 160 * 8);                /* per wave: 4-entry step tables (T4STRIDE) */
-  L.t8 = o;    o = sr_al16(o + rw * NWV * T8STRIDE * 8);              /* per wave: 8-entry step tables (T8STRIDE) */
+  L.t4 = o;    o = sr_al16(o + NT * 160 * 8);                         /* per wave: 4-entry step tables (T4STRIDE) */
+  L.t8 = o;    o = sr_al16(o + rw * NT * T8STRIDE * 8);               /* per wave: 8-entry step tables (T8STRIDE) */
   L.pre = o;   o = sr_al16(o + g * (NW + 1) * M * 2);                 /* column prefix ones per word boundary */
   L.part = o;  o = sr_al16(o + (size_t)2 * 16 * NWV * 8 * 4);         /* [2][proposal][wave] count sums */
   L.tot = o;   o = sr_al16(o + (size_t)2 * NWV * 4 * 4);               /* [2][wave] t0, f0, t1, f1 */
@@ -1072,6 +1078,215 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
   return res;
 }
 
+/* ---- pair kernels: two lanes per taxon ---------------------------------------------------
+ * Lanes 2t and 2t+1 of a wave share taxon t; the even lane ("lo") holds walk words 0..4 of a
+ * Gibbs draw, the odd lane ("hi") words 5..8 (walks of <= 9 words: N <= 287).  Partner values
+ * travel by one DPP quad_perm [1,0,3,2] (lane ^ 1) each. */
+__device__ __forceinline__ int pair_swap_i32(int x) { return __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false); }
+__device__ __forceinline__ double pair_swap_f64(double v)
+{
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)pair_swap_i32((int)(uint32_t)b), hi = (uint32_t)pair_swap_i32((int)(uint32_t)(b >> 32));
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+/* draw_fast_s<9> (mcmc_auxa + mcmc_logtop + mcmc_randompick, certified) with the walk split over a
+ * lane pair: each lane runs passes 0 and 1 over its five words; the hi lane's chain starts from
+ * y' = 1 at word 5 and is rescaled by the lo lane's y at word 5 (S = S_lo + y5 S'_hi, checkpoints
+ * S_lo + y5 ck'_k: a re-association of the same products, two more roundings per value -- inside
+ * REL, which gains 8 units for them); pass 2 runs identically in both lanes on word j's data taken
+ * from the lane that holds it.  wk: this lane's words 5h .. 5h+4 (word 9 = 0).  Both lanes return
+ * the same pick and count deltas.  Call pair-uniformly (both lanes active). */
+__device__ __forceinline__ int draw_pair9(const uint32_t (&wk)[5], int h, const uint32_t *Pm, int M, int N, int NW, bool rev,
+                                          int o, int L, int POo, double u, const CD &K, const sr_mtab &tb, double vA,
+                                          double vB, const double *T4, const double *T8, uint64_t *fbk, int &dt0, int &df0,
+                                          int &dt1, int &df1)
+{
+  constexpr int NWM = 9, NH = 5;
+  const int k0 = NH * h;
+  const int nk = (L >> 5) + 1;
+  const int kl = L >> 5, nbl = (L & 31) + 1;
+  /* ---- pass 0: window of words that can hold mass above 2^-40 relative to entry o */
+  int Otot = 0;
+#pragma unroll
+  for (int i = 0; i < NH; ++i) Otot += __popc(wk[i]);
+  const int Op = pair_swap_i32(Otot);
+  int klo = NWM, khi = -1;
+  double qlo = 0.0;
+  uint32_t wl = 0u;
+  {
+    const double dv = vB - vA;
+    const double Fo = __builtin_fma((double)POo, dv, (double)o * vA);
+    int O = h ? Op : 0;
+    const uint32_t lastm = (2u << (L & 31)) - 1u;
+#pragma unroll
+    for (int i = 0; i < NH; ++i) {
+      const int k = k0 + i;
+      const bool full = k < kl;
+      const int nb = full ? 32 : nbl;
+      const uint32_t vm = full ? 0xffffffffu : lastm;
+      const double qs = Fo - __builtin_fma((double)O, dv, (double)(32 * k) * vA);
+      const int ones = __popc(wk[i] & vm);
+      const double ub = qs - (double)(nb - ones) * vA;
+      const bool in = (k < nk) && ub > -SR_WIN_T;
+      const bool first = in && klo == NWM;
+      qlo = first ? qs : qlo;
+      klo = first ? k : klo;
+      khi = in ? k : khi;
+      O += __popc(wk[i]);
+      wl = (k == kl) ? wk[i] : wl;
+    }
+    const int klo_p = pair_swap_i32(klo), khi_p = pair_swap_i32(khi);
+    const double qlo_p = pair_swap_f64(qlo);
+    const uint32_t wl_p = (uint32_t)pair_swap_i32((int)wl);
+    qlo = (klo <= klo_p) ? qlo : qlo_p;
+    klo = min(klo, klo_p);
+    khi = max(khi, khi_p);
+    wl |= wl_p;
+  }
+  /* ---- pass 1: my words' sums (lo: from y0; hi: relative to y = 1 at word 5), then combined */
+  const double y0 = exp2_split(qlo);
+  double S = 0.0;
+  double ckr[NH], yst[NH];
+  double y = h ? 1.0 : y0;
+  {
+    auto wload = [&](int i, double2 (&t)[4]) {
+      const int k = k0 + i;
+      const bool inw = k >= klo && k <= khi;
+      const int nfk = inw ? ((k < kl) ? 4 : (nbl >> 3)) : 0;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const uint32_t e = (g < nfk) ? ((wk[i] >> (8 * g)) & 255u) : 256u;
+        t[g] = *reinterpret_cast<const double2 *>(T8 + 2 * e);
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < NH; ++i) {
+      double2 t[4];   /* no read-ahead: four waves per SIMD cover the table reads' latency */
+      wload(i, t);
+      yst[i] = y;
+      {
+        const double w23 = __builtin_fma(t[2].y, t[3].x, t[2].x);
+        const double w13 = __builtin_fma(t[1].y, w23, t[1].x);
+        const double W = __builtin_fma(t[0].y, w13, t[0].x);
+        const double pw = (t[0].y * t[1].y) * (t[2].y * t[3].y);
+        S = __builtin_fma(y, W, S);
+        y = y * pw;
+      }
+      ckr[i] = S;
+    }
+    /* the partial byte (c8 entries), by the lane that holds its word, when it lies in the window */
+    const int nfull = (L + 1) >> 3, c8 = (L + 1) & 7, kb = nfull >> 2;
+    const bool actb = c8 > 0 && kb >= klo && kb <= khi && kb >= k0 && kb < k0 + NH;
+    const uint32_t eb = (wl >> (8 * (nfull & 3))) & 255u;
+    const double2 tlo = t4sp(T4, actb ? min(c8, 4) : 0, eb & 15u);
+    const double shi = t4s(T4, actb ? max(c8 - 4, 0) : 0, eb >> 4);
+    S = __builtin_fma(y, tlo.x, S);
+    S = __builtin_fma(y * tlo.y, shi, S);
+  }
+  const double S_p = pair_swap_f64(S), y_p = pair_swap_f64(y);
+  const double S_lo = h ? S_p : S, y5 = h ? y_p : y, S_hi = h ? S : S_p;
+  const double St = S_lo + y5 * S_hi;
+  {
+    const double cb = h ? S_lo : 0.0, cs = h ? y5 : 1.0;
+#pragma unroll
+    for (int i = 0; i < NH; ++i) { ckr[i] = cb + cs * ckr[i]; yst[i] = cs * yst[i]; }
+  }
+  /* ---- pass 2 (both lanes, identical data): word, byte, nibble, entry; certification */
+  int res = -1, POp = 0;
+  if (St > 0.0 && St < 0x1p1000) {
+    const double inv = 1.0 / St;
+    const double REL = (double)(N + 41) * 0x1p-50;
+    const double ABS = (double)(N + 1) * 0x1p-39;
+    const double uS = u * St;
+    int jl = 0;
+#pragma unroll
+    for (int i = 0; i < NH; ++i) jl += (k0 + i < khi && ckr[i] < uS) ? 1 : 0;
+    int j = jl + pair_swap_i32(jl);
+    j = max(j, klo);
+    const int ij = j - k0, ijm = j - 1 - k0;
+    double cy = 0.0, csp = 0.0;
+    uint32_t cww = 0u;
+    int cO = h ? Op : 0;   /* ones among walk entries [0, 32 j) when I hold word j */
+#pragma unroll
+    for (int i = 0; i < NH; ++i) {
+      if (i == ij) { cy = yst[i]; cww = wk[i]; }
+      cO += (i < ij) ? __popc(wk[i]) : 0;
+      if (i == ijm) csp = ckr[i];
+    }
+    const double cy_p = pair_swap_f64(cy), csp_p = pair_swap_f64(csp);
+    const uint32_t cww_p = (uint32_t)pair_swap_i32((int)cww);
+    const int cO_p = pair_swap_i32(cO);
+    const bool own = ij >= 0 && ij < NH, ownm = ijm >= 0 && ijm < NH;
+    const double yj = own ? cy : cy_p, Sp0 = ownm ? csp : csp_p;
+    const uint32_t ww = own ? cww : cww_p;
+    const int Oj = own ? cO : cO_p;
+    const int w0 = 32 * j;
+    const int nb = min(32, L + 1 - w0);
+    const int nfb = nb >> 3, nlb = (nb + 7) >> 3;
+    double2 tb8[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) tb8[g] = *reinterpret_cast<const double2 *>(T8 + 2 * ((ww >> (8 * g)) & 255u));
+    double Bg[4], Yg[4];
+    int nbc = 0;
+    {
+      double acc = Sp0, yy = yj;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        Yg[g] = yy;
+        acc = __builtin_fma(yy, tb8[g].x, acc);
+        Bg[g] = acc;
+        yy = yy * tb8[g].y;
+        nbc += (g < nfb && acc < uS) ? 1 : 0;
+      }
+    }
+    const int bsel = min(nbc, nlb - 1);
+    double base_b = Sp0, y_b = yj;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      if (g == bsel) y_b = Yg[g];
+      if (g + 1 == bsel) base_b = Bg[g];
+    }
+    const uint32_t bv = (ww >> (8 * bsel)) & 255u;
+    const int ce = min(nb - 8 * bsel, 8), c_lo = min(ce, 4), c_hi = ce - c_lo;
+    const double2 tlo = t4sp(T4, c_lo, bv & 15u);
+    const double N0 = __builtin_fma(y_b, tlo.x, base_b);
+    const bool nsel = c_hi > 0 && N0 < uS;
+    const int gsel = 2 * bsel + (nsel ? 1 : 0);
+    const double base = nsel ? N0 : base_b, ys = nsel ? y_b * tlo.y : y_b;
+    const uint32_t nibs = nsel ? (bv >> 4) : (bv & 15u);
+    const int cmax = nsel ? c_hi : c_lo;
+    const double P1 = __builtin_fma(ys, t4s(T4, 1, nibs), base), P2 = __builtin_fma(ys, t4s(T4, 2, nibs), base);
+    const double P3 = __builtin_fma(ys, t4s(T4, 3, nibs), base), P4 = __builtin_fma(ys, t4s(T4, 4, nibs), base);
+    const int nc = ((cmax > 1 && P1 < uS) ? 1 : 0) + ((cmax > 2 && P2 < uS) ? 1 : 0) + ((cmax > 3 && P3 < uS) ? 1 : 0);
+    const double Ph = (nc == 0) ? P1 : (nc == 1) ? P2 : (nc == 2) ? P3 : P4;
+    const double Pp = (nc == 0) ? base : (nc == 1) ? P1 : (nc == 2) ? P2 : P3;
+    const int w = w0 + 4 * gsel + nc;
+    const double t = u - Ph * inv, tprev = u - Pp * inv;
+    const double e = 2.0 * REL * fmin(Ph, St - Ph) * inv + ABS;
+    const double eprev = 2.0 * REL * fmin(Pp, St - Pp) * inv + ABS;
+    const bool prev_ok = (w == 0) || (tprev > eprev);
+    const bool here_ok = (w == L) || (t < -e);
+#ifndef SR_FORCE_EXACT
+    if (prev_ok && here_ok) {
+      res = w;
+      POp = Oj + __popc(ww & ((1u << (w & 31)) - 1u));
+    }
+#else
+    (void)prev_ok; (void)here_ok; (void)w; (void)Oj;
+#endif
+  }
+  if (res < 0) {
+    if (h == 0) atomicAdd((unsigned long long *)fbk, 1ull);   /* exact-walk fallbacks (counted once per taxon) */
+    res = draw_exact(Pm, M, N, rev, o, L, u, K, tb);
+    POp = walk_prefix(Pm, M, N, NW, rev, res);
+  }
+  if (res == o) { dt0 = df0 = dt1 = df1 = 0; }
+  else if (res < o) { int O = POo - POp; int Z = (o - res) - O; dt0 = -Z; df0 = Z; dt1 = O; df1 = -O; }
+  else { int O = POp - POo; int Z = (res - o) - O; dt0 = Z; df0 = -Z; dt1 = -O; df1 = O; }
+  return res;
+}
+
 /* the forward walk words of column m (positions), NW <= NWM */
 template <int NWM>
 __device__ __forceinline__ void load_fwd(const uint32_t *Pm, int M, int NW, uint32_t (&fw)[NWM])
@@ -1206,13 +1421,14 @@ __device__ __forceinline__ int wave_sum_i32(int x)
  * 1435, 1630), computed by lane 0 of the calling wave and broadcast through its slot.
  * Zero terms are skipped (adding +-0 is exact; s is never -0.0).  Nonzero terms were
  * compacted per 64-taxon chunk (ascending m) into cbuf with counts ccnt. */
-__device__ __forceinline__ double exact_sum_wave(const double *cbuf, const int *ccnt, int nch, double *slot, int lane)
+__device__ __forceinline__ double exact_sum_wave(const double *cbuf, const int *ccnt, int nch, double *slot, int lane,
+                                                 int CH = 64)
 {
   if (lane == 0) {
     double s = 0.0;
     for (int ch = 0; ch < nch; ++ch) {
       const int n = ccnt[ch];
-      const double *p = cbuf + ch * 64;
+      const double *p = cbuf + ch * CH;
       int j = 0;
       for (; j + 4 <= n; j += 4) {
         const double a0 = p[j], a1 = p[j + 1], a2 = p[j + 2], a3 = p[j + 3];
@@ -1361,24 +1577,30 @@ __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, 
 /* The exact delta of one proposal: the reference's per-taxon terms (qval, mcmc.c:1214,
  * 1435, 1630 term order) compacted per 64-taxon chunk into cb, then summed sequentially in
  * ascending m by lane 0 of every wave.  Block-uniform call (contains a barrier). */
+/* PR (pair kernels): taxon m = m0 + lane / 2 is evaluated by its even lane; a wave's 32 taxa form
+ * one chunk (ballot bits of even lanes in ascending lane order = ascending m).  KT = chunks. */
+template <bool PR>
 __device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const int32_t *sab, const uint32_t *P, const uint16_t *pre,
                                               int M, int KT,
                                               int hl, int nh, const int16_t *hcnt, const int16_t *nhall, double *cb, int *cc, double *xs,
                                               int lane, int wave, int TB)
 {
-  for (int m0 = wave * 64; m0 < KT * 64; m0 += TB) {
-    const int ch = m0 >> 6, m = m0 + lane;
+  constexpr int CH = PR ? 32 : 64;
+  const bool ev = PR ? (lane & 1) == 0 : true;
+  for (int m0 = wave * CH; m0 < KT * CH; m0 += (PR ? TB / 2 : TB)) {
+    const int ch = m0 / CH, m = m0 + (PR ? (lane >> 1) : lane);
     int dt0 = 0, dt1 = 0;
-    if (m < M) taxon_dt(kind, q, sab[m], sab[M + m], P + m, pre + m, M, kind == PK_PI3 ? hard_bits_col(P + m, M, hl, nh) : 0u,
-                        hcnt, nhall, dt0, dt1);
-    const double tv = (m < M) ? qval(dt0, -dt0, dt1, -dt1, K) : 0.0;
+    if (m < M && ev)
+      taxon_dt(kind, q, sab[m], sab[M + m], P + m, pre + m, M, kind == PK_PI3 ? hard_bits_col(P + m, M, hl, nh) : 0u,
+               hcnt, nhall, dt0, dt1);
+    const double tv = (m < M && ev) ? qval(dt0, -dt0, dt1, -dt1, K) : 0.0;
     const uint64_t msk = __ballot(tv != 0.0);
     const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
-    if (tv != 0.0) cb[ch * 64 + pos] = tv;
+    if (tv != 0.0) cb[ch * CH + pos] = tv;
     if (lane == 0) cc[ch] = __popcll(msk);
   }
   __syncthreads();
-  return exact_sum_wave(cb, cc, KT, xs, lane);
+  return exact_sum_wave(cb, cc, KT, xs, lane, CH);
 }
 
 /* words of slack kept resident after the Gibbs draws: the proposals and the next c, d
@@ -1395,16 +1617,20 @@ __device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const i
  *   B  Gibbs (a_m, b_m) of own taxa (mcmc_sampleab); [barrier + logl on the last sweep]
  *   C  16 MH permutation proposals: draws, own taxa's count deltas and terms, per-wave
  *      partial sums -> one barrier -> certified decision -> apply to own taxa. */
-template <int TB, int NWM, bool GM>
+template <int TB, int NWM, bool GM, bool PR = false>
 __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NWV = TB / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  /* PR (pair kernels): lanes 2t, 2t+1 own taxon t (tx) together, hf = which half of the pair;
+     otherwise one thread per taxon */
+  const int hf = PR ? (tid & 1) : 0, tx = PR ? (tid >> 1) : tid;
+  constexpr int TXS = PR ? TB / 2 : TB;   /* taxon stride */
   const int chain = blockIdx.x;
   const int N = A.N, M = A.M, NW = A.NW, nh = A.nh;
-  const int KT = (M + 63) >> 6;
-  const Lay L = sr_layout(N, M, NW, TB, GM);
+  const int KTC = (M + sr_chunk(PR) - 1) / sr_chunk(PR);   /* exact-delta chunks */
+  const Lay L = sr_layout(N, M, NW, TB, GM, PR);
   double *tabs = (double *)(smem + L.tab);
   /* GM: the per-taxon arrays are the chain's HBM state itself (P, a/b, counts: updated in
      place) or its HBM scratch; otherwise LDS copies loaded here and stored at the end */
@@ -1424,8 +1650,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   int32_t *scnt = GM ? A.cnt + (size_t)chain * 4 * M : (int32_t *)(smem + L.scnt);  /* t0[M], f0[M], t1[M], f1[M] */
   int *hp = (int *)(smem + L.hpw) + wave * SR_NHMAX;   /* this wave's copy of the hard positions */
   uint32_t *hbw = (uint32_t *)(smem + L.hbw) + wave * NW;   /* this wave's hard bitmap */
-  double *T4w = (double *)(smem + L.t4) + wave * T4STRIDE;   /* this wave's 4-step tables */
-  double *T8w = (double *)(smem + L.t8) + wave * T8STRIDE;   /* this wave's 8-step tables (register walks) */
+  double *T4w = (double *)(smem + L.t4) + (PR ? 0 : wave) * T4STRIDE;   /* this wave's (PR: the block's) 4-step tables */
+  double *T8w = (double *)(smem + L.t8) + (PR ? 0 : wave) * T8STRIDE;   /* this wave's (PR: the block's) 8-step tables */
   int *part = (int *)(smem + L.part);
   int *tot = (int *)(smem + L.tot);
   double *xs = (double *)(smem + L.xs) + wave;
@@ -1486,7 +1712,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   for (int m = tid; m < M; m += TB) col_pre_build(pre + m, P + m, M, NW);   /* own columns */
   {
     const int hl0 = (lane < nh) ? hp[lane] : 0;   /* loaded with every lane active */
-    if (M <= TB && tid < M) hbc = hard_bits_col(P + tid, M, hl0, nh);
+    if (M <= TXS && tx < M) hbc = hard_bits_col(P + tx, M, hl0, nh);
   }
   const double ec = sr_exp_m(SR_LOGEPSILON, &tb);
   const uint32_t nhard = (uint32_t)nh;
@@ -1541,7 +1767,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       const double vB = (K.dd - K.c) * 1.4426950408889634;
       const double r2 = sr_exp_m(oddl ? K.c - K.dd : K.cc - K.d, &tb);
       const double rA = readlane_f64(r2, 0), rB = readlane_f64(r2, 1);   /* 2^-vA, 2^-vB */
-      if (lane < 16) {   /* per-wave tables for 4 walk entries with bits = lane */
+      /* PR: one shared copy of the tables, built by waves 0-4 (T8 quarters, T4), then a barrier */
+      if ((!PR || wave == 4) && lane < 16) {   /* per-wave tables for 4 walk entries with bits = lane */
         double pr = 1.0, sm = 1.0;
         double sc[5];
         sc[0] = 0.0;
@@ -1556,16 +1783,16 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       if constexpr (NWM > 0) {   /* per-wave tables for 8 walk entries with bits = e: {sum of the 8 prefix
                                     products, product of all 8}; 4 entries per lane */
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int e = lane + 64 * q;
+        for (int q = 0; q < (PR ? 1 : 4); ++q) {
+          const int e = lane + 64 * (PR ? wave : q);
           double pr = 1.0, sm = 0.0;
 #pragma unroll
           for (int k = 0; k < 8; ++k) { sm = sm + pr; pr = pr * (((e >> k) & 1) ? rB : rA); }
-          *reinterpret_cast<double2 *>(T8w + 2 * e) = make_double2(sm, pr);
+          if (!PR || wave < 4) *reinterpret_cast<double2 *>(T8w + 2 * e) = make_double2(sm, pr);
         }
-        if (lane == 0) *reinterpret_cast<double2 *>(T8w + 2 * 256) = make_double2(0.0, 1.0);
+        if (lane == 0 && (!PR || wave == 4)) *reinterpret_cast<double2 *>(T8w + 2 * 256) = make_double2(0.0, 1.0);
       }
-      wsync();
+      if constexpr (PR) __syncthreads(); else wsync();
 
 #ifdef SR_STAMP_GIBBS
       STAMP(5);
@@ -1585,7 +1812,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         FST(1);
         rng_ensure(R, min(2 * (mhi - mlo) + SR_RNG_SLACK, rcap), tid, TB);
         FST(8);
-        for (int m = mlo + tid; m < mhi; m += TB) {
+        for (int m = mlo + tx; m < mhi; m += TXS) {   /* PR: pair-uniform */
           const uint32_t *Pm = P + m;
           const double ua = rng_peek(R, 2 * (m - mlo)) / 4294967296.0;
           const double ub = rng_peek(R, 2 * (m - mlo) + 1) / 4294967296.0;
@@ -1594,7 +1821,25 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           /* a_m over [0, b_m], then b_m over the reversed column with limit N - a_new: one
              inlined copy of the draw, two trips */
           int na = a0, nb = b0;
-          if constexpr (NWM > 0) {   /* column in registers, branch-free draws */
+          if constexpr (PR) {   /* pair kernels: each lane of the pair walks half of the words */
+            const uint16_t *prem = pre + m;
+            const int POa = col_pre(prem, Pm, M, a0);
+            const int POb = (int)prem[NW * M] - col_pre(prem, Pm, M, b0);
+            uint32_t wk[5];
+            int d0, e0, d1, e1;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) { const int k = 5 * hf + i; wk[i] = (k < NW) ? Pm[min(k, NW - 1) * M] : 0u; }
+            na = draw_pair9(wk, hf, Pm, M, N, NW, false, a0, b0, POa, ua, K, tb, vA, vB, T4w, T8w, &misc[MS_FBK], d0, e0, d1, e1);
+            t0 += d0; f0 += e0; t1 += d1; f1 += e1;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+              const int k = 5 * hf + i;
+              wk[i] = (k < NW) ? walk_word(Pm, M, N, NW, true, min(k, NW - 1)) : 0u;
+            }
+            nb = N - draw_pair9(wk, hf, Pm, M, N, NW, true, N - b0, N - na, POb, ub, K, tb, vA, vB, T4w, T8w, &misc[MS_FBK],
+                                d0, e0, d1, e1);
+            t0 += d0; f0 += e0; t1 += d1; f1 += e1;
+          } else if constexpr (NWM > 0) {   /* column in registers, branch-free draws */
             uint32_t wk[NWM];   /* forward walk words, then (second trip) the reversed ones */
             load_fwd<NWM>(Pm, M, NW, wk);
             /* ones before each trip's start entry from the column prefix table: forward, positions
@@ -1626,11 +1871,13 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             t0 += d0; f0 += e0; t1 += d1; f1 += e1;
             if (rev) nb = N - res; else na = res;
           }
-          nchg += (na != a0) + (nb != b0);
-          sab[m] = na; sab[M + m] = nb;
-          scnt[m] = t0; scnt[M + m] = f0; scnt[2 * M + m] = t1; scnt[3 * M + m] = f1;
-          if (want_logl)   /* mcmc_logl term (mcmc.c:643-644) */
-            lbuf[m] = (double)t0 * K.cc + (double)f0 * K.d + (double)t1 * K.dd + (double)f1 * K.c;
+          if (!PR || hf == 0) {   /* PR: the even lane writes the pair's results */
+            nchg += (na != a0) + (nb != b0);
+            sab[m] = na; sab[M + m] = nb;
+            scnt[m] = t0; scnt[M + m] = f0; scnt[2 * M + m] = t1; scnt[3 * M + m] = f1;
+            if (want_logl)   /* mcmc_logl term (mcmc.c:643-644) */
+              lbuf[m] = (double)t0 * K.cc + (double)f0 * K.d + (double)t1 * K.dd + (double)f1 * K.c;
+          }
         }
         rng_skip(R, 2 * (mhi - mlo));
         }
@@ -1641,7 +1888,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       STAMP(1);
       if (want_logl) {   /* mcmc_logl (mcmc.c:639-645), sequential over m, lane 0 of every wave */
         __syncthreads();
-        if (lane == 0) {
+        if (PR ? tid == 0 : lane == 0) {
           double s = 0.0;
           int m = 0;
           for (; m + 4 <= M; m += 4) {
@@ -1649,11 +1896,16 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             s = s + a0; s = s + a1; s = s + a2; s = s + a3;
           }
           for (; m < M; ++m) s = s + lbuf[m];
-          *xs = s;
+          if (PR) *reinterpret_cast<double *>(&misc[MS_LOGL]) = s; else *xs = s;
         }
-        wsync();
-        loglik = *xs;
-        wsync();
+        if constexpr (PR) {   /* one sum (thread 0), read by all behind a barrier */
+          __syncthreads();
+          loglik = *reinterpret_cast<const double *>(&misc[MS_LOGL]);
+        } else {
+          wsync();
+          loglik = *xs;
+          wsync();
+        }
       }
       STAMP(2);
       FST(0);
@@ -1914,10 +2166,10 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           int *pw = part + (bpar * 16) * NWV * 8;
           const bool pack = N < 512;   /* one taxon per thread: per-wave sums fit 16-bit fields */
           /* own taxon's limits and hard-site bits, fixed for the batch (one taxon per thread) */
-          const bool one = M <= TB;
+          const bool one = M <= TXS;
           int a1 = 0, b1 = 0;
           const uint32_t hb1 = hbc;
-          if (one && tid < M) { a1 = sab[tid]; b1 = sab[M + tid]; }
+          if (one && tx < M) { a1 = sab[tx]; b1 = sab[M + tx]; }
           FST(13);
 #if defined(SR_STAMP_DRAWS)
           STAMP(5);
@@ -1926,7 +2178,52 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 #else
           STAMP(3);
 #endif
-          if (one) {
+          if constexpr (PR) {
+            /* pair kernels: the proposals in slot pairs of one code path (kinds pi1, pi2 / swap,
+               pi3); the even lane of a taxon evaluates the pair's first proposal, the odd lane the
+               second, and the per-wave sums are kept per lane parity (the two proposals' sums) */
+            constexpr int SPA[9] = {1, 2, 3, 7, 8, 9, 13, 14, 15};
+            constexpr int SPB[9] = {4, 5, 6, 10, 11, 12, -1, 0, -1};
+            constexpr uint64_t EV = 0x5555555555555555ull, OD = 0xAAAAAAAAAAAAAAAAull;
+#pragma unroll
+            for (int sp = 0; sp < 9; ++sp) {   /* terms and their sums per slot pair (no per-slot arrays:
+                                                  the register budget is 128 at four waves per SIMD) */
+              const int pa = SPA[sp], pb = SPB[sp];
+              const bool va = pa >= p0 && pa < pend && !(__builtin_amdgcn_readlane(vfl, pa) & 4);
+              const bool vb = pb >= 0 && pb >= p0 && pb < pend && !(__builtin_amdgcn_readlane(vfl, pb >= 0 ? pb : 0) & 4);
+              if (va || vb) {
+                const Prop qa = load_prop(pa), qb = load_prop(pb >= 0 ? pb : pa);
+                Prop q;
+                q.i = hf ? qb.i : qa.i; q.j = hf ? qb.j : qa.j; q.ii = hf ? qb.ii : qa.ii; q.jj = hf ? qb.jj : qa.jj;
+                q.inc1 = hf ? qb.inc1 : qa.inc1; q.inc2 = hf ? qb.inc2 : qa.inc2;
+                q.Kn = hf ? qb.Kn : qa.Kn; q.r0 = hf ? qb.r0 : qa.r0;
+                int d0 = 0, d1 = 0;
+                if ((hf ? vb : va) && tx < M)
+                  taxon_dt(prop_kind(pa), q, a1, b1, P + tx, pre + tx, M, hb1, hcnt, nhall, d0, d1);
+                int Xa0, Xa1, Ya, Xb0, Xb1, Yb;
+                if (prop_kind(pa) == PK_PI1) {   /* dt in {-1, 0, 1}, dt0 dt1 = 0: ballot counts per parity */
+                  const uint64_t p0m = __ballot(d0 > 0), n0m = __ballot(d0 < 0);
+                  const uint64_t p1m = __ballot(d1 > 0), n1m = __ballot(d1 < 0);
+                  Xa0 = (int)__popcll(p0m & EV) - (int)__popcll(n0m & EV); Xb0 = (int)__popcll(p0m & OD) - (int)__popcll(n0m & OD);
+                  Xa1 = (int)__popcll(p1m & EV) - (int)__popcll(n1m & EV); Xb1 = (int)__popcll(p1m & OD) - (int)__popcll(n1m & OD);
+                  Ya = (int)(__popcll((p0m | n0m) & EV) + __popcll((p1m | n1m) & EV));
+                  Yb = (int)(__popcll((p0m | n0m) & OD) + __popcll((p1m | n1m) & OD));
+                } else {   /* 16-bit field per parity: 32 lanes x (dt + N) < 2^16 for N < 1024 */
+                  const int sh = 16 * hf;
+                  const uint32_t u0 = (uint32_t)wave_sum_i32((int)((uint32_t)(d0 + N) << sh));
+                  const uint32_t u1 = (uint32_t)wave_sum_i32((int)((uint32_t)(d1 + N) << sh));
+                  const uint32_t u2 = (uint32_t)wave_sum_i32((int)((uint32_t)(abs(d0) + abs(d1)) << sh));
+                  Xa0 = (int)(u0 & 0xffffu) - 32 * N; Xb0 = (int)(u0 >> 16) - 32 * N;
+                  Xa1 = (int)(u1 & 0xffffu) - 32 * N; Xb1 = (int)(u1 >> 16) - 32 * N;
+                  Ya = (int)(u2 & 0xffffu); Yb = (int)(u2 >> 16);
+                }
+                if (lane == 0 && va) { int *o = pw + (pa * NWV + wave) * 8; o[0] = Xa0; o[1] = Xa1; o[2] = Ya; o[3] = 0; }
+                if (lane == 1 && vb) { int *o = pw + (pb * NWV + wave) * 8; o[0] = Xb0; o[1] = Xb1; o[2] = Yb; o[3] = 0; }
+              }
+            }
+            FST(3);
+            STAMP_K(PK_PI3);
+          } else if (one) {
             /* one taxon per thread: all 16 proposal slots unrolled; slot s has the compile-time
                kind prop_kind(s), so each copy holds one kind's code and the slots' loads, ALU
                and reductions are independent */
@@ -2017,7 +2314,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                   X0 += o[0]; X1 += o[1]; Y0 += o[2]; Y1 += o[3];
                 }
                 Sp = ((double)X0 * K.cc - (double)X0 * K.d) + ((double)X1 * K.dd - (double)X1 * K.c);
-                const double B = (double)Y0 * aC + (double)Y1 * aD;
+                /* PR: o[2] holds Y0 + Y1 (one packed field), o[3] = 0 -- bounded by the larger coefficient */
+                const double B = PR ? (double)(Y0 + Y1) * fmax(aC, aD) : (double)Y0 * aC + (double)Y1 * aD;
                 Knz = Y0 + Y1;   /* >= the number of nonzero terms: each has |dt0| + |dt1| >= 1 */
                 Ebp = ((double)Knz + 16.0) * 0x1p-52 * B;
                 uwp = (uint32_t)vuw;
@@ -2065,7 +2363,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               }
             }
             if (!decided || (accept && want_logl && !have_exact)) {   /* the exact sequential delta */
-              dl = sr_exact_delta(kind, q, K, sab, P, pre, M, KT, hl, nh, hcnt, nhall, cbuf + xpar * KT * 64, ccnt + xpar * KT,
+              dl = sr_exact_delta<PR>(kind, q, K, sab, P, pre, M, KTC, hl, nh, hcnt, nhall, cbuf + xpar * KTC * sr_chunk(PR),
+                                      ccnt + xpar * KTC,
                                   xs, lane, wave, TB);
               xpar ^= 1;
               if (!decided) {
@@ -2101,7 +2400,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           if (tid == 0) misc[MS_ACC + (kind == PK_PI1 ? 3 : kind == PK_PI2 ? 4 : kind == PK_SWAP ? 5 : 6)]++;
           loglik += delta;
           const int16_t *nhp = nhall + q.r0;   /* pi3: the non-hard positions of [i, j] in order */
-          for (int m = tid; m < M; m += TB) {
+          for (int m = (PR && hf) ? M : tx; m < M; m += TXS) {   /* PR: the even lane of each pair */
             uint32_t *Pm = P + m;
             const int a = sab[m], b = sab[M + m];
             int dt0, dt1;
@@ -2272,7 +2571,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   fprintf(stderr, "seriation: HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); return -5; } } while (0)
 
 struct srk_dev {
-  int device, N, M, NW, nh, nchains, TB, TPT, rec_cap, gm;
+  int device, N, M, NW, nh, nchains, TB, TPT, rec_cap, gm, pr;
   size_t lds;
   hipStream_t stream;
   int own_stream;
@@ -2287,8 +2586,26 @@ typedef void (*sr_kfn)(KArgs);
 
 /* NWM: walks of <= 9 / 17 words (N + 1 entries: N <= 287 / 543) use the register-resident
  * Gibbs draw, longer ones the LDS walk.  gm: the HBM-column variant (sr_layout) */
-static sr_kfn sr_pick_kernel(int TB, int N, bool gm)
+/* the pair kernel (two lanes per taxon, 1024 threads): walks of <= 9 words (N <= 287) and 257..512
+ * taxa with columns in LDS.  Opt-in (SR_KERNEL=pair in the environment): bit-exact, but 1.67x slower
+ * than the one-thread-per-taxon kernel on the bench workload (profiles/r03c_ab_pair.json: 24.6 vs
+ * 14.7 ms per launch) -- its per-wave instruction count fell only 13 % (4.3 k vs 5.0 k VALU per
+ * wave per sweep: most of a wave's work is per proposal and per sweep, not per taxon, and all 16
+ * waves repeat it), the 128-VGPR budget spills 171 registers, and waves park 60 % of their cycles
+ * (r03d SQ passes). */
+static bool sr_pair_ok(int N, int M)
 {
+  const char *e = getenv("SR_KERNEL");
+  if (!e || strcmp(e, "pair") != 0) return false;
+  return sr_nwm(N) == 9 && M > 256 && M <= 512;
+}
+
+static sr_kfn sr_pick_kernel(int TB, int N, bool gm, bool pr = false)
+{
+  if (pr) return (TB == 1024 && !gm) ? (sr_kfn)sr_sweep_kernel<1024, 9, false, true> : nullptr;
+#ifdef SR_PAIR_ONLY   /* register-pressure experiments: compile the pair kernel alone */
+  return nullptr;
+#endif
   if (gm) {
     if (TB == 256) return (sr_kfn)sr_sweep_kernel<256, 0, true>;
     if (TB == 512) return (sr_kfn)sr_sweep_kernel<512, 0, true>;
@@ -2331,18 +2648,23 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
   srk_dev *d = new srk_dev();
   d->device = device; d->N = st->N; d->M = st->M; d->NW = st->NW; d->nh = st->nh; d->nchains = st->nchains;
   int TB = block_threads;
+  /* default: the pair kernel where it applies (two lanes per taxon, 1024 threads), else one thread
+     per taxon in the smallest block of 256..1024 threads that covers M */
+  d->pr = (TB <= 0 && gm_force != 1 && sr_pair_ok(st->N, st->M)) ? 1 : 0;
+  if (d->pr) TB = 1024;
   if (TB <= 0) { TB = 256; while (TB < st->M && TB < 1024) TB *= 2; }
   d->TB = TB; d->TPT = 1;
   /* columns in LDS when the whole layout fits, else the HBM-column variant */
   d->gm = 0;
-  Lay L = sr_layout(st->N, st->M, st->NW, TB, false);
+  Lay L = sr_layout(st->N, st->M, st->NW, TB, false, d->pr != 0);
   if (L.total > 160 * 1024) { d->gm = 1; L = sr_layout(st->N, st->M, st->NW, TB, true); }
   if (gm_force >= 0 && gm_force != d->gm) {   /* explicit variant request (tests) */
     d->gm = gm_force;
-    L = sr_layout(st->N, st->M, st->NW, TB, d->gm != 0);
+    L = sr_layout(st->N, st->M, st->NW, TB, d->gm != 0, d->pr != 0);
   }
+  if (d->gm) d->pr = 0;
   d->lds = L.total;
-  if (!sr_pick_kernel(TB, st->N, d->gm != 0) || d->lds > 160 * 1024) { delete d; return -6; }
+  if (!sr_pick_kernel(TB, st->N, d->gm != 0, d->pr != 0) || d->lds > 160 * 1024) { delete d; return -6; }
   d->rec_cap = rec_cap_calls > 0 ? rec_cap_calls : 1;
   const size_t C = st->nchains;
   KArgs &A = d->args;
@@ -2369,7 +2691,7 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
     rc |= dev_alloc_copy(d, &A.gcbuf, (const double *)nullptr, C * sr_gm_cbuf(st->M));
   }
   if (rc) { srk_destroy(d); return -5; }
-  sr_kfn k = sr_pick_kernel(TB, st->N, d->gm != 0);
+  sr_kfn k = sr_pick_kernel(TB, st->N, d->gm != 0, d->pr != 0);
   if (hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d->lds) != hipSuccess) {
     srk_destroy(d);
     return -5;
@@ -2399,7 +2721,7 @@ extern "C" int srk_run(srk_dev *d, int calls, int spc, int save, int rec_base)
   HIPCHK(hipSetDevice(d->device));
   KArgs A = d->args;
   A.calls = calls; A.spc = spc; A.save = save; A.rec_base = rec_base;
-  sr_kfn k = sr_pick_kernel(d->TB, d->N, d->gm != 0);
+  sr_kfn k = sr_pick_kernel(d->TB, d->N, d->gm != 0, d->pr != 0);
   if (d->have_events) HIPCHK(hipEventRecord(d->ev0, d->stream));
   hipLaunchKernelGGL(k, dim3(d->nchains), dim3(d->TB), d->lds, d->stream, A);
   HIPCHK(hipGetLastError());
@@ -2424,7 +2746,7 @@ extern "C" double srk_last_ms(srk_dev *d)
 }
 
 extern "C" int srk_block_threads(const srk_dev *d) { return d->TB; }
-extern "C" int srk_variant(const srk_dev *d) { return d->gm; }
+extern "C" int srk_variant(const srk_dev *d) { return d->gm ? 1 : (d->pr ? 2 : 0); }
 
 extern "C" int srk_fetch_dbg(srk_dev *d, unsigned long long *out)
 {

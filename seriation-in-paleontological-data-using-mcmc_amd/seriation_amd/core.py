@@ -157,6 +157,11 @@ class Session:
         """Kernel variant: "lds" (occurrence columns in LDS) or "hbm" (columns in HBM)."""
         return "hbm" if L.lib().sr_session_variant(self.h) == 1 else "lds"
 
+    @property
+    def kernel(self):
+        """"pair" (two lanes per taxon) or "single" (one thread per taxon)."""
+        return "pair" if L.lib().sr_session_variant(self.h) == 2 else "single"
+
     def set_stream(self, stream_handle):
         _check(L.lib().sr_session_set_stream(self.h, ctypes.c_void_p(stream_handle)), "set_stream")
 

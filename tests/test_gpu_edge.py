@@ -130,3 +130,25 @@ def test_johnk_beta_branch(columns):
         np.testing.assert_array_equal(ri[k], o["rec_int"], err_msg="seed %d" % s)
         assert np.array_equal(rd[k].view(np.uint64), o["rec_dbl"].view(np.uint64)), s
         assert summ[k]["consistent"] == 0
+
+
+PAIR_CASES = [("synth-like", 256, 512, 12), ("m300", 200, 300, 5), ("n287", 287, 400, 9), ("nh0", 128, 260, 0)]
+
+
+@pytest.mark.parametrize("name,N,M,nh", PAIR_CASES, ids=[c[0] for c in PAIR_CASES])
+def test_pair_kernel_parity(monkeypatch, name, N, M, nh):
+    """The opt-in pair kernel (SR_KERNEL=pair: two lanes per taxon, each walking half of a Gibbs
+    column; proposal terms in slot pairs) is bit-exact too (it is slower: DESIGN.md section 4)."""
+    monkeypatch.setenv("SR_KERNEL", "pair")
+    text = make_text(N, M, nh, seed=N * 1000 + M + 7)
+    ds = sa.Dataset.parse(text, maxs=0)
+    seeds = [4, 19]
+    with sa.Session(ds, seeds) as s:
+        assert s.kernel == "pair" and s.block_threads == 1024
+    summ, (ri, rd) = sa.run_chains(ds, seeds, burnin_calls=3, sample_calls=4, keep_records=True)
+    for k, s in enumerate(seeds):
+        o = oracle_ref.run_chain(text, s, 3, 4, maxs=0)
+        assert o["rc"] == 0
+        np.testing.assert_array_equal(ri[k], o["rec_int"], err_msg="%s seed %d" % (name, s))
+        assert np.array_equal(rd[k].view(np.uint64), o["rec_dbl"].view(np.uint64)), (name, s)
+        assert summ[k]["consistent"] == 0

@@ -29,6 +29,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <type_traits>
 #define SR_TABLES_NO_ARRAYS
 #include "sr_tables.h"
 #include "sr_math.h"
@@ -68,7 +69,12 @@ __host__ __device__ static inline size_t sr_al16(size_t x) { return (x + 15) & ~
  * N <= 287, 17 for N <= 543, else 0 (columns walked in LDS, Gibbs checkpoints in LDS) */
 __host__ __device__ static inline int sr_nwm(int N) { const int nk = (N >> 5) + 1; return nk <= 9 ? 9 : (nk <= 17 ? 17 : 0); }
 /* the register-column kernels exist for TB 256 and 512 (LDS columns only) */
-__host__ __device__ static inline bool sr_regwalk(int N, int TB, bool gm) { return !gm && TB <= 512 && sr_nwm(N) > 0; }
+/* (and their 32-bit hard-site masks: more than 32 hard sites take the LDS-walk kernels, 64-bit masks;
+ * one taxon per thread, M <= TB: the several-taxa branches are compiled out of them) */
+__host__ __device__ static inline bool sr_regwalk(int N, int M, int TB, bool gm, int nh)
+{
+  return !gm && TB <= 512 && M <= TB && sr_nwm(N) > 0 && nh <= 32;
+}
 #define T8STRIDE 514   /* doubles per wave: 256 byte entries {sum, product} + the dead entry {0, 1} */
 /* Gibbs checkpoint slots per word: one per thread that owns a taxon */
 __host__ __device__ static inline int sr_ckstride(int M, int TB) { return M >= TB ? TB : ((M + 63) & ~63); }
@@ -77,7 +83,7 @@ __host__ __device__ static inline int sr_ckstride(int M, int TB) { return M >= T
  * owner-thread access, L2/MALL-resident) and get no LDS slot */
 /* taxa per exact-delta chunk (one wave's taxa): 64, or 32 in the pair kernels (two lanes per taxon) */
 __host__ __device__ static inline int sr_chunk(bool pr) { return pr ? 32 : 64; }
-__host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB, bool gm, bool pr = false)
+__host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB, bool gm, bool pr = false, int nh = 0)
 {
   Lay L;
   size_t o = 0;
@@ -93,7 +99,7 @@ __host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB, bo
   L.rpi0 = o;  o = sr_al16(o + (size_t)N * 4);
   L.rpi1 = o;  o = sr_al16(o + (size_t)N * 4);
   L.ht = o;    o = sr_al16(o + (size_t)NWV * (2 * N + 2) * 2);           /* per wave: hcnt[N+1], nhall[N] (int16) */
-  const size_t rw = (pr || sr_regwalk(N, TB, gm)) ? 1 : 0;   /* register walks (pair kernels too): byte tables instead of LDS checkpoints */
+  const size_t rw = (pr || sr_regwalk(N, M, TB, gm, nh)) ? 1 : 0;   /* register walks (pair kernels too): byte tables instead of LDS checkpoints */
   L.ck = o;    o = sr_al16(o + g * (1 - rw) * ((N >> 5) + 1) * sr_ckstride(M, TB) * sizeof(double));
   L.ccnt = o;  o = sr_al16(o + (size_t)2 * KT * 4);
   L.sab = o;   o = sr_al16(o + g * 2 * M * 4);
@@ -331,7 +337,7 @@ __device__ __forceinline__ uint32_t udiv_word(uint32_t g, const UDiv &u)
 }
 
 /* gsl_rng_uniform_int's quotient g / scale by an invariant-divisor multiply (Hacker's Delight
- * round-up method, exact for every 32-bit g; scale >= 2 here since n <= 2048): scalar ALU only */
+ * round-up method, exact for every 32-bit g; scale >= 2 here since n <= 4095): scalar ALU only */
 struct UDivM { uint32_t n, m; int l; };
 __device__ __forceinline__ UDivM make_udivm(uint32_t n)
 {
@@ -699,33 +705,73 @@ __device__ __forceinline__ double exp2_split(double q)
  * Index k is accepted only if u - F^_{k-1} and F^_k - u both exceed the error bound; then the
  * reference's exact sequential computation provably returns the same k.  Otherwise (or on
  * overflow) the exact path runs.  ck: this lane's checkpoint slots (stride ckstride). */
-__device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int NW, bool rev, int o, int L, double u,
+#ifndef SR_WCH
+#define SR_WCH 8   /* walk words read together: one memory round trip per 8 words (HBM columns: L2 / MALL latency) */
+#endif
+#define SR_QSPAN 600.0   /* window trim below the largest word-start q (log2 units), draw_fast */
+__device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int NW, bool rev, int o, int L, int POo, double u,
                                          const CD &K, const sr_mtab &tb, double vA, double vB, double rA, double rB,
                                          const double *T4, double *ck, int ckstride, uint64_t *fbk, int &dt0, int &df0,
                                          int &dt1, int &df1 GSTAMP_ARGS)
 {
-  const int POo = walk_prefix(Pm, M, N, NW, rev, o);
+  /* POo: ones among walk entries [0, o), from the caller's column prefix table */
   const int nk = (L >> 5) + 1;
-  /* pass 0: window of words that can hold mass above 2^-40 relative to entry o */
-  int klo = nk, khi = -1;
-  double qlo = 0.0;
+  /* pass 0: window of words that can hold mass above 2^-40 relative to entry o; the ones before
+     its first word are kept for the pick's count (no prefix walk afterwards).  Long walks (N up to
+     4095) can span q ranges far beyond the f64 exponent range: the chain is scaled by the largest
+     word-start q of the window (qmx), and window words whose start q lies more than SR_QSPAN below it
+     are dropped from the ends (their entries hold < 2^-(SR_QSPAN-75) of the mass each; ABS covers it);
+     ck[k] keeps O(32k) of every word for that trim. */
+  int klo = nk, khi = -1, Oklo = 0;
+  double qlo = 0.0, qmx = -__builtin_inf(), qmn = __builtin_inf();
   {
     int O = 0;   /* ones among walk entries [0, 32k) */
-        for (int k = 0; k < nk; ++k) {
-      const uint32_t ww = walk_word(Pm, M, N, NW, rev, k);
-      const int nb = min(32, L + 1 - 32 * k);
-      const uint32_t vm = (nb >= 32) ? 0xffffffffu : ((1u << nb) - 1u);
-      const int w0 = 32 * k;
-      /* q at entry w0 from exact counts */
-      const double qs = (w0 <= o) ? ((double)((o - w0) - (POo - O)) * vA + (double)(POo - O) * vB)
-                                  : -((double)((w0 - o) - (O - POo)) * vA + (double)(O - POo) * vB);
-      const int ones = __popc(ww & vm);
-      const double ub = qs - (double)(nb - ones) * vA;   /* every zero raises q by -vA */
-      if (ub > -SR_WIN_T) {
-        if (k < klo) { klo = k; qlo = qs; }
-        khi = k;
+    for (int k0 = 0; k0 < nk; k0 += SR_WCH) {
+      uint32_t wv[SR_WCH];
+#pragma unroll
+      for (int t = 0; t < SR_WCH; ++t) wv[t] = (k0 + t < nk) ? walk_word(Pm, M, N, NW, rev, k0 + t) : 0u;
+#pragma unroll
+      for (int t = 0; t < SR_WCH; ++t) {
+        const int k = k0 + t;
+        if (k < nk) {
+          const uint32_t ww = wv[t];
+          const int nb = min(32, L + 1 - 32 * k);
+          const uint32_t vm = (nb >= 32) ? 0xffffffffu : ((1u << nb) - 1u);
+          const int w0 = 32 * k;
+          /* q at entry w0 from exact counts */
+          const double qs = (w0 <= o) ? ((double)((o - w0) - (POo - O)) * vA + (double)(POo - O) * vB)
+                                      : -((double)((w0 - o) - (O - POo)) * vA + (double)(O - POo) * vB);
+          const int ones = __popc(ww & vm);
+          const double ub = qs - (double)(nb - ones) * vA;   /* every zero raises q by -vA */
+          if (ub > -SR_WIN_T) {
+            if (k < klo) { klo = k; qlo = qs; Oklo = O; }
+            khi = k;
+            qmx = fmax(qmx, qs);
+            qmn = fmin(qmn, qs);
+          }
+          ck[k * ckstride] = __builtin_bit_cast(double, (uint64_t)(uint32_t)O);
+          O += __popc(ww);
+        }
       }
-      O += __popc(ww);
+    }
+  }
+  if (klo <= khi && qmx - qmn > SR_QSPAN) {   /* trim the window's ends to start q >= qmx - SR_QSPAN */
+    const int k1 = klo, k2 = khi;
+    klo = nk; khi = -1;
+    for (int k0 = k1; k0 <= k2; k0 += SR_WCH) {
+      int Ov[SR_WCH];
+#pragma unroll
+      for (int t = 0; t < SR_WCH; ++t) Ov[t] = (k0 + t <= k2) ? (int)__builtin_bit_cast(uint64_t, ck[(k0 + t) * ckstride]) : 0;
+#pragma unroll
+      for (int t = 0; t < SR_WCH; ++t) {
+        const int k = k0 + t, O = Ov[t], w0 = 32 * k;
+        const double qs = (w0 <= o) ? ((double)((o - w0) - (POo - O)) * vA + (double)(POo - O) * vB)
+                                    : -((double)((w0 - o) - (O - POo)) * vA + (double)(O - POo) * vB);
+        if (k <= k2 && qs >= qmx - SR_QSPAN) {
+          if (k < klo) { klo = k; qlo = qs; Oklo = O; }
+          khi = k;
+        }
+      }
     }
   }
   GSTAMP(1);
@@ -740,41 +786,69 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
     atomicAdd((unsigned long long *)fbk + 29, 1ull);
   }
 #endif
-  /* pass 1: S over the window, checkpoints */
-  const double y0 = exp2_split(qlo);
+  /* pass 1: S over the window, checkpoints; the chain scaled by 2^-qmx.  A chain that falls below
+     2^-700 at a word start inside the window (q dipping far below qmx and possibly rising again)
+     would lose precision: that draw takes the exact path (uf). */
+  const double y0 = exp2_split(qlo - (klo <= khi ? qmx : 0.0));
   double S = 0.0;
+  bool uf = false;
   {
     double y = y0;
-        for (int k = klo; k <= khi; ++k) {
-      const uint32_t ww = walk_word(Pm, M, N, NW, rev, k);
-      const int nb = min(32, L + 1 - 32 * k);
-      /* 4 entries per step: T4[c][nibble] = sum of the first c prefix products of the nibble's
-         ratios (c = valid entries of the group, 0..4), T4[5][nibble] = product of all four */
+    for (int k0 = klo; k0 <= khi; k0 += SR_WCH) {
+      uint32_t wv[SR_WCH];
 #pragma unroll
-      for (int g = 0; g < 8; ++g) {
-        const uint32_t nib = (ww >> (4 * g)) & 15u;
-        const int c = min(max(nb - 4 * g, 0), 4);
-        const double2 t = t4sp(T4, c, nib);
-        S = __builtin_fma(y, t.x, S);
-        y = y * t.y;
+      for (int t = 0; t < SR_WCH; ++t) wv[t] = (k0 + t <= khi) ? walk_word(Pm, M, N, NW, rev, k0 + t) : 0u;
+#pragma unroll
+      for (int t = 0; t < SR_WCH; ++t) {
+        const int k = k0 + t;
+        if (k <= khi) {
+          const uint32_t ww = wv[t];
+          const int nb = min(32, L + 1 - 32 * k);
+          uf |= y < 0x1p-700;
+          /* 4 entries per step: T4[c][nibble] = sum of the first c prefix products of the nibble's
+             ratios (c = valid entries of the group, 0..4), T4[5][nibble] = product of all four */
+#pragma unroll
+          for (int g = 0; g < 8; ++g) {
+            const uint32_t nib = (ww >> (4 * g)) & 15u;
+            const int c = min(max(nb - 4 * g, 0), 4);
+            const double2 t4 = t4sp(T4, c, nib);
+            S = __builtin_fma(y, t4.x, S);
+            y = y * t4.y;
+          }
+          ck[k * ckstride] = S;
+        }
       }
-      ck[k * ckstride] = S;
     }
   }
   GSTAMP(2);
   /* pass 2: locate the word, replay the chain to it, certify inside it */
-  int res = -1;
-  if (S > 0.0 && S < 0x1p1000) {
+  int res = -1, POp = 0;
+  if (S > 0.0 && S < 0x1p1000 && !uf) {
     const double inv = 1.0 / S;
     const double REL = (double)(N + 1) * 0x1p-50;
     const double ABS = (double)(N + 1) * 0x1p-39;
     int j = klo;   /* first window word whose checkpoint reaches u (checkpoints ascend) */
-        for (int k = klo; k < khi; ++k) j += (ck[k * ckstride] * inv < u) ? 1 : 0;
-    double y = y0;
-        for (int k = klo; k < j; ++k) {   /* words before j are full (only the walk's last word is partial) */
-      const uint32_t ww = walk_word(Pm, M, N, NW, rev, k);
+    for (int k0 = klo; k0 < khi; k0 += SR_WCH) {
+      double cv[SR_WCH];
 #pragma unroll
-      for (int g = 0; g < 8; ++g) y = y * t4p(T4, (ww >> (4 * g)) & 15u);
+      for (int t = 0; t < SR_WCH; ++t) cv[t] = (k0 + t < khi) ? ck[(k0 + t) * ckstride] : 0.0;
+#pragma unroll
+      for (int t = 0; t < SR_WCH; ++t) j += (k0 + t < khi && cv[t] * inv < u) ? 1 : 0;
+    }
+    double y = y0;
+    int Oj = Oklo;   /* ones among walk entries [0, 32 j) */
+    for (int k0 = klo; k0 < j; k0 += SR_WCH) {   /* words before j are full (only the walk's last word is partial) */
+      uint32_t wv[SR_WCH];
+#pragma unroll
+      for (int t = 0; t < SR_WCH; ++t) wv[t] = (k0 + t < j) ? walk_word(Pm, M, N, NW, rev, k0 + t) : 0u;
+#pragma unroll
+      for (int t = 0; t < SR_WCH; ++t) {
+        if (k0 + t < j) {
+#pragma unroll
+          for (int g = 0; g < 8; ++g) y = y * t4p(T4, (wv[t] >> (4 * g)) & 15u);
+          Oj += __popc(wv[t]);
+        }
+      }
     }
     const double Sp0 = (j == klo) ? 0.0 : ck[(j - 1) * ckstride];
     const int w0 = 32 * j;
@@ -821,12 +895,15 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
     const bool prev_ok = (w == 0) || (tprev > eprev);
     const bool here_ok = (w == L) || (t < -e);
 #ifndef SR_FORCE_EXACT
-    if (prev_ok && here_ok) res = w;
+    if (prev_ok && here_ok) {
+      res = w;
+      POp = Oj + __popc(ww & ((1u << (w & 31)) - 1u));
+    }
 #else   /* test build: every Gibbs draw takes the exact three-pass walk */
-    (void)prev_ok; (void)here_ok; (void)w;
+    (void)prev_ok; (void)here_ok; (void)w; (void)Oj;
 #endif
 #ifdef SR_STAMPS
-    else atomicAdd((unsigned long long *)fbk + (prev_ok ? 2 : 1), 1ull);
+    if (!(prev_ok && here_ok)) atomicAdd((unsigned long long *)fbk + (prev_ok ? 2 : 1), 1ull);
 #endif
   }
   if (res < 0) {
@@ -835,10 +912,10 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
     if (!(S > 0.0)) atomicAdd((unsigned long long *)fbk + 3, 1ull);
 #endif
     res = draw_exact(Pm, M, N, rev, o, L, u, K, tb);
+    POp = walk_prefix(Pm, M, N, NW, rev, res);
   }
   GSTAMP(3);
   /* count deltas at the pick (the dt arrays of mcmc_auxa) */
-  const int POp = walk_prefix(Pm, M, N, NW, rev, res);
   if (res == o) { dt0 = df0 = dt1 = df1 = 0; }
   else if (res < o) { int O = POo - POp; int Z = (o - res) - O; dt0 = -Z; df0 = Z; dt1 = O; df1 = -O; }
   else { int O = POp - POo; int Z = (res - o) - O; dt0 = Z; df0 = -Z; dt1 = -O; df1 = O; }
@@ -886,6 +963,7 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
      (the window only bounds the skipped mass: the pick is certified independently of it). */
   int klo = NWM, khi = -1;
   double qlo = 0.0;
+  [[maybe_unused]] uint32_t lowm = 0u;   /* 17-word walks: words whose start q lies below -700 (pass 2) */
   const int kl = L >> 5, nbl = (L & 31) + 1;   /* the walk's last word and its entries */
   uint32_t wl = 0u;                              /* word kl */
   {
@@ -908,6 +986,7 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
       const int ones = __popc(wk[k] & vm);
       const double ub = qs - (double)(nb - ones) * vA;
       const bool in = (k < nk) && ub > -SR_WIN_T;
+      if constexpr (NWM > 9) lowm |= (qs < -700.0 ? 1u : 0u) << k;
       const bool first = in && klo == NWM;
       qlo = first ? qs : qlo;
       klo = first ? k : klo;
@@ -989,7 +1068,18 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
   /* pass 2: locate the word, then the byte, nibble and entry where u falls (the searches compare
      against u S; the pick is certified below, independently of how it was found) */
   int res = -1, POp = 0;   /* the pick and the ones among walk entries [0, pick) */
-  if (S > 0.0 && S < 0x1p1000) {
+  /* Underflow: y at a window word start is 2^q up to rounding, and a chain that sank into the
+     subnormal range would lose its relative precision.  Only zeros raise q (by |vA| each) and the
+     window's last word reaches q > -40, so every window word start lies above -40 - 32 nk |vA|;
+     d >= 0.2 and c <= 0.1 always (mcmc_samplebeta's bounds MIND / MAXC, mcmc.h:27-30; the initial
+     values log .01 / log .3, mcmc.c:419-420) give |vA| = log2((1 - c) / d) <= log2 5 = 2.33.  Walks of
+     <= 9 words therefore stay above 2^-710 and next words' y above 2^-1018 (a word's product is
+     >= 2^-32 vB >= 2^-309): no test.  17-word walks can sink further: a window word start below
+     2^-700 sends the draw to the exact path (pass 0's exact q, a bit mask; a per-draw test costs
+     2 % of the 9-word kernel, profiles/r03n_ab_yguard.json). */
+  bool yok = true;
+  if constexpr (NWM > 9) yok = klo > khi || (lowm & ((2u << khi) - 1u) & ~((1u << klo) - 1u)) == 0u;
+  if (S > 0.0 && S < 0x1p1000 && yok) {
     const double inv = 1.0 / S;
     const double REL = (double)(N + 33) * 0x1p-50;   /* + the byte tables' own rounding (<= 16 ulp per entry) */
     const double ABS = (double)(N + 1) * 0x1p-39;
@@ -1194,7 +1284,11 @@ __device__ __forceinline__ int draw_pair9(const uint32_t (&wk)[5], int h, const 
   }
   /* ---- pass 2 (both lanes, identical data): word, byte, nibble, entry; certification */
   int res = -1, POp = 0;
-  if (St > 0.0 && St < 0x1p1000) {
+  bool uf = false;   /* as draw_fast_s: a window word start below 2^-700 takes the exact path */
+#pragma unroll
+  for (int i = 0; i < NH; ++i) uf |= k0 + i >= klo && k0 + i <= khi && yst[i] < 0x1p-700;
+  uf = uf || pair_swap_i32(uf ? 1 : 0) != 0;
+  if (St > 0.0 && St < 0x1p1000 && !uf) {
     const double inv = 1.0 / St;
     const double REL = (double)(N + 41) * 0x1p-50;
     const double ABS = (double)(N + 1) * 0x1p-39;
@@ -1461,7 +1555,7 @@ __device__ __forceinline__ void build_hard_tables(const int *hp, int nh, int N, 
                                                   int16_t *nhall, int lane)
 {
   /* hard bitmap (hbw: this wave's NW words, NW <= 64), then ranks by ballot over positions */
-  if (lane < NW) hbw[lane] = 0u;
+  for (int w = lane; w < NW; w += 64) hbw[w] = 0u;
   wsync();
   if (lane < nh) { const int h = hp[lane]; atomicOr(&hbw[h >> 5], 1u << (h & 31)); }
   wsync();
@@ -1483,26 +1577,29 @@ __device__ __forceinline__ void build_hard_tables(const int *hp, int nh, int N, 
  * (mcmc.c:1175-1256 pi1, 1367-1436 pi2, 1568-1631 pi3).  hcnt/nhall: the wave's hard-site tables. */
 /* column bits at the hard positions, bit k = hard site k (input of the pi3 count change) */
 /* hl: lane k holds hard position k (loaded by the caller with every lane active) */
-__device__ __forceinline__ uint32_t hard_bits_col(const uint32_t *Pm, int M, int hl, int nh)
+/* HM: uint32_t (register-walk kernels, <= 32 hard sites) or uint64_t (LDS-walk kernels, <= SR_NHMAX = 64) */
+template <typename HM = uint64_t>
+__device__ __forceinline__ HM hard_bits_col(const uint32_t *Pm, int M, int hl, int nh)
 {
-  uint32_t hbm = 0;
+  HM hbm = 0;
   if (nh > 0) {
 #pragma unroll
     for (int k = 0; k < 16; ++k) {   /* independent loads, one round trip */
       const int h = __builtin_amdgcn_readlane(hl, min(k, nh - 1));
-      const uint32_t bit = (Pm[(h >> 5) * M] >> (h & 31)) & 1u;
-      hbm |= (k < nh ? bit : 0u) << k;
+      const HM bit = (Pm[(h >> 5) * M] >> (h & 31)) & 1u;
+      hbm |= (k < nh ? bit : (HM)0) << k;
     }
     for (int k = 16; k < nh; ++k) {
       const int h = __builtin_amdgcn_readlane(hl, k);
-      hbm |= ((Pm[(h >> 5) * M] >> (h & 31)) & 1u) << k;
+      hbm |= (HM)((Pm[(h >> 5) * M] >> (h & 31)) & 1u) << k;
     }
   }
   return hbm;
 }
 
+template <typename HM>
 __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, const uint32_t *Pm, const uint16_t *prem,
-                                         int M, uint32_t hbm, const int16_t *hcnt, const int16_t *nhall, int &dt0, int &dt1)
+                                         int M, HM hbm, const int16_t *hcnt, const int16_t *nhall, int &dt0, int &dt1)
 {
   const int i = q.i, j = q.j;
   dt0 = 0; dt1 = 0;
@@ -1548,8 +1645,9 @@ __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, 
       if (hi < lo) { cnt = 0; return 0; }
       const int kl = hcnt[lo], kh = hcnt[hi + 1];
       cnt = kh - kl;
-      const uint32_t km = ((kh >= 32) ? 0xffffffffu : ((1u << kh) - 1u)) & ~((kl >= 32) ? 0xffffffffu : ((1u << kl) - 1u));
-      return __popc(hbm & km);
+      constexpr int HB = 8 * (int)sizeof(HM);
+      const HM km = ((kh >= HB) ? ~(HM)0 : (((HM)1 << kh) - (HM)1)) & ~((kl >= HB) ? ~(HM)0 : (((HM)1 << kl) - (HM)1));
+      return (int)__popcll((uint64_t)(hbm & km));
     };
     const int wlo = max(a, i), whi = min(b - 1, j);
     const int sizeW = max(0, whi - wlo + 1);
@@ -1591,7 +1689,7 @@ __device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const i
     const int ch = m0 / CH, m = m0 + (PR ? (lane >> 1) : lane);
     int dt0 = 0, dt1 = 0;
     if (m < M && ev)
-      taxon_dt(kind, q, sab[m], sab[M + m], P + m, pre + m, M, kind == PK_PI3 ? hard_bits_col(P + m, M, hl, nh) : 0u,
+      taxon_dt(kind, q, sab[m], sab[M + m], P + m, pre + m, M, kind == PK_PI3 ? hard_bits_col<uint64_t>(P + m, M, hl, nh) : 0ull,
                hcnt, nhall, dt0, dt1);
     const double tv = (m < M && ev) ? qval(dt0, -dt0, dt1, -dt1, K) : 0.0;
     const uint64_t msk = __ballot(tv != 0.0);
@@ -1630,7 +1728,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   const int chain = blockIdx.x;
   const int N = A.N, M = A.M, NW = A.NW, nh = A.nh;
   const int KTC = (M + sr_chunk(PR) - 1) / sr_chunk(PR);   /* exact-delta chunks */
-  const Lay L = sr_layout(N, M, NW, TB, GM, PR);
+  const Lay L = sr_layout(N, M, NW, TB, GM, PR, nh);
   double *tabs = (double *)(smem + L.tab);
   /* GM: the per-taxon arrays are the chain's HBM state itself (P, a/b, counts: updated in
      place) or its HBM scratch; otherwise LDS copies loaded here and stored at the end */
@@ -1702,7 +1800,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
      kernels).  Invariant for the whole run: every move that would change the hard sites' relative
      order is vetoed (mcmc.c:1153-1160, 1343-1348; pi3 moves non-hard sites only), so position hp[k]
      always holds the same site and its bits travel with it. */
-  uint32_t hbc = 0;
+  using HM = typename std::conditional<(NWM > 0), uint32_t, uint64_t>::type;   /* hard-site mask type */
+  HM hbc = 0;
   int par = 0;      /* parity of the double-buffered totals */
   int bpar = 0;     /* parity of the double-buffered proposal count sums */
   int xpar = 0;     /* parity of the double-buffered exact-delta term lists */
@@ -1712,7 +1811,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   for (int m = tid; m < M; m += TB) col_pre_build(pre + m, P + m, M, NW);   /* own columns */
   {
     const int hl0 = (lane < nh) ? hp[lane] : 0;   /* loaded with every lane active */
-    if (M <= TXS && tx < M) hbc = hard_bits_col(P + tx, M, hl0, nh);
+    if (M <= TXS && tx < M) hbc = hard_bits_col<HM>(P + tx, M, hl0, nh);
   }
   const double ec = sr_exp_m(SR_LOGEPSILON, &tb);
   const uint32_t nhard = (uint32_t)nh;
@@ -1861,15 +1960,20 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               t0 += d0; f0 += e0; t1 += d1; f1 += e1;
               if (rev) nb = N - res; else na = res;
             }
-          } else
+          } else {
+          const uint16_t *prem = pre + m;   /* ones before each trip's start entry, as above */
+          const int POa = col_pre(prem, Pm, M, a0);
+          const int POb = (int)prem[NW * M] - col_pre(prem, Pm, M, b0);
           for (int pass = 0; pass < 2; ++pass) {
             int d0, e0, d1, e1;
             const bool rev = pass != 0;
-            const int res = draw_fast(Pm, M, N, NW, rev, rev ? N - b0 : a0, rev ? N - na : b0, rev ? ub : ua, K, tb,
-                                      vA, vB, rA, rB, T4w, ckb + tid, CKS, &misc[MS_FBK], d0, e0, d1, e1 GSTAMP_PASS);
+            const int res = draw_fast(Pm, M, N, NW, rev, rev ? N - b0 : a0, rev ? N - na : b0, rev ? POb : POa,
+                                      rev ? ub : ua, K, tb, vA, vB, rA, rB, T4w, ckb + tid, CKS, &misc[MS_FBK], d0, e0,
+                                      d1, e1 GSTAMP_PASS);
             GSTAMP_K4();
             t0 += d0; f0 += e0; t1 += d1; f1 += e1;
             if (rev) nb = N - res; else na = res;
+          }
           }
           if (!PR || hf == 0) {   /* PR: the even lane writes the pair's results */
             nchg += (na != a0) + (nb != b0);
@@ -1886,7 +1990,24 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       }
       FST(1);
       STAMP(1);
-      if (want_logl) {   /* mcmc_logl (mcmc.c:639-645), sequential over m, lane 0 of every wave */
+      if (GM && want_logl) {   /* mcmc_logl with the terms in HBM: each wave reads them 64 at a time
+                                  (coalesced, 4 chunks in flight) and adds them in m order through readlane */
+        __syncthreads();
+        double s = 0.0;
+        for (int c0 = 0; c0 < M; c0 += 256) {
+          double v[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) { const int m = c0 + 64 * q + lane; v[q] = (m < M) ? lbuf[m] : 0.0; }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int n = min(64, M - (c0 + 64 * q));
+#pragma unroll 16
+            for (int l = 0; l < 64; ++l)
+              if (l < n) s = s + readlane_f64(v[q], l);
+          }
+        }
+        loglik = s;
+      } else if (want_logl) {   /* mcmc_logl (mcmc.c:639-645), sequential over m, lane 0 of every wave */
         __syncthreads();
         if (PR ? tid == 0 : lane == 0) {
           double s = 0.0;
@@ -1918,7 +2039,9 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
          one that is accepted (or needs the exact delta) ends the batch: it is applied with the
          cursor it really consumed, and the proposals after it are re-batched. */
       {
-        int vi = 0, vj = 0, vfl = 4, vkn = 0, vuw = 1, vnd = 0, voff = 0, vr0 = 0;   /* lane p: proposal p */
+        /* lane p: proposal p -- vpk = i | j << 12 | inc1 << 24 | inc2 << 25 | veto << 26 (one readlane per
+           proposal where its fields are read), vkr = Kn | r0 << 16 (pi3) */
+        int vpk = 1 << 26, vkr = 0, vuw = 1, vnd = 0, voff = 0;
         int p0 = 0;
         /* the lane-parallel proposal tables (ptab) hold "a proposal of each kind starting at word o"
            for the 128 words from stream position (tblk, toff); a later batch of the sweep reuses them
@@ -2009,19 +2132,17 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               uint32_t uw = 0;
               if (!veto) { do { uw = word(); } while (!bad && uw == 0u); }   /* gsl_rng_uniform_pos */
               if (bad) return false;
-              vi = (lane == p) ? (i) : vi;
-              vj = (lane == p) ? (j) : vj;
-              vfl = (lane == p) ? (inc1 | (inc2 << 1) | (veto ? 4 : 0)) : vfl;
-              vkn = (lane == p) ? (Kn) : vkn;
+              vpk = (lane == p) ? (i | (j << 12) | (inc1 << 24) | (inc2 << 25) | (veto ? 1 << 26 : 0)) : vpk;
+              vkr = (lane == p) ? (Kn | (r0 << 16)) : vkr;
               vuw = (lane == p) ? ((int)uw) : vuw;
               vnd = (lane == p) ? (nd) : vnd;
               voff = (lane == p) ? (off) : voff;
-              vr0 = (lane == p) ? (r0) : vr0;
               pend = p + 1;
               return true;
           };
           /* the swap (accepted ~44 %) is drawn first and forms its own batch */
           if (p0 == 0) (void)scalar_one(0);
+          /* (the swap in one batch with proposals 1..15 measured no faster: profiles/r03e_ab_phasec.json) */
           if (p0 > 0) {
             /* Lane-parallel draws: lane l evaluates "a pi1 / pi2 / pi3 proposal starting at word
                offset o" for o = l and o = l + 64 (words o..o+4) into ptab; the scan below then walks
@@ -2054,7 +2175,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                   const int ic = min(i, N - 1), jc = min(j, N - 1);
                   const bool veto = (hcnt[ic + 1] != hcnt[ic]) && (hcnt[max(ic, jc) + 1] - hcnt[min(ic, jc)] > 1);
                   const bool ok = okN && (veto || w[2] != 0u);
-                  ptab[o] = (uint32_t)ic | ((uint32_t)jc << 11) | (veto ? 1u << 22 : 0u) | (ok ? 1u << 23 : 0u);
+                  ptab[o] = (uint32_t)ic | ((uint32_t)jc << 12) | (veto ? 1u << 24 : 0u) | (ok ? 1u << 25 : 0u);
                 }
                 /* pi2 (mcmc.c:1317-1364): words o, o+1, [o+2, o+3 inc], uniform_pos at o+4 */
                 {
@@ -2063,8 +2184,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                   const int ic = min(i, N - 1), jc = min(j, N - 1);
                   const bool veto = hcnt[jc + 1] - hcnt[ic] > 1;
                   const bool ok = okN && (veto || (okab && w[4] != 0u));
-                  ptab[128 + o] = (uint32_t)ic | ((uint32_t)jc << 11) | (veto ? 1u << 22 : 0u) | (ok ? 1u << 23 : 0u) |
-                                  (qa << 24) | (qb << 25);
+                  ptab[128 + o] = (uint32_t)ic | ((uint32_t)jc << 12) | (veto ? 1u << 24 : 0u) | (ok ? 1u << 25 : 0u) |
+                                  (qa << 26) | (qb << 27);
                 }
                 /* pi3 (mcmc.c:1495-1565): words o..o+3, uniform_pos at o+4 */
                 {
@@ -2075,7 +2196,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                   ri = min(ri, max(NH - 1, 0)); rj = min(rj, max(NH - 1, 0));
                   const int i = nhall[ri], j = nhall[rj];
                   const bool ok = in && NH >= 2 && qH < mdH.n && qH1 < mdH1.n && okab && w[4] != 0u;
-                  ptab[256 + o] = (uint32_t)i | ((uint32_t)j << 11) | (ok ? 1u << 23 : 0u) | (qa << 24) | (qb << 25);
+                  ptab[256 + o] = (uint32_t)i | ((uint32_t)j << 12) | (ok ? 1u << 25 : 0u) | (qa << 26) | (qb << 27);
                   ptab[384 + o] = (uint32_t)ri | ((uint32_t)(rj - ri + 1) << 16);
                 }
               }
@@ -2093,8 +2214,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               const int t = delta + lane + 64 * h;   /* table index of batch offset lane + 64 h */
               const int tc = min(t, 127);
               const uint32_t a1 = ptab[tc], a2 = ptab[128 + tc], a3 = ptab[256 + tc];
-              const uint32_t e = ((a1 >> 23) & 1u) | ((((a1 >> 22) & 1u) ^ 1u) << 1) | (((a2 >> 23) & 1u) << 2) |
-                                 (((a2 >> 22) & 1u) << 3) | (((a3 >> 23) & 1u) << 4);
+              const uint32_t e = ((a1 >> 25) & 1u) | ((((a1 >> 24) & 1u) ^ 1u) << 1) | (((a2 >> 25) & 1u) << 2) |
+                                 (((a2 >> 24) & 1u) << 3) | (((a3 >> 25) & 1u) << 4);
               lent |= (t < 128 ? e : 0u) << (16 * h);   /* past the tables: not ok (scalar path) */
             }
             const int sstart = pend;
@@ -2123,14 +2244,11 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               uint32_t iu = base + (uint32_t)min(o + (kind == PK_PI1 ? 2 : 4), avail - 1);   /* the uniform_pos word */
               iu = (iu >= SR_RING * SR_MT_N) ? iu - SR_RING * SR_MT_N : iu;
               const uint32_t ru = sr_mt_temper(ring[iu]);
-              const bool veto = (ra >> 22) & 1u;
+              const bool veto = (ra >> 24) & 1u;
               const int nd = o + (kind == PK_PI1 ? 2 : (kind == PK_PI2 ? (veto ? 2 : 4) : 4));
               if (lane >= sstart && lane < pend) {
-                vi = (int)(ra & 2047u);
-                vj = (int)((ra >> 11) & 2047u);
-                vfl = (int)((ra >> 24) & 3u) | (veto ? 4 : 0);
-                vkn = (int)(rb >> 16);
-                vr0 = (int)(rb & 0xffffu);
+                vpk = (int)((ra & 0xffffffu) | (((ra >> 26) & 3u) << 24) | (veto ? 1u << 26 : 0u));
+                vkr = (int)((rb >> 16) | ((rb & 0xffffu) << 16));
                 vuw = (int)ru;
                 vnd = nd;
                 voff = nd + (veto ? 0 : 1);
@@ -2150,25 +2268,27 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             tvalid = false;
             continue;
           }
-          auto load_prop = [&](int p) -> Prop {
+          auto load_prop = [&](int p) -> Prop {   /* fields unpacked by scalar ALU */
             Prop q;
-            q.i = __builtin_amdgcn_readlane(vi, p);
-            q.j = __builtin_amdgcn_readlane(vj, p);
+            const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane(vpk, p);
+            q.i = (int)(pk & 4095u);
+            q.j = (int)((pk >> 12) & 4095u);
             q.ii = min(q.i, q.j); q.jj = max(q.i, q.j);
-            const int fl = __builtin_amdgcn_readlane(vfl, p);
-            q.inc1 = fl & 1; q.inc2 = (fl >> 1) & 1;
-            q.Kn = __builtin_amdgcn_readlane(vkn, p);
-            q.r0 = __builtin_amdgcn_readlane(vr0, p);
+            q.inc1 = (int)((pk >> 24) & 1u); q.inc2 = (int)((pk >> 25) & 1u);
+            const uint32_t kr = (uint32_t)__builtin_amdgcn_readlane(vkr, p);
+            q.Kn = (int)(kr & 0xffffu);
+            q.r0 = (int)(kr >> 16);
             return q;
           };
+          auto vetoed = [&](int p) -> bool { return ((uint32_t)__builtin_amdgcn_readlane(vpk, p) >> 26) & 1u; };
 
           /* ---- exact integer count sums of every drawn proposal over own taxa, per wave */
           int *pw = part + (bpar * 16) * NWV * 8;
           const bool pack = N < 512;   /* one taxon per thread: per-wave sums fit 16-bit fields */
           /* own taxon's limits and hard-site bits, fixed for the batch (one taxon per thread) */
-          const bool one = M <= TXS;
+          const bool one = NWM > 0 || M <= TXS;   /* register-walk kernels: M <= TB (sr_regwalk) */
           int a1 = 0, b1 = 0;
-          const uint32_t hb1 = hbc;
+          const HM hb1 = hbc;
           if (one && tx < M) { a1 = sab[tx]; b1 = sab[M + tx]; }
           FST(13);
 #if defined(SR_STAMP_DRAWS)
@@ -2189,8 +2309,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             for (int sp = 0; sp < 9; ++sp) {   /* terms and their sums per slot pair (no per-slot arrays:
                                                   the register budget is 128 at four waves per SIMD) */
               const int pa = SPA[sp], pb = SPB[sp];
-              const bool va = pa >= p0 && pa < pend && !(__builtin_amdgcn_readlane(vfl, pa) & 4);
-              const bool vb = pb >= 0 && pb >= p0 && pb < pend && !(__builtin_amdgcn_readlane(vfl, pb >= 0 ? pb : 0) & 4);
+              const bool va = pa >= p0 && pa < pend && !vetoed(pa);
+              const bool vb = pb >= 0 && pb >= p0 && pb < pend && !vetoed(pb >= 0 ? pb : 0);
               if (va || vb) {
                 const Prop qa = load_prop(pa), qb = load_prop(pb >= 0 ? pb : pa);
                 Prop q;
@@ -2231,8 +2351,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 #pragma unroll
             for (int sI = 0; sI < 16; ++sI) {
               d0s[sI] = 0; d1s[sI] = 0;
-              const int fl = __builtin_amdgcn_readlane(vfl, sI);
-              if (sI >= p0 && sI < pend && !(fl & 4)) {
+              if (sI >= p0 && sI < pend && !vetoed(sI)) {
                 const Prop q = load_prop(sI);
                 int dt0 = 0, dt1 = 0;
                 if (tid < M) taxon_dt(prop_kind(sI), q, a1, b1, P + tid, pre + tid, M, hb1, hcnt, nhall, dt0, dt1);
@@ -2242,18 +2361,25 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             FST(3);
 #pragma unroll
             for (int sI = 0; sI < 16; ++sI) {
-              const int fl = __builtin_amdgcn_readlane(vfl, sI);
-              if (sI >= p0 && sI < pend && !(fl & 4)) {
+              if (sI >= p0 && sI < pend && !vetoed(sI)) {
                 int X0, X1, Y0, Y1;
                 if (prop_kind(sI) == PK_PI1) {   /* pi1: dt in {-1, 0, 1} and dt0 dt1 = 0: every sum is a ballot count */
                   const int cp0 = (int)__popcll(__ballot(d0s[sI] > 0)), cn0 = (int)__popcll(__ballot(d0s[sI] < 0));
                   const int cp1 = (int)__popcll(__ballot(d1s[sI] > 0)), cn1 = (int)__popcll(__ballot(d1s[sI] < 0));
                   X0 = cp0 - cn0; X1 = cp1 - cn1; Y0 = cp0 + cn0; Y1 = cp1 + cn1;
-                } else if (pack) {   /* per-wave sums of (dt + N) and |dt| fit 16-bit fields (N < 512) */
+                } else if (pack) {   /* per-wave sums of (dt + N) fit 16-bit fields (N < 512) */
                   const uint32_t u1 = (uint32_t)wave_sum_i32((int)((uint32_t)(d0s[sI] + N) | ((uint32_t)(d1s[sI] + N) << 16)));
-                  const uint32_t u2 = (uint32_t)wave_sum_i32((int)((uint32_t)abs(d0s[sI]) | ((uint32_t)abs(d1s[sI]) << 16)));
                   X0 = (int)(u1 & 0xffffu) - 64 * N; X1 = (int)(u1 >> 16) - 64 * N;
+#ifdef SR_EXACT_Y
+                  const uint32_t u2 = (uint32_t)wave_sum_i32((int)((uint32_t)abs(d0s[sI]) | ((uint32_t)abs(d1s[sI]) << 16)));
                   Y0 = (int)(u2 & 0xffffu); Y1 = (int)(u2 >> 16);
+#else
+                  /* the error bound needs only upper bounds of sum |dt0| and sum |dt1|: a reversal of
+                     [ii, jj] changes a taxon's alive cells inside it only, |dt0| + |dt1| <= 2 (jj - ii + 1),
+                     times the taxa with a nonzero change (one ballot instead of a second reduction) */
+                  const Prop qb = load_prop(sI);
+                  Y0 = Y1 = (int)__popcll(__ballot((d0s[sI] | d1s[sI]) != 0)) * 2 * (qb.jj - qb.ii + 1);
+#endif
                 } else {
                   X0 = wave_sum_i32(d0s[sI]); X1 = wave_sum_i32(d1s[sI]);
                   Y0 = wave_sum_i32(abs(d0s[sI])); Y1 = wave_sum_i32(abs(d1s[sI]));
@@ -2265,26 +2391,45 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               }
             }
             STAMP_K(PK_PI3);
-          } else
-          for (int p = p0; p < pend; ++p) {   /* several taxa per thread */
-            if (__builtin_amdgcn_readlane(vfl, p) & 4) continue;
-            const int kind = prop_kind(p);
-            const Prop q = load_prop(p);
-            int x0 = 0, x1 = 0, y0 = 0, y1 = 0;
+          } else {
+            /* several taxa per thread (M > TB; the HBM-column kernels): per taxon, every proposal slot
+               unrolled (compile-time kinds) so that the taxon's state and column reads of all slots are
+               in flight together -- one memory round trip per taxon, not one per proposal and taxon;
+               per-slot sums kept in registers across the taxa */
+            int x0s[16], x1s[16], ys[16];
+            bool anyp3 = false;
+#pragma unroll
+            for (int sI = 0; sI < 16; ++sI) {
+              x0s[sI] = 0; x1s[sI] = 0; ys[sI] = 0;
+              if (prop_kind(sI) == PK_PI3) anyp3 |= sI >= p0 && sI < pend && !vetoed(sI);
+            }
             for (int m0 = wave * 64; m0 < M; m0 += TB) {
               const int m = m0 + lane;
-              int dt0 = 0, dt1 = 0;
-              if (m < M)
-                taxon_dt(kind, q, sab[m], sab[M + m], P + m, pre + m, M, kind == PK_PI3 ? hard_bits_col(P + m, M, hl, nh) : 0u,
-                         hcnt, nhall, dt0, dt1);
-              x0 += dt0; x1 += dt1; y0 += abs(dt0); y1 += abs(dt1);
+              const bool mv = m < M;
+              const int a = mv ? sab[m] : 0, b = mv ? sab[M + m] : 0;
+              const HM hb = (anyp3 && mv) ? hard_bits_col<HM>(P + m, M, hl, nh) : (HM)0;
+#pragma unroll
+              for (int sI = 0; sI < 16; ++sI) {
+                if (sI >= p0 && sI < pend && !vetoed(sI)) {
+                  const Prop q = load_prop(sI);
+                  int dt0 = 0, dt1 = 0;
+                  if (mv) taxon_dt(prop_kind(sI), q, a, b, P + m, pre + m, M, hb, hcnt, nhall, dt0, dt1);
+                  x0s[sI] += dt0; x1s[sI] += dt1; ys[sI] += abs(dt0) + abs(dt1);
+                }
+              }
             }
-            const int X0 = wave_sum_i32(x0), X1 = wave_sum_i32(x1), Y0 = wave_sum_i32(y0), Y1 = wave_sum_i32(y1);
-            if (lane == 0) {
-              int *o = pw + (p * NWV + wave) * 8;
-              o[0] = X0; o[1] = X1; o[2] = Y0; o[3] = Y1;
+#pragma unroll
+            for (int sI = 0; sI < 16; ++sI) {
+              if (sI >= p0 && sI < pend && !vetoed(sI)) {
+                /* Y0 = Y1 = sum (|dt0| + |dt1|): upper bounds of both (the decision's error bound) */
+                const int X0 = wave_sum_i32(x0s[sI]), X1 = wave_sum_i32(x1s[sI]), Y = wave_sum_i32(ys[sI]);
+                if (lane == 0) {
+                  int *o = pw + (sI * NWV + wave) * 8;
+                  o[0] = X0; o[1] = X1; o[2] = Y; o[3] = Y;
+                }
+              }
             }
-            STAMP_K(kind);
+            STAMP_K(PK_PI3);
           }
           FST(4);
           __syncthreads();
@@ -2306,7 +2451,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           {
             const int p = lane;
             if (p >= p0 && p < pend) {
-              if (!(vfl & 4)) {
+              if (!((vpk >> 26) & 1)) {
                 int X0 = 0, X1 = 0, Y0 = 0, Y1 = 0;
 #pragma unroll
                 for (int w = 0; w < NWV; ++w) {
@@ -2404,34 +2549,52 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             uint32_t *Pm = P + m;
             const int a = sab[m], b = sab[M + m];
             int dt0, dt1;
-            taxon_dt(kind, q, a, b, Pm, pre + m, M, kind == PK_PI3 ? hard_bits_col(Pm, M, hl, nh) : 0u, hcnt, nhall, dt0, dt1);
+            taxon_dt(kind, q, a, b, Pm, pre + m, M, kind == PK_PI3 ? hard_bits_col<HM>(Pm, M, hl, nh) : (HM)0, hcnt, nhall, dt0, dt1);
             scnt[m] += dt0; scnt[M + m] -= dt0; scnt[2 * M + m] += dt1; scnt[3 * M + m] -= dt1;
             if (kind == PK_PI1) {                                  /* mcmc.c:1266-1297 */
+              /* the shifted words read 8 at a time before they are rewritten (one memory round trip
+                 per 8 words: the HBM-column kernels) */
               if (i < j) {
                 if (ii < a && a <= jj + 1) sab[m] = a - 1;
                 if (ii < b && b <= jj + 1) sab[M + m] = b - 1;
                 const uint32_t vb = (Pm[(i >> 5) * M] >> (i & 31)) & 1u;
-                for (int w = i >> 5; w <= (j >> 5); ++w) {
-                  const uint32_t old = Pm[w * M];
-                  const uint32_t nxt = (w + 1 < NW) ? Pm[(w + 1) * M] : 0u;
-                  const uint32_t sh = (old >> 1) | (nxt << 31);
-                  const uint32_t m1 = range_mask(w, i, j - 1);
-                  uint32_t nw = (old & ~m1) | (sh & m1);
-                  if ((j >> 5) == w) nw = (nw & ~(1u << (j & 31))) | (vb << (j & 31));
-                  Pm[w * M] = nw;
+                for (int w0 = i >> 5; w0 <= (j >> 5); w0 += 8) {
+                  uint32_t wv[9];
+#pragma unroll
+                  for (int t = 0; t < 9; ++t) wv[t] = (w0 + t <= (j >> 5) + 1 && w0 + t < NW) ? Pm[(w0 + t) * M] : 0u;
+#pragma unroll
+                  for (int t = 0; t < 8; ++t) {
+                    const int w = w0 + t;
+                    if (w <= (j >> 5)) {
+                      const uint32_t old = wv[t], nxt = wv[t + 1];
+                      const uint32_t sh = (old >> 1) | (nxt << 31);
+                      const uint32_t m1 = range_mask(w, i, j - 1);
+                      uint32_t nw = (old & ~m1) | (sh & m1);
+                      if ((j >> 5) == w) nw = (nw & ~(1u << (j & 31))) | (vb << (j & 31));
+                      Pm[w * M] = nw;
+                    }
+                  }
                 }
               } else {
                 if (ii <= a && a <= jj) sab[m] = a + 1;
                 if (ii <= b && b <= jj) sab[M + m] = b + 1;
                 const uint32_t vb = (Pm[(i >> 5) * M] >> (i & 31)) & 1u;
-                for (int w = i >> 5; w >= (j >> 5); --w) {
-                  const uint32_t old = Pm[w * M];
-                  const uint32_t prv = (w > 0) ? Pm[(w - 1) * M] : 0u;
-                  const uint32_t sh = (old << 1) | (prv >> 31);
-                  const uint32_t m1 = range_mask(w, j + 1, i);
-                  uint32_t nw = (old & ~m1) | (sh & m1);
-                  if ((j >> 5) == w) nw = (nw & ~(1u << (j & 31))) | (vb << (j & 31));
-                  Pm[w * M] = nw;
+                for (int w0 = i >> 5; w0 >= (j >> 5); w0 -= 8) {
+                  uint32_t wv[9];   /* wv[t] = word w0 - t */
+#pragma unroll
+                  for (int t = 0; t < 9; ++t) wv[t] = (w0 - t >= (j >> 5) - 1 && w0 - t >= 0) ? Pm[(w0 - t) * M] : 0u;
+#pragma unroll
+                  for (int t = 0; t < 8; ++t) {
+                    const int w = w0 - t;
+                    if (w >= (j >> 5)) {
+                      const uint32_t old = wv[t], prv = wv[t + 1];
+                      const uint32_t sh = (old << 1) | (prv >> 31);
+                      const uint32_t m1 = range_mask(w, j + 1, i);
+                      uint32_t nw = (old & ~m1) | (sh & m1);
+                      if ((j >> 5) == w) nw = (nw & ~(1u << (j & 31))) | (vb << (j & 31));
+                      Pm[w * M] = nw;
+                    }
+                  }
                 }
               }
             } else {                                               /* mcmc.c:1446-1474, 1641-1670 */
@@ -2458,7 +2621,14 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               const int lo = min(i, j), hi = max(i, j), rlo = (lo >> 5) + 1, rhi = hi >> 5;
               uint16_t *prem = pre + m;
               int sacc = prem[(rlo - 1) * M];
-              for (int r = rlo; r <= rhi; ++r) { sacc += __popc(Pm[(r - 1) * M]); prem[r * M] = (uint16_t)sacc; }
+              for (int r0 = rlo; r0 <= rhi; r0 += 8) {
+                uint32_t wv[8];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) wv[t] = (r0 + t <= rhi) ? Pm[(r0 + t - 1) * M] : 0u;
+#pragma unroll
+                for (int t = 0; t < 8; ++t)
+                  if (r0 + t <= rhi) { sacc += __popc(wv[t]); prem[(r0 + t) * M] = (uint16_t)sacc; }
+              }
             }
           }
           FST(7);
@@ -2600,7 +2770,7 @@ static bool sr_pair_ok(int N, int M)
   return sr_nwm(N) == 9 && M > 256 && M <= 512;
 }
 
-static sr_kfn sr_pick_kernel(int TB, int N, bool gm, bool pr = false)
+static sr_kfn sr_pick_kernel(int TB, int N, int M, bool gm, bool pr, int nh)
 {
   if (pr) return (TB == 1024 && !gm) ? (sr_kfn)sr_sweep_kernel<1024, 9, false, true> : nullptr;
 #ifdef SR_PAIR_ONLY   /* register-pressure experiments: compile the pair kernel alone */
@@ -2612,7 +2782,7 @@ static sr_kfn sr_pick_kernel(int TB, int N, bool gm, bool pr = false)
     if (TB == 1024) return (sr_kfn)sr_sweep_kernel<1024, 0, true>;
     return nullptr;
   }
-  const int nwm = sr_regwalk(N, TB, false) ? sr_nwm(N) : 0;
+  const int nwm = sr_regwalk(N, M, TB, false, nh) ? sr_nwm(N) : 0;
   if (TB == 256) return nwm == 9 ? (sr_kfn)sr_sweep_kernel<256, 9, false> : nwm == 17 ? (sr_kfn)sr_sweep_kernel<256, 17, false> : (sr_kfn)sr_sweep_kernel<256, 0, false>;
   if (TB == 512) return nwm == 9 ? (sr_kfn)sr_sweep_kernel<512, 9, false> : nwm == 17 ? (sr_kfn)sr_sweep_kernel<512, 17, false> : (sr_kfn)sr_sweep_kernel<512, 0, false>;
   if (TB == 1024) return (sr_kfn)sr_sweep_kernel<1024, 0, false>;
@@ -2650,21 +2820,21 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
   int TB = block_threads;
   /* default: the pair kernel where it applies (two lanes per taxon, 1024 threads), else one thread
      per taxon in the smallest block of 256..1024 threads that covers M */
-  d->pr = (TB <= 0 && gm_force != 1 && sr_pair_ok(st->N, st->M)) ? 1 : 0;
+  d->pr = (TB <= 0 && gm_force != 1 && st->nh <= 32 && sr_pair_ok(st->N, st->M)) ? 1 : 0;
   if (d->pr) TB = 1024;
   if (TB <= 0) { TB = 256; while (TB < st->M && TB < 1024) TB *= 2; }
   d->TB = TB; d->TPT = 1;
   /* columns in LDS when the whole layout fits, else the HBM-column variant */
   d->gm = 0;
-  Lay L = sr_layout(st->N, st->M, st->NW, TB, false, d->pr != 0);
-  if (L.total > 160 * 1024) { d->gm = 1; L = sr_layout(st->N, st->M, st->NW, TB, true); }
+  Lay L = sr_layout(st->N, st->M, st->NW, TB, false, d->pr != 0, st->nh);
+  if (L.total > 160 * 1024) { d->gm = 1; L = sr_layout(st->N, st->M, st->NW, TB, true, false, st->nh); }
   if (gm_force >= 0 && gm_force != d->gm) {   /* explicit variant request (tests) */
     d->gm = gm_force;
-    L = sr_layout(st->N, st->M, st->NW, TB, d->gm != 0, d->pr != 0);
+    L = sr_layout(st->N, st->M, st->NW, TB, d->gm != 0, d->pr != 0, st->nh);
   }
   if (d->gm) d->pr = 0;
   d->lds = L.total;
-  if (!sr_pick_kernel(TB, st->N, d->gm != 0, d->pr != 0) || d->lds > 160 * 1024) { delete d; return -6; }
+  if (!sr_pick_kernel(TB, st->N, st->M, d->gm != 0, d->pr != 0, st->nh) || d->lds > 160 * 1024) { delete d; return -6; }
   d->rec_cap = rec_cap_calls > 0 ? rec_cap_calls : 1;
   const size_t C = st->nchains;
   KArgs &A = d->args;
@@ -2691,7 +2861,7 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
     rc |= dev_alloc_copy(d, &A.gcbuf, (const double *)nullptr, C * sr_gm_cbuf(st->M));
   }
   if (rc) { srk_destroy(d); return -5; }
-  sr_kfn k = sr_pick_kernel(TB, st->N, d->gm != 0, d->pr != 0);
+  sr_kfn k = sr_pick_kernel(TB, st->N, st->M, d->gm != 0, d->pr != 0, st->nh);
   if (hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d->lds) != hipSuccess) {
     srk_destroy(d);
     return -5;
@@ -2721,7 +2891,7 @@ extern "C" int srk_run(srk_dev *d, int calls, int spc, int save, int rec_base)
   HIPCHK(hipSetDevice(d->device));
   KArgs A = d->args;
   A.calls = calls; A.spc = spc; A.save = save; A.rec_base = rec_base;
-  sr_kfn k = sr_pick_kernel(d->TB, d->N, d->gm != 0, d->pr != 0);
+  sr_kfn k = sr_pick_kernel(d->TB, d->N, d->M, d->gm != 0, d->pr != 0, d->nh);
   if (d->have_events) HIPCHK(hipEventRecord(d->ev0, d->stream));
   hipLaunchKernelGGL(k, dim3(d->nchains), dim3(d->TB), d->lds, d->stream, A);
   HIPCHK(hipGetLastError());

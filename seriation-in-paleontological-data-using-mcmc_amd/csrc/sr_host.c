@@ -422,8 +422,9 @@ static int session_new(const sr_dataset *ds, const sr_chain_spec *specs, int32_t
   if (opts) o = *opts; else sr_default_opts(&o);
   if (o.sweeps_per_call <= 0) return SR_EINVAL;
   if (o.manycd != 0) return SR_EUNSUPPORTED;
-  /* nh <= 32 hard sites (register-held), N <= 2048 (a wave holds the hard bitmap, one word per lane) */
-  if (ds->nh > SR_NHMAX || ds->N > 2048 || ds->M > 32767) return SR_EUNSUPPORTED;
+  /* nh <= 64 hard sites (a 64-bit mask per taxon), N <= 4095 (12-bit positions in the packed proposal
+     records); records are int16 (M <= 32767).  The LDS layout must also fit 160 KB (srk_create). */
+  if (ds->nh > SR_NHMAX || ds->N > 4095 || ds->M > 32767) return SR_EUNSUPPORTED;
   sr_session *s = (sr_session *)calloc(1, sizeof(*s));
   if (!s) return SR_ENOMEM;
   s->ds.N = ds->N; s->ds.M = ds->M; s->ds.nh = ds->nh;
@@ -621,7 +622,7 @@ static uint64_t dataset_hash(const sr_dataset *ds)
 }
 
 typedef struct { size_t bytes; void *p; } ck_part;
-#define SR_CK_VERSION 2   /* 2: SR_NACC counters per chain */
+#define SR_CK_VERSION 3   /* 2: SR_NACC counters per chain; 3: SR_NHMAX = 64 hard positions per chain */
 
 static int ck_parts(sr_state_host *st, ck_part *pt)
 {

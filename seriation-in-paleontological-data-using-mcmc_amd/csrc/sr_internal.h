@@ -7,7 +7,7 @@
 #include <stdint.h>
 #include <stddef.h>
 
-#define SR_NHMAX 32      /* hard sites per dataset the kernel supports */
+#define SR_NHMAX 64      /* hard sites per dataset the kernel supports (a 64-bit mask per taxon; one per lane) */
 #define SR_RING 8        /* MT19937 blocks resident per chain */
 
 /* Per-chain state in HBM, struct-of-arrays over chains.  Layout (per chain c):

@@ -100,10 +100,10 @@ def test_restore_rejects_bad_checkpoints(tmp_path):
     bad.write_bytes(b"XXXX" + bytes(40))
     assert restore(bad) == -2                                              # SR_EPARSE
     other = tmp_path / "other.srck"
-    other.write_bytes(b"SRCK" + struct.pack("<I4iQ", 2, ds.N + 1, ds.M, 0, 2, 0))
+    other.write_bytes(b"SRCK" + struct.pack("<I4iQ", 3, ds.N + 1, ds.M, 0, 2, 0))
     assert restore(other) == -1                                            # SR_EINVAL: other dataset
     samedims = tmp_path / "hash.srck"
-    samedims.write_bytes(b"SRCK" + struct.pack("<I4iQ", 2, ds.N, ds.M, ds.nh, 2, 12345))
+    samedims.write_bytes(b"SRCK" + struct.pack("<I4iQ", 3, ds.N, ds.M, ds.nh, 2, 12345))
     assert restore(samedims) == -1                                         # SR_EINVAL: dataset hash differs
 
 
@@ -133,7 +133,7 @@ def test_restore_validates_chain_state(tmp_path):
     assert restore(good) in (0, L.SR_EDEVICE)
     N, M, nh, NW = ds.N, ds.M, ds.nh, (ds.N + 31) // 32
     off = 32 + C * ctypes.sizeof(L.sr_chain_spec)
-    sizes = [("P", C * NW * M * 4), ("rpi", C * N * 4), ("hp", C * 32 * 4), ("ab", C * 2 * M * 4),
+    sizes = [("P", C * NW * M * 4), ("rpi", C * N * 4), ("hp", C * 64 * 4), ("ab", C * 2 * M * 4),
              ("cnt", C * 4 * M * 4), ("cdl", C * 4 * 8), ("mt", C * 8 * 624 * 4), ("rng", C * 2 * 8), ("acc", C * 10 * 8)]
     base = {}
     for name, n in sizes:
@@ -165,27 +165,33 @@ def test_restore_validates_chain_state(tmp_path):
 
 
 def test_hard_site_limit_boundary():
-    """The kernel holds at most SR_NHMAX = 32 hard sites (a 32-bit mask per taxon): 33 are refused
-    with SR_EUNSUPPORTED before any device call (the 32-site case runs in tests/test_gpu_edge.py
-    'nh32').  The reference has no such limit."""
-    def text(nh, N=40, M=6):
+    """The kernel holds at most SR_NHMAX = 64 hard sites (a 64-bit mask per taxon, one hard site per
+    lane): 65 are refused with SR_EUNSUPPORTED before any device call (40 and 64 run bit-exact in
+    tests/test_gpu_edge.py 'nh40' / 'nh64').  Sites are limited to N <= 4095 (12-bit positions in the
+    packed proposal records): 4096 are refused the same way.  The reference has neither limit."""
+    def text(nh, N=90, M=6):
         rows = ["%d %d" % (N, M)]
         for i in range(N):
             rows.append(" ".join("1" if (i + m) % 3 == 0 else "0" for m in range(M)) + (" *" if i < nh else ""))
         return ("\n".join(rows) + "\n").encode()
-    ds33 = sa.Dataset.parse(text(33))
-    assert ds33.nh == 33
+    ds65 = sa.Dataset.parse(text(65))
+    assert ds65.nh == 65
     with pytest.raises(sa.SrError) as e:
-        sa.Session(ds33, [1])
+        sa.Session(ds65, [1])
     assert e.value.code == L.SR_EUNSUPPORTED
     out = (L.sr_chain_summary * 1)()
     devs = (ctypes.c_int32 * 1)(0)
-    assert sa.lib().sr_run_chains_multi(ctypes.byref(ds33.c), sa.core.make_specs([1]), 1, None, devs, 1,
+    assert sa.lib().sr_run_chains_multi(ctypes.byref(ds65.c), sa.core.make_specs([1]), 1, None, devs, 1,
                                         ctypes.cast(None, L.SINK_FN), None, out) == L.SR_EUNSUPPORTED
+    big = sa.Dataset.parse(text(3, N=4096, M=2), maxs=0)
+    with pytest.raises(sa.SrError) as e:
+        sa.Session(big, [1])
+    assert e.value.code == L.SR_EUNSUPPORTED
     if not _gpu_present():
-        with pytest.raises(sa.SrError) as e:
-            sa.Session(sa.Dataset.parse(text(32)), [1])
-        assert e.value.code == L.SR_EDEVICE   # accepted by the limit check, then no device
+        for ok in (sa.Dataset.parse(text(64)), sa.Dataset.parse(text(3, N=4095, M=2), maxs=0)):
+            with pytest.raises(sa.SrError) as e:
+                sa.Session(ok, [1])
+            assert e.value.code == L.SR_EDEVICE   # accepted by the limit check, then no device
 
 
 def test_multi_device_arguments_rejected():

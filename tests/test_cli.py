@@ -136,3 +136,21 @@ def test_product_cli_stderr_lines_on_fake_device(tmp_path):
                  "chain_00")
     assert pa.returncode == 0 and pb.returncode == 0, pb.stderr
     assert ref_lines(pa.stderr) == ref_lines(pb.stderr) and len(ref_lines(pb.stderr)) == 7
+
+
+def test_manycd_refused(tmp_path):
+    """`mcmc manycd Tburnin T` with manycd = 1 (per-taxon c, d: mcmc.c:118, 777-786, 807-816) is refused
+    with SR_EUNSUPPORTED's message and exit 1 before any device call; the reference's own driver never
+    sets it (script.py:44 passes the chain index alone).  The library refuses it the same way."""
+    p = run_cli(PRODUCT_CLI, str(tmp_path), "g5s5.txt", ["1", "2", "2"], 5, "chain_00")
+    assert p.returncode == 1
+    assert L.lib().sr_strerror(L.SR_EUNSUPPORTED).decode() in p.stderr.decode()
+    import ctypes
+    import seriation_amd as sa
+    ds = sa.Dataset.load(os.path.join(DS, "g5s5.txt"))
+    o = L.sr_run_opts()
+    L.lib().sr_default_opts(ctypes.byref(o))
+    o.manycd = 1
+    h = ctypes.c_void_p()
+    assert L.lib().sr_session_create(ctypes.byref(ds.c), sa.core.make_specs([1]), 1, ctypes.byref(o), ctypes.byref(h)) == \
+        L.SR_EUNSUPPORTED

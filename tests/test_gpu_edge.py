@@ -1,6 +1,6 @@
 """GPU parity on edge-case datasets (every integer and f64 bit against the oracle).
 
-Covers: tiny matrices, no hard sites, many hard sites (<= 32), N - nh < 2 (pi3 always vetoed),
+Covers: tiny matrices, no hard sites, many hard sites (<= 64), N - nh < 2 (pi3 always vetoed), N > 2048,
 M not a multiple of 64, all-zero columns, N on a word boundary, the register-resident Gibbs
 kernels (walks of <= 9 and <= 17 words) and the LDS-walk kernel (longer walks), block sizes
 256 / 512 / 1024 and several taxa per thread.
@@ -14,13 +14,13 @@ import seriation_amd as sa
 pytestmark = pytest.mark.gpu
 
 
-def make_text(N, M, nh, seed, zero_cols=2, density=0.15):
+def make_text(N, M, nh, seed, zero_cols=2, density=0.15, noise=0.02):
     rng = np.random.default_rng(seed)
     X = np.zeros((N, M), np.uint8)
     for m in range(M):
         a = rng.integers(0, N)
         L = rng.integers(1, max(2, N // 2) + 1)
-        col = (rng.random(N) < 0.02).astype(np.uint8)
+        col = (rng.random(N) < noise).astype(np.uint8)
         col[a:min(N, a + L)] = (rng.random(min(N, a + L) - a) < density * 3).astype(np.uint8)
         X[:, m] = col
     X[:, rng.choice(M, size=min(zero_cols, M), replace=False)] = 0
@@ -40,6 +40,13 @@ CASES = [
     ("no-hard", 40, 70, 0, 0),
     ("many-hard", 60, 100, 30, 0),
     ("nh32", 90, 64, 32, 0),
+    ("nh40", 120, 70, 40, 0),
+    ("nh64", 150, 64, 64, 0),
+    ("n2500", 2500, 24, 10, 0),
+    # nh = N - 1 / N - 2: mcmc_randomize's hard-position scan reads q[nh] past the end there
+    # (mcmc.c:530, UB); host and oracle both stop at nh (the intended reading)
+    ("nh-n-1", 40, 30, 39, 0),
+    ("nh-n-2", 41, 30, 39, 0),
     ("word-boundary-256", 256, 64, 12, 0),
     ("walk17", 300, 130, 9, 0),
     ("lds-walk", 600, 80, 7, 0),
@@ -65,7 +72,7 @@ def test_edge_parity(name, N, M, nh, tb):
 
 # The HBM-column variant (columns, prefix tables, a/b, counts in HBM; chosen automatically when
 # the LDS layout exceeds 160 KB) forced on small cases: same bits as the oracle.
-HBM_CASES = [c for c in CASES if c[0] in ("tiny", "many-hard", "walk17", "lds-walk", "tb256-2-per-thread",
+HBM_CASES = [c for c in CASES if c[0] in ("tiny", "many-hard", "nh64", "n2500", "walk17", "lds-walk", "tb256-2-per-thread",
                                           "3-per-thread")]
 
 
@@ -84,6 +91,28 @@ def test_edge_parity_hbm_columns(name, N, M, nh, tb):
         np.testing.assert_array_equal(ri[k], o["rec_int"], err_msg="%s seed %d" % (name, s))
         assert np.array_equal(rd[k].view(np.uint64), o["rec_dbl"].view(np.uint64)), (name, s)
         assert summ[k]["consistent"] == 0
+
+
+@pytest.mark.parametrize("N,M,noise,seeds,burnin", [(256, 300, 0.003, [4], 60), (400, 150, 0.02, [4, 19], 45)],
+                         ids=["walk9", "walk17"])
+def test_steep_walks(N, M, noise, seeds, burnin):
+    """Ranges filled with ones (little noise outside): once the order settles d ends near its bound 0.2
+    and |vA| = |log2(d / (1 - c))| near its largest value, the regime where Gibbs walks sink deepest
+    between window words (draw_fast_s: the 9-word walks rely on the bound -40 - 32 nk |vA| > -710
+    and take no test; the 17-word walks test for window word starts below 2^-700).  Same bits as
+    the oracle."""
+    text = make_text(N, M, 5, seed=N * 7 + M, density=0.34, noise=noise)
+    ds = sa.Dataset.parse(text, maxs=0)
+    summ, (ri, rd) = sa.run_chains(ds, seeds, burnin_calls=burnin, sample_calls=10, keep_records=True)
+    for k, s in enumerate(seeds):
+        o = oracle_ref.run_chain(text, s, burnin, 10, maxs=0)
+        assert o["rc"] == 0
+        np.testing.assert_array_equal(ri[k], o["rec_int"], err_msg="seed %d" % s)
+        assert np.array_equal(rd[k].view(np.uint64), o["rec_dbl"].view(np.uint64)), s
+        assert summ[k]["consistent"] == 0
+        # the steep regime on the last call: 32 nk |vA| > 650 with its c, d (log values in the records)
+        c, d = np.exp(rd[k][-1, 0]), np.exp(rd[k][-1, 1])
+        assert 32 * ((N >> 5) + 1) * abs(np.log2(d / (1 - c))) > 650, (c, d)
 
 
 def test_checkpoint_resume_continues_exactly(tmp_path):

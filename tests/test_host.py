@@ -149,3 +149,34 @@ def test_init_chain_matches_oracle(name):
         # hard sites keep their relative order under mcmc_randomize (mcmc.c:496-593)
         hp = pi[ds.hard.astype(bool)]
         assert (np.diff(hp) > 0).all()
+
+
+@pytest.mark.parametrize("N,nh", [(40, 39), (41, 39), (12, 11), (30, 0), (30, 30)])
+def test_init_chain_hard_sites_near_n(N, nh):
+    """mcmc_randomize with nh close to N: the reference's scan of the chosen hard positions reads
+    q[nh] one past the end once all nh are matched (mcmc.c:530, UB); host and oracle both stop at nh.
+    nh = 0 only shuffles (no initab, mcmc.c:486-494); nh = N keeps the identity order.  The host
+    initialisation equals the oracle's for several seeds, hard sites in their original order."""
+    rng = np.random.default_rng(N * 100 + nh)
+    M = 9
+    X = (rng.random((N, M)) < 0.3).astype(int)
+    X[:, 3] = 0   # a zero column
+    hard = np.zeros(N, bool)
+    hard[rng.choice(N, nh, replace=False)] = True
+    text = ("%d %d\n" % (N, M) + "".join(" ".join(map(str, X[i])) + (" *" if hard[i] else "") + "\n"
+                                        for i in range(N))).encode()
+    ds = sa.Dataset.parse(text)
+    assert ds.nh == nh
+    for seed in (1, 5, 99):
+        a = np.zeros(M, np.int32)
+        b = np.zeros(M, np.int32)
+        pi = np.zeros(N, np.int32)
+        cdl = np.zeros(3)
+        pos = ctypes.c_uint64()
+        assert sa.lib().sr_host_init_chain(ctypes.byref(ds.c), seed, a.ctypes.data_as(PI), b.ctypes.data_as(PI),
+                                           pi.ctypes.data_as(PI), cdl.ctypes.data_as(PD), ctypes.byref(pos)) == 0
+        o = oracle_ref.run_chain(text, seed, 0, 0)
+        np.testing.assert_array_equal(np.concatenate([a, b, pi]), o["init"])
+        assert cdl.view(np.uint64).tolist() == o["init_cdl"].view(np.uint64).tolist()
+        assert sorted(pi.tolist()) == list(range(N))
+        assert (np.diff(pi[hard]) > 0).all()

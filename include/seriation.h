@@ -163,7 +163,9 @@ int32_t sr_session_block_threads(const sr_session *s);
 /* Kernel variant the session runs: 0 = occurrence columns in LDS, one thread per taxon; 1 = columns
  * in HBM (chosen when the LDS layout exceeds 160 KB, e.g. 1024 sites x 2048 taxa); 2 = columns in
  * LDS, two lanes per taxon (the pair kernel: walks of <= 9 words and 257..512 taxa; opt-in with
- * SR_KERNEL=pair in the environment and block_threads unset -- slower than variant 0). */
+ * SR_KERNEL=pair in the environment and block_threads unset -- slower than variant 0);
+ * 3 = columns in HBM, split chains: two co-resident workgroups per chain, each owning half of the
+ * taxa (1024 threads, 1025..2048 taxa, grid co-resident; SR_SPLIT=0 in the environment disables it). */
 int32_t sr_session_variant(const sr_session *s);
 /* Checkpoint / resume (the reference has none): the full chain state (columns, pi,
    limits, counts, c/d/loglik, MT19937 ring and cursor, acceptance counters) to a file; restoring

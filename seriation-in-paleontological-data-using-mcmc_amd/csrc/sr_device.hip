@@ -58,6 +58,7 @@ struct KArgs {
   uint16_t *gpre;            /* gm variant scratch, per chain: column prefix tables */
   uint32_t *pkey;            /* [chain][2] Philox keys (SR_F_RNG_PHILOX), else null: MT19937 */
   double *gck, *glbuf, *gcbuf;   /* gm variant scratch: Gibbs checkpoints, logl terms, exact-delta terms */
+  int *xflag, *xbuf, *xerr;      /* split chains (SP kernels): [chain][2] progress flags, exchange slots, timeout flag */
 };
 
 /* ---------------------------------------------------------------- LDS carve */
@@ -117,10 +118,19 @@ __host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB, bo
   L.total = o;
   return L;
 }
+/* Split chains (SP kernels: HBM columns, two co-resident workgroups per chain, each owning half of
+ * the taxa, one taxon per thread).  Half h owns taxa [h Mh, min(M, (h + 1) Mh)), Mh a multiple of 64
+ * (whole exact-delta chunks); blocks 16 g + 8 h + x hold chain 8 g + x, so a chain's halves are
+ * dispatched to the same XCD (round-robin placement) and exchange through the same L2.  Exchange
+ * slots per chain (ints): [2 parity][2 half][4] totals, [2 parity][2 half][16][4] proposal sums,
+ * [2 parity][KT] exact-delta chunk counts. */
+__host__ __device__ static inline int sr_sp_half(int M) { return (((M + 1) / 2) + 63) & ~63; }
+__host__ __device__ static inline size_t sr_sp_xb(int M) { return 16 + 256 + 2 * (size_t)((M + 63) / 64); }
 /* per-chain HBM scratch of the gm variant (elements): pre u16, ck f64, lbuf f64, cbuf f64 */
 __host__ __device__ static inline size_t sr_gm_pre(int M, int NW) { return (size_t)(NW + 1) * M; }
 __host__ __device__ static inline size_t sr_gm_ck(int N, int M, int TB) { return (size_t)((N >> 5) + 1) * sr_ckstride(M, TB); }
 __host__ __device__ static inline size_t sr_gm_cbuf(int M) { return (size_t)2 * ((M + 63) / 64) * 64; }
+__host__ __device__ static inline size_t sr_sp_ck(int N, int TB) { return (size_t)((N >> 5) + 1) * 2 * TB; }   /* split chains */
 /* misc slots (8-byte words) */
 #define MS_TOT 0      /* 4 ints in 2 words */
 #define MS_DELTA 2
@@ -1538,6 +1548,40 @@ __device__ __forceinline__ double exact_sum_wave(const double *cbuf, const int *
   return r;
 }
 
+/* Split chains: the exchange data crosses workgroups (other CUs, possibly other XCDs), so it is
+ * written and read with relaxed agent-scope atomics -- accesses that bypass the caches not coherent
+ * across the agent -- and a flag store follows the data only after s_waitcnt (xsync in the kernel). */
+template <typename T> __device__ __forceinline__ void xst(T *p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <typename T> __device__ __forceinline__ T xld(const T *p)
+{
+  return __hip_atomic_load(const_cast<T *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+/* exact_sum_wave for terms in HBM (gm kernels): every wave reads 4 chunks per round trip (one
+ * coalesced load per lane) and adds them in chunk and position order through readlane, so the
+ * sum is the same sequential sum and is wave-uniform in every wave (no broadcast).  XA: terms and
+ * counts written by the other half of a split chain (agent-scope loads). */
+template <bool XA>
+__device__ __forceinline__ double exact_sum_gm(const double *cbuf, const int *ccnt, int nch, int lane, int CH)
+{
+  double s = 0.0;
+  for (int c0 = 0; c0 < nch; c0 += 4) {
+    double v[4];
+    int n[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      n[q] = (c0 + q < nch) ? (XA ? xld(ccnt + c0 + q) : ccnt[c0 + q]) : 0;
+      n[q] = __builtin_amdgcn_readfirstlane(n[q]);
+      const double *pq = cbuf + (size_t)(c0 + q) * CH + lane;
+      v[q] = (lane < n[q]) ? (XA ? xld(pq) : *pq) : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      for (int l = 0; l < n[q]; ++l) s = s + readlane_f64(v[q], l);
+  }
+  return s;
+}
+
 /* ---------------------------------------------------------------- proposals */
 #define PK_PI1 1
 #define PK_PI2 20
@@ -1677,15 +1721,18 @@ __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, 
  * ascending m by lane 0 of every wave.  Block-uniform call (contains a barrier). */
 /* PR (pair kernels): taxon m = m0 + lane / 2 is evaluated by its even lane; a wave's 32 taxa form
  * one chunk (ballot bits of even lanes in ascending lane order = ascending m).  KT = chunks. */
-template <bool PR>
+/* GM: terms in HBM (exact_sum_gm).  SP (split chains): this half evaluates its own taxa [olo, ohi)
+ * (whole chunks), the terms and counts go through the exchange (xsync: both halves' writes done),
+ * and both halves compute the same sum. */
+template <bool PR, bool GM, bool SP, typename XSync>
 __device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const int32_t *sab, const uint32_t *P, const uint16_t *pre,
-                                              int M, int KT,
+                                              int M, int KT, int olo, int ohi,
                                               int hl, int nh, const int16_t *hcnt, const int16_t *nhall, double *cb, int *cc, double *xs,
-                                              int lane, int wave, int TB)
+                                              int lane, int wave, int TB, XSync &&xsync)
 {
   constexpr int CH = PR ? 32 : 64;
   const bool ev = PR ? (lane & 1) == 0 : true;
-  for (int m0 = wave * CH; m0 < KT * CH; m0 += (PR ? TB / 2 : TB)) {
+  for (int m0 = olo + wave * CH; m0 < ohi; m0 += (PR ? TB / 2 : TB)) {   /* (chunk starts below M: KT chunks) */
     const int ch = m0 / CH, m = m0 + (PR ? (lane >> 1) : lane);
     int dt0 = 0, dt1 = 0;
     if (m < M && ev)
@@ -1694,11 +1741,12 @@ __device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const i
     const double tv = (m < M && ev) ? qval(dt0, -dt0, dt1, -dt1, K) : 0.0;
     const uint64_t msk = __ballot(tv != 0.0);
     const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
-    if (tv != 0.0) cb[ch * CH + pos] = tv;
-    if (lane == 0) cc[ch] = __popcll(msk);
+    if (tv != 0.0) { if constexpr (SP) xst(cb + ch * CH + pos, tv); else cb[ch * CH + pos] = tv; }
+    if (lane == 0) { if constexpr (SP) xst(cc + ch, (int)__popcll(msk)); else cc[ch] = __popcll(msk); }
   }
-  __syncthreads();
-  return exact_sum_wave(cb, cc, KT, xs, lane, CH);
+  if constexpr (SP) xsync(); else __syncthreads();
+  if constexpr (GM) return exact_sum_gm<SP>(cb, cc, KT, lane, CH);
+  else return exact_sum_wave(cb, cc, KT, xs, lane, CH);
 }
 
 /* words of slack kept resident after the Gibbs draws: the proposals and the next c, d
@@ -1715,9 +1763,10 @@ __device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const i
  *   B  Gibbs (a_m, b_m) of own taxa (mcmc_sampleab); [barrier + logl on the last sweep]
  *   C  16 MH permutation proposals: draws, own taxa's count deltas and terms, per-wave
  *      partial sums -> one barrier -> certified decision -> apply to own taxa. */
-template <int TB, int NWM, bool GM, bool PR = false>
+template <int TB, int NWM, bool GM, bool PR = false, bool SP = false>
 __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 {
+  static_assert(!SP || (GM && !PR && NWM == 0), "split chains: HBM-column kernels only");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NWV = TB / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1725,8 +1774,15 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
      otherwise one thread per taxon */
   const int hf = PR ? (tid & 1) : 0, tx = PR ? (tid >> 1) : tid;
   constexpr int TXS = PR ? TB / 2 : TB;   /* taxon stride */
-  const int chain = blockIdx.x;
+  /* SP: two workgroups per chain (sr_sp_half); both hold the whole block-uniform state (RNG ring,
+     rpi, hard tables, c, d, loglik) and take every decision identically, each from sums exchanged
+     with the other half; each owns half of the taxa (one per thread) */
+  const int chain = SP ? (int)((blockIdx.x >> 4) << 3) + (int)(blockIdx.x & 7) : (int)blockIdx.x;
+  const int half = SP ? (int)((blockIdx.x >> 3) & 1) : 0;
+  if (SP && chain >= A.nchains) return;   /* grid padding (whole blocks) */
   const int N = A.N, M = A.M, NW = A.NW, nh = A.nh;
+  const int olo = SP ? half * sr_sp_half(M) : 0, ohi = SP ? min(M, olo + sr_sp_half(M)) : M;   /* own taxa */
+  const int mt = olo + tx;   /* own taxon, one-taxon-per-thread kernels */
   const int KTC = (M + sr_chunk(PR) - 1) / sr_chunk(PR);   /* exact-delta chunks */
   const Lay L = sr_layout(N, M, NW, TB, GM, PR, nh);
   double *tabs = (double *)(smem + L.tab);
@@ -1741,8 +1797,9 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   uint16_t *pre = GM ? A.gpre + (size_t)chain * sr_gm_pre(M, NW) : (uint16_t *)(smem + L.pre);   /* column prefix ones */
   int16_t *hcnt = (int16_t *)(smem + L.ht) + wave * (2 * N + 2);    /* this wave's hard-site tables */
   int16_t *nhall = hcnt + N + 1;
-  const int CKS = sr_ckstride(M, TB);
-  double *ckb = GM ? A.gck + (size_t)chain * sr_gm_ck(N, M, TB) : (double *)(smem + L.ck);
+  const int CKS = SP ? 2 * TB : sr_ckstride(M, TB);   /* SP: slots [half TB + tid] */
+  double *ckb = GM ? A.gck + (size_t)chain * (SP ? sr_sp_ck(N, TB) : sr_gm_ck(N, M, TB)) : (double *)(smem + L.ck);
+  const int ckslot = SP ? half * TB + tid : tid;   /* this thread's Gibbs checkpoint slots */
   int *ccnt = (int *)(smem + L.ccnt);
   int32_t *sab = GM ? A.ab + (size_t)chain * 2 * M : (int32_t *)(smem + L.sab);     /* a[M], b[M] */
   int32_t *scnt = GM ? A.cnt + (size_t)chain * 4 * M : (int32_t *)(smem + L.scnt);  /* t0[M], f0[M], t1[M], f1[M] */
@@ -1755,6 +1812,33 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   double *xs = (double *)(smem + L.xs) + wave;
   uint64_t *misc = (uint64_t *)(smem + L.misc);
   uint32_t *ptab = (uint32_t *)(smem + L.ptab);   /* [4][128]: pi1, pi2, pi3 records and pi3 ranks per word offset */
+  /* SP exchange: flags [2], slots (sr_sp_xb); xseq counts exchanges (block-uniform, the same
+     sequence in both halves) */
+  int *xfl = SP ? A.xflag + 2 * (size_t)chain : nullptr;
+  int *xb = SP ? A.xbuf + (size_t)chain * sr_sp_xb(M) : nullptr;
+  int xseq = 0;
+  bool xbroken = false;   /* thread 0: the other half missed a deadline once; stop waiting */
+  /* both halves' exchange writes done and visible: each thread's stores acknowledged, the block's
+     flag raised, the other half's flag awaited (bounded: a half that never arrives -- not
+     co-resident -- sets xerr and the launch completes with garbage the host refuses) */
+  auto xsync = [&]() {
+    if constexpr (SP) {
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      ++xseq;
+      if (tid == 0) {
+        xst(xfl + half, xseq);
+        if (!xbroken) {
+          int n = 0;
+          while (xld(xfl + (half ^ 1)) < xseq) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++n > (1 << 22)) { xbroken = true; xst(A.xerr, 1); break; }
+          }
+        }
+      }
+      __syncthreads();
+    }
+  };
 
   /* ---- load tables and state */
   for (int i = tid; i < 256; i += TB) {
@@ -1808,10 +1892,10 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   __syncthreads();
 
   build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane);
-  for (int m = tid; m < M; m += TB) col_pre_build(pre + m, P + m, M, NW);   /* own columns */
+  for (int m = olo + tid; m < ohi; m += TB) col_pre_build(pre + m, P + m, M, NW);   /* own columns */
   {
     const int hl0 = (lane < nh) ? hp[lane] : 0;   /* loaded with every lane active */
-    if (M <= TXS && tx < M) hbc = hard_bits_col<HM>(P + tx, M, hl0, nh);
+    if ((SP || M <= TXS) && mt < ohi) hbc = hard_bits_col<HM>(P + mt, M, hl0, nh);
   }
   const double ec = sr_exp_m(SR_LOGEPSILON, &tb);
   const uint32_t nhard = (uint32_t)nh;
@@ -1826,7 +1910,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       /* ============ phase A: totals and the c, d draws (mcmc.c:768-825) */
       {
         int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-        for (int m = tid; m < M; m += TB) { s0 += scnt[m]; s1 += scnt[M + m]; s2 += scnt[2 * M + m]; s3 += scnt[3 * M + m]; }
+        for (int m = olo + tid; m < ohi; m += TB) { s0 += scnt[m]; s1 += scnt[M + m]; s2 += scnt[2 * M + m]; s3 += scnt[3 * M + m]; }
         s0 = wave_sum_i32(s0); s1 = wave_sum_i32(s1); s2 = wave_sum_i32(s2); s3 = wave_sum_i32(s3);
         int *tw = tot + (par * NWV + wave) * 4;
         if (lane == 0) { tw[0] = s0; tw[1] = s1; tw[2] = s2; tw[3] = s3; }
@@ -1841,6 +1925,13 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         for (int w = 0; w < NWV; ++w) {
           const int *tw = tot + (par * NWV + w) * 4;
           s0 += tw[0]; s1 += tw[1]; s2 += tw[2]; s3 += tw[3];
+        }
+        if constexpr (SP) {   /* + the other half's totals */
+          int *xt = xb + par * 8;
+          if (tid == 0) { xst(xt + 4 * half, s0); xst(xt + 4 * half + 1, s1); xst(xt + 4 * half + 2, s2); xst(xt + 4 * half + 3, s3); }
+          xsync();
+          const int *yt = xt + 4 * (half ^ 1);
+          s0 += xld(yt); s1 += xld(yt + 1); s2 += xld(yt + 2); s3 += xld(yt + 3);
         }
         /* mcmc_samplec then mcmc_sampled: Beta(1 + f1, 1 + t0), Beta(1 + f0, 1 + t1) */
         if (!draw_cd_fast(R, c, d, s3, s0, s1, s2, tb, lane)) {
@@ -1911,7 +2002,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         FST(1);
         rng_ensure(R, min(2 * (mhi - mlo) + SR_RNG_SLACK, rcap), tid, TB);
         FST(8);
-        for (int m = mlo + tx; m < mhi; m += TXS) {   /* PR: pair-uniform */
+        for (int m = max(mlo, olo) + tx; m < min(mhi, ohi); m += TXS) {   /* PR: pair-uniform; SP: own taxa */
           const uint32_t *Pm = P + m;
           const double ua = rng_peek(R, 2 * (m - mlo)) / 4294967296.0;
           const double ub = rng_peek(R, 2 * (m - mlo) + 1) / 4294967296.0;
@@ -1968,7 +2059,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             int d0, e0, d1, e1;
             const bool rev = pass != 0;
             const int res = draw_fast(Pm, M, N, NW, rev, rev ? N - b0 : a0, rev ? N - na : b0, rev ? POb : POa,
-                                      rev ? ub : ua, K, tb, vA, vB, rA, rB, T4w, ckb + tid, CKS, &misc[MS_FBK], d0, e0,
+                                      rev ? ub : ua, K, tb, vA, vB, rA, rB, T4w, ckb + ckslot, CKS, &misc[MS_FBK], d0, e0,
                                       d1, e1 GSTAMP_PASS);
             GSTAMP_K4();
             t0 += d0; f0 += e0; t1 += d1; f1 += e1;
@@ -1979,8 +2070,10 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             nchg += (na != a0) + (nb != b0);
             sab[m] = na; sab[M + m] = nb;
             scnt[m] = t0; scnt[M + m] = f0; scnt[2 * M + m] = t1; scnt[3 * M + m] = f1;
-            if (want_logl)   /* mcmc_logl term (mcmc.c:643-644) */
-              lbuf[m] = (double)t0 * K.cc + (double)f0 * K.d + (double)t1 * K.dd + (double)f1 * K.c;
+            if (want_logl) {   /* mcmc_logl term (mcmc.c:643-644) */
+              const double lt = (double)t0 * K.cc + (double)f0 * K.d + (double)t1 * K.dd + (double)f1 * K.c;
+              if constexpr (SP) xst(lbuf + m, lt); else lbuf[m] = lt;
+            }
           }
         }
         rng_skip(R, 2 * (mhi - mlo));
@@ -1992,12 +2085,15 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       STAMP(1);
       if (GM && want_logl) {   /* mcmc_logl with the terms in HBM: each wave reads them 64 at a time
                                   (coalesced, 4 chunks in flight) and adds them in m order through readlane */
-        __syncthreads();
+        if constexpr (SP) xsync(); else __syncthreads();
         double s = 0.0;
         for (int c0 = 0; c0 < M; c0 += 256) {
           double v[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) { const int m = c0 + 64 * q + lane; v[q] = (m < M) ? lbuf[m] : 0.0; }
+          for (int q = 0; q < 4; ++q) {
+            const int m = c0 + 64 * q + lane;
+            v[q] = (m < M) ? (SP ? xld(lbuf + m) : lbuf[m]) : 0.0;
+          }
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int n = min(64, M - (c0 + 64 * q));
@@ -2286,10 +2382,10 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           int *pw = part + (bpar * 16) * NWV * 8;
           const bool pack = N < 512;   /* one taxon per thread: per-wave sums fit 16-bit fields */
           /* own taxon's limits and hard-site bits, fixed for the batch (one taxon per thread) */
-          const bool one = NWM > 0 || M <= TXS;   /* register-walk kernels: M <= TB (sr_regwalk) */
+          const bool one = NWM > 0 || SP || M <= TXS;   /* register-walk kernels: M <= TB (sr_regwalk); SP: halves <= TB */
           int a1 = 0, b1 = 0;
           const HM hb1 = hbc;
-          if (one && tx < M) { a1 = sab[tx]; b1 = sab[M + tx]; }
+          if (one && mt < ohi) { a1 = sab[mt]; b1 = sab[M + mt]; }
           FST(13);
 #if defined(SR_STAMP_DRAWS)
           STAMP(5);
@@ -2354,7 +2450,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               if (sI >= p0 && sI < pend && !vetoed(sI)) {
                 const Prop q = load_prop(sI);
                 int dt0 = 0, dt1 = 0;
-                if (tid < M) taxon_dt(prop_kind(sI), q, a1, b1, P + tid, pre + tid, M, hb1, hcnt, nhall, dt0, dt1);
+                if (mt < ohi) taxon_dt(prop_kind(sI), q, a1, b1, P + mt, pre + mt, M, hb1, hcnt, nhall, dt0, dt1);
                 d0s[sI] = dt0; d1s[sI] = dt1;
               }
             }
@@ -2433,6 +2529,18 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           }
           FST(4);
           __syncthreads();
+          if constexpr (SP) {   /* this half's sums of the batch's proposals (lane p of wave 0), exchanged */
+            if (wave == 0 && lane >= p0 && lane < pend && lane < 16 && !((vpk >> 26) & 1)) {
+              int X0 = 0, X1 = 0, Y0 = 0, Y1 = 0;
+              for (int w = 0; w < NWV; ++w) {
+                const int *o = pw + (lane * NWV + w) * 8;
+                X0 += o[0]; X1 += o[1]; Y0 += o[2]; Y1 += o[3];
+              }
+              int *xp = xb + 16 + ((bpar * 2 + half) * 16 + lane) * 4;
+              xst(xp, X0); xst(xp + 1, X1); xst(xp + 2, Y0); xst(xp + 3, Y1);
+            }
+            xsync();
+          }
           STAMP_E(5);
           FST(5);
 
@@ -2457,6 +2565,10 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 for (int w = 0; w < NWV; ++w) {
                   const int *o = pw + (p * NWV + w) * 8;
                   X0 += o[0]; X1 += o[1]; Y0 += o[2]; Y1 += o[3];
+                }
+                if constexpr (SP) {   /* + the other half's */
+                  const int *yp = xb + 16 + ((bpar * 2 + (half ^ 1)) * 16 + p) * 4;
+                  X0 += xld(yp); X1 += xld(yp + 1); Y0 += xld(yp + 2); Y1 += xld(yp + 3);
                 }
                 Sp = ((double)X0 * K.cc - (double)X0 * K.d) + ((double)X1 * K.dd - (double)X1 * K.c);
                 /* PR: o[2] holds Y0 + Y1 (one packed field), o[3] = 0 -- bounded by the larger coefficient */
@@ -2508,9 +2620,9 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               }
             }
             if (!decided || (accept && want_logl && !have_exact)) {   /* the exact sequential delta */
-              dl = sr_exact_delta<PR>(kind, q, K, sab, P, pre, M, KTC, hl, nh, hcnt, nhall, cbuf + xpar * KTC * sr_chunk(PR),
-                                      ccnt + xpar * KTC,
-                                  xs, lane, wave, TB);
+              dl = sr_exact_delta<PR, GM, SP>(kind, q, K, sab, P, pre, M, KTC, olo, ohi, hl, nh, hcnt, nhall,
+                                              cbuf + xpar * KTC * sr_chunk(PR),
+                                              SP ? xb + 272 + xpar * KTC : ccnt + xpar * KTC, xs, lane, wave, TB, xsync);
               xpar ^= 1;
               if (!decided) {
                 if (tid == 0) misc[MS_NEXACT]++;
@@ -2545,7 +2657,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           if (tid == 0) misc[MS_ACC + (kind == PK_PI1 ? 3 : kind == PK_PI2 ? 4 : kind == PK_SWAP ? 5 : 6)]++;
           loglik += delta;
           const int16_t *nhp = nhall + q.r0;   /* pi3: the non-hard positions of [i, j] in order */
-          for (int m = (PR && hf) ? M : tx; m < M; m += TXS) {   /* PR: the even lane of each pair */
+          for (int m = (PR && hf) ? M : olo + tx; m < ohi; m += TXS) {   /* PR: the even lane of each pair; SP: own taxa */
             uint32_t *Pm = P + m;
             const int a = sab[m], b = sab[M + m];
             int dt0, dt1;
@@ -2687,10 +2799,15 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       const int slot = A.rec_base + call;
       const int W = 2 * M + N;
       int16_t *rec = A.rec_abpi + ((size_t)chain * A.rec_cap + slot) * W;
-      for (int m = tid; m < 2 * M; m += TB) rec[m] = (int16_t)sab[m];
+      if constexpr (SP) {   /* own taxa; the permutation and c, d, loglik from half 0 */
+        for (int m = olo + tid; m < ohi; m += TB) { rec[m] = (int16_t)sab[m]; rec[M + m] = (int16_t)sab[M + m]; }
+      } else {
+        for (int m = tid; m < 2 * M; m += TB) rec[m] = (int16_t)sab[m];
+      }
       const int32_t *rc = rcur ? rpiB : rpiA;
-      for (int n = tid; n < N; n += TB) rec[2 * M + rc[n]] = (int16_t)n;
-      if (tid == 0) {
+      if (!SP || half == 0)
+        for (int n = tid; n < N; n += TB) rec[2 * M + rc[n]] = (int16_t)n;
+      if (tid == 0 && (!SP || half == 0)) {
         double *rd = A.rec_cdl + ((size_t)chain * A.rec_cap + slot) * 3;
         rd[0] = c; rd[1] = d; rd[2] = loglik;
       }
@@ -2714,25 +2831,37 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   if (!GM) for (int i = tid; i < NW * M; i += TB) oP[i] = P[i];
   const int32_t *rc = rcur ? rpiB : rpiA;
   int32_t *orpi = A.rpi + (size_t)chain * N;
-  for (int i = tid; i < N; i += TB) orpi[i] = rc[i];
   uint32_t *omt = A.mt + (size_t)chain * SR_RING * SR_MT_N;
-  for (int i = tid; i < SR_RING * SR_MT_N; i += TB) omt[i] = ring[i];
+  if (!SP || half == 0) {   /* SP: block-uniform state, identical in both halves */
+    for (int i = tid; i < N; i += TB) orpi[i] = rc[i];
+    for (int i = tid; i < SR_RING * SR_MT_N; i += TB) omt[i] = ring[i];
+  }
   int32_t *oab = A.ab + (size_t)chain * 2 * M;
   if (!GM) for (int i = tid; i < 2 * M; i += TB) oab[i] = sab[i];
   int32_t *ocnt = A.cnt + (size_t)chain * 4 * M;
   if (!GM) for (int i = tid; i < 4 * M; i += TB) ocnt[i] = scnt[i];
   if (tid == 0) {
-    for (int k = 0; k < nh; ++k) A.hp[(size_t)chain * SR_NHMAX + k] = hp[k];
-    A.cdl[(size_t)chain * 4 + 0] = c;
-    A.cdl[(size_t)chain * 4 + 1] = d;
-    A.cdl[(size_t)chain * 4 + 2] = loglik;
-    A.rng[(size_t)chain * 2 + 0] = (uint64_t)R.blk * SR_MT_N + R.off;
-    A.rng[(size_t)chain * 2 + 1] = R.gen;
-    for (int k = 0; k < 7; ++k) A.acc[(size_t)chain * SR_NACC + k] += misc[MS_ACC + k];
-    A.acc[(size_t)chain * SR_NACC + 2] += misc[MS_CAB];
-    A.acc[(size_t)chain * SR_NACC + 7] += misc[MS_NEXACT];
-    A.acc[(size_t)chain * SR_NACC + 8] += misc[MS_FBK];
-    A.acc[(size_t)chain * SR_NACC + 9] += misc[MS_CDSEQ];
+    uint64_t *acc = A.acc + (size_t)chain * SR_NACC;
+    if (!SP || half == 0) {
+      for (int k = 0; k < nh; ++k) A.hp[(size_t)chain * SR_NHMAX + k] = hp[k];
+      A.cdl[(size_t)chain * 4 + 0] = c;
+      A.cdl[(size_t)chain * 4 + 1] = d;
+      A.cdl[(size_t)chain * 4 + 2] = loglik;
+      A.rng[(size_t)chain * 2 + 0] = (uint64_t)R.blk * SR_MT_N + R.off;
+      A.rng[(size_t)chain * 2 + 1] = R.gen;
+      for (int k = 0; k < 7; ++k)
+        if (k != 2) acc[k] += misc[MS_ACC + k];
+      acc[7] += misc[MS_NEXACT];
+      acc[9] += misc[MS_CDSEQ];
+    }
+    /* the Gibbs counters (a / b changes, exact-walk fallbacks) are per half under SP: atomics */
+    if constexpr (SP) {
+      atomicAdd((unsigned long long *)acc + 2, (unsigned long long)(misc[MS_ACC + 2] + misc[MS_CAB]));
+      atomicAdd((unsigned long long *)acc + 8, (unsigned long long)misc[MS_FBK]);
+    } else {
+      acc[2] += misc[MS_ACC + 2] + misc[MS_CAB];
+      acc[8] += misc[MS_FBK];
+    }
   }
 }
 
@@ -2741,7 +2870,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   fprintf(stderr, "seriation: HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); return -5; } } while (0)
 
 struct srk_dev {
-  int device, N, M, NW, nh, nchains, TB, TPT, rec_cap, gm, pr;
+  int device, N, M, NW, nh, nchains, TB, TPT, rec_cap, gm, pr, sp, grid;
   size_t lds;
   hipStream_t stream;
   int own_stream;
@@ -2770,9 +2899,14 @@ static bool sr_pair_ok(int N, int M)
   return sr_nwm(N) == 9 && M > 256 && M <= 512;
 }
 
-static sr_kfn sr_pick_kernel(int TB, int N, int M, bool gm, bool pr, int nh)
+static sr_kfn sr_pick_kernel(int TB, int N, int M, bool gm, bool pr, int nh, bool sp = false)
 {
   if (pr) return (TB == 1024 && !gm) ? (sr_kfn)sr_sweep_kernel<1024, 9, false, true> : nullptr;
+#ifndef SR_STAMPS
+  if (sp) return (TB == 1024 && gm) ? (sr_kfn)sr_sweep_kernel<1024, 0, true, false, true> : nullptr;
+#else
+  if (sp) return nullptr;   /* (stamp builds index their counters by block) */
+#endif
 #ifdef SR_PAIR_ONLY   /* register-pressure experiments: compile the pair kernel alone */
   return nullptr;
 #endif
@@ -2835,6 +2969,29 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
   if (d->gm) d->pr = 0;
   d->lds = L.total;
   if (!sr_pick_kernel(TB, st->N, st->M, d->gm != 0, d->pr != 0, st->nh) || d->lds > 160 * 1024) { delete d; return -6; }
+  /* split chains (two co-resident workgroups per chain, one taxon per thread): HBM columns at 1024
+     threads when the taxa exceed one block but each half fits it, and the whole grid (16 blocks per
+     8 chains) is co-resident -- launched cooperatively.  SR_SPLIT=0 disables it, SR_SPLIT=1 also
+     splits chains of <= 1024 taxa (tests). */
+  d->sp = 0; d->grid = st->nchains;
+  {
+    const char *e = getenv("SR_SPLIT");
+    const int want = e ? atoi(e) : -1;
+    const int Mh = sr_sp_half(st->M);
+    sr_kfn ks = sr_pick_kernel(TB, st->N, st->M, true, false, st->nh, true);
+    if (want != 0 && d->gm && ks && Mh <= TB && st->M > 128 && (st->M > TB || want == 1)) {
+      int cus = 0, occ = 0, coop = 0;
+      const int grid = 16 * ((st->nchains + 7) / 8);
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+          hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device) == hipSuccess && coop &&
+          hipFuncSetAttribute((const void *)ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d->lds) == hipSuccess &&
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)ks, TB, d->lds) == hipSuccess &&
+          grid <= occ * cus) {
+        d->sp = 1;
+        d->grid = grid;
+      }
+    }
+  }
   d->rec_cap = rec_cap_calls > 0 ? rec_cap_calls : 1;
   const size_t C = st->nchains;
   KArgs &A = d->args;
@@ -2856,12 +3013,17 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
   if (pkey) rc |= dev_alloc_copy(d, &A.pkey, pkey, C * 2);
   if (d->gm) {
     rc |= dev_alloc_copy(d, &A.gpre, (const uint16_t *)nullptr, C * sr_gm_pre(st->M, st->NW));
-    rc |= dev_alloc_copy(d, &A.gck, (const double *)nullptr, C * sr_gm_ck(st->N, st->M, TB));
+    rc |= dev_alloc_copy(d, &A.gck, (const double *)nullptr, C * (d->sp ? sr_sp_ck(st->N, TB) : sr_gm_ck(st->N, st->M, TB)));
     rc |= dev_alloc_copy(d, &A.glbuf, (const double *)nullptr, C * st->M);
     rc |= dev_alloc_copy(d, &A.gcbuf, (const double *)nullptr, C * sr_gm_cbuf(st->M));
   }
+  if (d->sp) {
+    rc |= dev_alloc_copy(d, &A.xflag, (const int *)nullptr, C * 2);
+    rc |= dev_alloc_copy(d, &A.xbuf, (const int *)nullptr, C * sr_sp_xb(st->M));
+    rc |= dev_alloc_copy(d, &A.xerr, (const int *)nullptr, 1);
+  }
   if (rc) { srk_destroy(d); return -5; }
-  sr_kfn k = sr_pick_kernel(TB, st->N, st->M, d->gm != 0, d->pr != 0, st->nh);
+  sr_kfn k = sr_pick_kernel(TB, st->N, st->M, d->gm != 0, d->pr != 0, st->nh, d->sp != 0);
   if (hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d->lds) != hipSuccess) {
     srk_destroy(d);
     return -5;
@@ -2891,11 +3053,27 @@ extern "C" int srk_run(srk_dev *d, int calls, int spc, int save, int rec_base)
   HIPCHK(hipSetDevice(d->device));
   KArgs A = d->args;
   A.calls = calls; A.spc = spc; A.save = save; A.rec_base = rec_base;
-  sr_kfn k = sr_pick_kernel(d->TB, d->N, d->M, d->gm != 0, d->pr != 0, d->nh);
+  sr_kfn k = sr_pick_kernel(d->TB, d->N, d->M, d->gm != 0, d->pr != 0, d->nh, d->sp != 0);
+  if (d->sp) HIPCHK(hipMemsetAsync(A.xflag, 0, (size_t)d->nchains * 2 * sizeof(int), d->stream));   /* exchange sequence restarts */
   if (d->have_events) HIPCHK(hipEventRecord(d->ev0, d->stream));
-  hipLaunchKernelGGL(k, dim3(d->nchains), dim3(d->TB), d->lds, d->stream, A);
+  if (d->sp) {   /* both halves of every chain must be resident together */
+    void *kargs[] = {&A};
+    HIPCHK(hipLaunchCooperativeKernel((const void *)k, dim3(d->grid), dim3(d->TB), kargs, (unsigned)d->lds, d->stream));
+  } else {
+    hipLaunchKernelGGL(k, dim3(d->nchains), dim3(d->TB), d->lds, d->stream, A);
+  }
   HIPCHK(hipGetLastError());
   if (d->have_events) HIPCHK(hipEventRecord(d->ev1, d->stream));
+  return 0;
+}
+
+/* split chains: a half that waited past its deadline (the other half not resident) left garbage */
+static int sp_check(srk_dev *d)
+{
+  if (!d->sp) return 0;
+  int e = 0;
+  HIPCHK(hipMemcpy(&e, d->args.xerr, sizeof(int), hipMemcpyDeviceToHost));
+  if (e) { fprintf(stderr, "seriation: split-chain exchange timed out (halves not co-resident)\n"); return -5; }
   return 0;
 }
 
@@ -2903,7 +3081,7 @@ extern "C" int srk_sync(srk_dev *d)
 {
   HIPCHK(hipSetDevice(d->device));
   HIPCHK(hipStreamSynchronize(d->stream));
-  return 0;
+  return sp_check(d);
 }
 
 extern "C" double srk_last_ms(srk_dev *d)
@@ -2916,7 +3094,7 @@ extern "C" double srk_last_ms(srk_dev *d)
 }
 
 extern "C" int srk_block_threads(const srk_dev *d) { return d->TB; }
-extern "C" int srk_variant(const srk_dev *d) { return d->gm ? 1 : (d->pr ? 2 : 0); }
+extern "C" int srk_variant(const srk_dev *d) { return d->gm ? (d->sp ? 3 : 1) : (d->pr ? 2 : 0); }
 
 extern "C" int srk_fetch_dbg(srk_dev *d, unsigned long long *out)
 {
@@ -2931,6 +3109,7 @@ extern "C" int srk_fetch_records(srk_dev *d, int first, int count, int16_t *ab_p
   if (first < 0 || count < 0 || first + count > d->rec_cap) return -1;
   HIPCHK(hipSetDevice(d->device));
   HIPCHK(hipStreamSynchronize(d->stream));
+  if (int e = sp_check(d)) return e;
   if (count == 0) return 0;
   const size_t W = 2 * (size_t)d->M + d->N;
   /* chain c's rows [first, first + count) of its rec_cap-row slab; one copy when they are the whole slab */
@@ -2953,6 +3132,7 @@ extern "C" int srk_fetch_chain_records(srk_dev *d, int chain, int first, int cou
   if (chain < 0 || chain >= d->nchains || first < 0 || count < 0 || first + count > d->rec_cap) return -1;
   HIPCHK(hipSetDevice(d->device));
   HIPCHK(hipStreamSynchronize(d->stream));
+  if (int e = sp_check(d)) return e;
   if (count == 0) return 0;
   const size_t W = 2 * (size_t)d->M + d->N, row = (size_t)chain * d->rec_cap + first;
   if (ab_pi) HIPCHK(hipMemcpy(ab_pi, d->args.rec_abpi + row * W, (size_t)count * W * sizeof(int16_t), hipMemcpyDeviceToHost));
@@ -3011,6 +3191,7 @@ extern "C" int srk_run_pipelined(srk_dev *d, int total_calls, int cpl, int spc,
     else if (consume(ctx, first[p], cnt[p], hab[p], hcd[p])) rc = -1;
   }
   (void)hipStreamSynchronize(d->stream);
+  if (!rc) rc = sp_check(d);
   for (int h = 0; h < 2; ++h) {
     if (hab[h]) (void)hipHostFree(hab[h]);
     if (hcd[h]) (void)hipHostFree(hcd[h]);
@@ -3023,6 +3204,7 @@ extern "C" int srk_records_device(srk_dev *d, const int16_t **rec, int *rec_cap,
 {
   HIPCHK(hipSetDevice(d->device));
   HIPCHK(hipStreamSynchronize(d->stream));
+  if (int e = sp_check(d)) return e;
   *rec = d->args.rec_abpi;
   *rec_cap = d->rec_cap;
   *device = d->device;
@@ -3034,6 +3216,7 @@ extern "C" int srk_download_state(srk_dev *d, sr_state_host *st)
 {
   HIPCHK(hipSetDevice(d->device));
   HIPCHK(hipStreamSynchronize(d->stream));
+  if (int e = sp_check(d)) return e;
   const size_t C = d->nchains;
   const KArgs &A = d->args;
   if (st->P) HIPCHK(hipMemcpy(st->P, A.P, C * d->NW * d->M * 4, hipMemcpyDeviceToHost));

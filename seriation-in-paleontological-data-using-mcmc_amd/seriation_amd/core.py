@@ -155,12 +155,13 @@ class Session:
     @property
     def variant(self):
         """Kernel variant: "lds" (occurrence columns in LDS) or "hbm" (columns in HBM)."""
-        return "hbm" if L.lib().sr_session_variant(self.h) == 1 else "lds"
+        return "hbm" if L.lib().sr_session_variant(self.h) in (1, 3) else "lds"
 
     @property
     def kernel(self):
-        """"pair" (two lanes per taxon) or "single" (one thread per taxon)."""
-        return "pair" if L.lib().sr_session_variant(self.h) == 2 else "single"
+        """"pair" (two lanes per taxon), "split" (HBM columns, two workgroups per chain) or "single"
+        (one workgroup per chain, one thread per taxon or several)."""
+        return {2: "pair", 3: "split"}.get(L.lib().sr_session_variant(self.h), "single")
 
     def set_stream(self, stream_handle):
         _check(L.lib().sr_session_set_stream(self.h, ctypes.c_void_p(stream_handle)), "set_stream")

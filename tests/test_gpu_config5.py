@@ -24,7 +24,7 @@ def test_config5_variant_is_hbm(config5):
     ds = sa.Dataset.parse(config5, maxs=0)
     assert (ds.N, ds.M) == (1024, 2048)
     with sa.Session(ds, [1]) as s:
-        assert s.variant == "hbm"
+        assert s.variant == "hbm" and s.kernel == "split"   # two workgroups per chain, 1024 taxa each
     with pytest.raises(sa.SrError):
         sa.Session(ds, [1], columns="lds")
 
@@ -48,3 +48,26 @@ def test_config5_parity(config5):
         np.testing.assert_array_equal(ri[k], oi, err_msg="seed %d" % s)
         assert np.array_equal(rd[k].view(np.uint64), od.view(np.uint64)), s
         assert summ[k]["consistent"] == 0
+
+
+def test_config5_parity_one_workgroup(config5, monkeypatch):
+    """The one-workgroup HBM-column kernel (two taxa per thread; what more than 128 chains per GPU
+    run) on the same data: 8 chains x (1 + 10) calls against the oracle."""
+    from concurrent.futures import ThreadPoolExecutor
+    monkeypatch.setenv("SR_SPLIT", "0")
+    ds = sa.Dataset.parse(config5, maxs=0)
+    seeds = [11, 12, 13, 14, 15, 16, 17, 18]
+    with sa.Session(ds, seeds[:1]) as s:
+        assert s.kernel == "single"
+    summ, (ri, rd) = sa.run_chains(ds, seeds, burnin_calls=1, sample_calls=10, keep_records=True)
+
+    def one(s):
+        o = oracle_ref.run_chain(config5, s, 1, 10, maxs=0)
+        return o["rc"], o["rec_int"].copy(), o["rec_dbl"].copy()
+
+    with ThreadPoolExecutor(8) as ex:
+        ref = list(ex.map(one, seeds))
+    for k, (s, (rc, oi, od)) in enumerate(zip(seeds, ref)):
+        assert rc == 0
+        np.testing.assert_array_equal(ri[k], oi, err_msg="seed %d" % s)
+        assert np.array_equal(rd[k].view(np.uint64), od.view(np.uint64)), s

@@ -115,6 +115,39 @@ def test_steep_walks(N, M, noise, seeds, burnin):
         assert 32 * ((N >> 5) + 1) * abs(np.log2(d / (1 - c))) > 650, (c, d)
 
 
+# Split chains (two workgroups per chain exchanging sums through HBM flags), forced on small HBM-column
+# cases at 1024 threads (SR_SPLIT=1; by default only chains of 1025..2048 taxa split).
+SPLIT_CASES = [("m700", 64, 700, 4), ("m1100", 64, 1100, 6), ("nh64", 150, 1200, 64), ("lds-walk", 600, 1300, 7),
+               ("many-hard", 60, 1500, 30)]
+
+
+@pytest.mark.parametrize("name,N,M,nh", SPLIT_CASES, ids=["split-" + c[0] for c in SPLIT_CASES])
+def test_split_chain_parity(monkeypatch, name, N, M, nh):
+    monkeypatch.setenv("SR_SPLIT", "1")
+    text = make_text(N, M, nh, seed=N * 1000 + M)
+    ds = sa.Dataset.parse(text, maxs=0)
+    seeds = [5, 13, 21]
+    with sa.Session(ds, seeds, block_threads=1024, columns="hbm") as s:
+        assert s.variant == "hbm" and s.kernel == "split"
+    summ, (ri, rd) = sa.run_chains(ds, seeds, burnin_calls=2, sample_calls=3, keep_records=True, block_threads=1024,
+                                   columns="hbm")
+    for k, s in enumerate(seeds):
+        o = oracle_ref.run_chain(text, s, 2, 3, maxs=0)
+        assert o["rc"] == 0
+        np.testing.assert_array_equal(ri[k], o["rec_int"], err_msg="%s seed %d" % (name, s))
+        assert np.array_equal(rd[k].view(np.uint64), o["rec_dbl"].view(np.uint64)), (name, s)
+        assert summ[k]["consistent"] == 0
+    # the per-half counters (a / b changes, exact-walk fallbacks) add up to the one-workgroup kernel's
+    counts = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("SR_SPLIT", mode)
+        with sa.Session(ds, seeds, block_threads=1024, columns="hbm") as s:
+            assert s.kernel == ("split" if mode == "1" else "single")
+            s.run(5)
+            counts[mode] = [np.concatenate([s.accept_counts(k), s.fallback_counts(k)]) for k in range(len(seeds))]
+    np.testing.assert_array_equal(np.array(counts["1"]), np.array(counts["0"]))
+
+
 def test_checkpoint_resume_continues_exactly(tmp_path):
     """sr_session_checkpoint after 10 calls + sr_session_restore + 20 calls == 30 calls straight."""
     import os

@@ -22,7 +22,7 @@ path = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "tests/golden/da
 C = int(sys.argv[2]) if len(sys.argv) > 2 else 100
 calls = int(sys.argv[3]) if len(sys.argv) > 3 else 10
 tbk = int(sys.argv[4]) if len(sys.argv) > 4 else 0
-ds = sa.Dataset.load(path)
+ds = sa.Dataset.load(path, maxs=0)   # full lines (the bench loads synthetic data the same way)
 s = sa.Session(ds, list(range(1, C + 1)), calls_per_launch=calls, block_threads=tbk)
 s.run(calls)
 s.sync()

@@ -285,7 +285,8 @@ def main():
     # HBM-column variant (columns too large for LDS, config 5) re-reads its columns from L2 / HBM
     limiter = dict(prof.get("limiter") or {})
     limiter["bound"] = ("issue / latency (working set in LDS; HBM carries only chain state and records)"
-                        if sess.variant == "lds" else "HBM / L2 (occurrence columns re-read from HBM every sweep)")
+                        if sess.variant == "lds" else "L2 / MALL latency of the occurrence-column reads (columns in HBM, "
+                        "re-read every sweep; HBM bandwidth far from peak)")
     limiter["source"] = traffic_src
     out = {
         "metric": "chain-iterations/sec (100 chains, 256x512 matrix) at 1/2/4/8 MI355X",
@@ -310,6 +311,7 @@ def main():
                            ds.N, ds.M, C, cps, sweeps_per_step),
             "sites": ds.N, "taxa": ds.M, "chains": total_chains, "chains_per_gpu": C,
             "sweeps_per_step": sweeps_per_step, "block_threads": sess.block_threads, "columns": sess.variant,
+            "kernel": sess.kernel,   # "split": two workgroups per chain (HBM columns)
             "rng": "GSL MT19937 (the reference's stream)" if args.rng == "mt" else "Philox4x32-10 (opt-in)",
             "parallelism": "chains sharded over %d GPU(s), RCCL all-gather at end" % world,
         },

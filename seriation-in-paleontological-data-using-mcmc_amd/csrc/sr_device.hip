@@ -2620,9 +2620,14 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               }
             }
             if (!decided || (accept && want_logl && !have_exact)) {   /* the exact sequential delta */
-              dl = sr_exact_delta<PR, GM, SP>(kind, q, K, sab, P, pre, M, KTC, olo, ohi, hl, nh, hcnt, nhall,
-                                              cbuf + xpar * KTC * sr_chunk(PR),
-                                              SP ? xb + 272 + xpar * KTC : ccnt + xpar * KTC, xs, lane, wave, TB, xsync);
+              if constexpr (SP)
+                dl = sr_exact_delta<PR, GM, SP>(kind, q, K, sab, P, pre, M, KTC, olo, ohi, hl, nh, hcnt, nhall,
+                                                cbuf + xpar * KTC * sr_chunk(PR), xb + 272 + xpar * KTC, xs, lane, wave,
+                                                TB, xsync);
+              else   /* (no exchange: the one-workgroup kernels never see the split machinery) */
+                dl = sr_exact_delta<PR, GM, SP>(kind, q, K, sab, P, pre, M, KTC, 0, M, hl, nh, hcnt, nhall,
+                                                cbuf + xpar * KTC * sr_chunk(PR), ccnt + xpar * KTC, xs, lane, wave, TB,
+                                                [] {});
               xpar ^= 1;
               if (!decided) {
                 if (tid == 0) misc[MS_NEXACT]++;
@@ -2870,7 +2875,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   fprintf(stderr, "seriation: HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); return -5; } } while (0)
 
 struct srk_dev {
-  int device, N, M, NW, nh, nchains, TB, TPT, rec_cap, gm, pr, sp, grid;
+  int device, N, M, NW, nh, nchains, TB, TPT, rec_cap, gm, pr, sp, grid, coop;
   size_t lds;
   hipStream_t stream;
   int own_stream;
@@ -2989,6 +2994,11 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
           grid <= occ * cus) {
         d->sp = 1;
         d->grid = grid;
+        /* SR_COOP=0: an ordinary launch of the same grid (rocprofv3's kernel tracer crashes at
+           process exit after cooperative launches; on an otherwise idle GPU the grid is resident
+           anyway, and a wait that times out fails the session instead of hanging) */
+        const char *ce = getenv("SR_COOP");
+        d->coop = (ce && atoi(ce) == 0) ? 0 : 1;
       }
     }
   }
@@ -3056,9 +3066,11 @@ extern "C" int srk_run(srk_dev *d, int calls, int spc, int save, int rec_base)
   sr_kfn k = sr_pick_kernel(d->TB, d->N, d->M, d->gm != 0, d->pr != 0, d->nh, d->sp != 0);
   if (d->sp) HIPCHK(hipMemsetAsync(A.xflag, 0, (size_t)d->nchains * 2 * sizeof(int), d->stream));   /* exchange sequence restarts */
   if (d->have_events) HIPCHK(hipEventRecord(d->ev0, d->stream));
-  if (d->sp) {   /* both halves of every chain must be resident together */
+  if (d->sp && d->coop) {   /* both halves of every chain must be resident together */
     void *kargs[] = {&A};
     HIPCHK(hipLaunchCooperativeKernel((const void *)k, dim3(d->grid), dim3(d->TB), kargs, (unsigned)d->lds, d->stream));
+  } else if (d->sp) {
+    hipLaunchKernelGGL(k, dim3(d->grid), dim3(d->TB), d->lds, d->stream, A);
   } else {
     hipLaunchKernelGGL(k, dim3(d->nchains), dim3(d->TB), d->lds, d->stream, A);
   }

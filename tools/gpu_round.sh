@@ -26,7 +26,7 @@ timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o w -- python3 $P > "$OUT/pmc_write.log" 2>&1 &&
 timeout -s KILL 180 rocprofv3 --pmc $SQA --output-format csv -d "$OUT/pmc_sq" -o s -- python3 $P > "$OUT/pmc_sq.log" 2>&1 &&
 timeout -s KILL 180 rocprofv3 --pmc $SQB --output-format csv -d "$OUT/pmc_sq_b" -o s -- python3 $P > "$OUT/pmc_sq_b.log" 2>&1 &&
-timeout -k 10 200 python $C5 > "$OUT/c5_bench.json" 2> "$OUT/c5_bench.err" &&
+timeout -k 10 200 python $C5 > "$OUT/c5_bench.json" 2> "$OUT/c5_bench.err" && export SR_COOP=0 &&   # (rocprofv3 + cooperative launch: see tools/gpu_c5_round.sh)
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c5_prof" -o c5 -- python3 $C5 > "$OUT/c5_prof.log" 2>&1 &&
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/c5_fetch" -o f -- python3 $C5 > "$OUT/c5_fetch.log" 2>&1 &&
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/c5_write" -o w -- python3 $C5 > "$OUT/c5_write.log" 2>&1 &&

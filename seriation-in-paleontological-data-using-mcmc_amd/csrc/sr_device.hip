@@ -695,7 +695,7 @@ __device__ __forceinline__ double exp2_split(double q)
   return __builtin_amdgcn_ldexp((double)y, (int)n);
 }
 
-#define SR_WIN_T 40.0        /* words whose q stays 40 bits below q(o) are skipped (mass <= 2^-40 each entry) */
+#define SR_WIN_T 40.0       /* words whose q stays 40 bits below q(o) are skipped (mass <= 2^-40 each entry) */
 
 /* mcmc_auxa + mcmc_logtop + mcmc_randompick for one limit of one taxon (exact version:
  * draw_exact), certified fast path.  The picked index depends only on where u falls in the
@@ -957,6 +957,104 @@ __device__ __forceinline__ int walk_prefix_s(const uint32_t (&wk)[NWM], int w)
   return s;
 }
 
+/* count deltas at the pick (the dt arrays of mcmc_auxa): POo, POp = ones among walk entries [0, o), [0, res) */
+__device__ __forceinline__ void pick_counts(int res, int o, int POo, int POp, int &dt0, int &df0, int &dt1, int &df1)
+{
+  if (res == o) { dt0 = df0 = dt1 = df1 = 0; }
+  else if (res < o) { int O = POo - POp; int Z = (o - res) - O; dt0 = -Z; df0 = Z; dt1 = O; df1 = -O; }
+  else { int O = POp - POo; int Z = (res - o) - O; dt0 = Z; df0 = -Z; dt1 = -O; df1 = O; }
+}
+
+/* pass 2 of a register walk (draw_fast_s): locate the word, then the byte, nibble and
+ * entry where u falls (the searches compare against u S), and certify the pick; -1 when it is not
+ * certified (the caller runs the exact walk).  ckr / yst: S after and y at the start of each word
+ * (0 / y0 before the window, unchanged after it), S the walk's total over entries [0, L]. */
+template <int NWM>
+__device__ __forceinline__ int walk_pick_s(const uint32_t (&wk)[NWM], const double (&ckr)[NWM], const double (&yst)[NWM],
+                                           double S, int klo, int khi, int L, int N, double u, const double *T4,
+                                           const double *T8, int &POp)
+{
+  int res = -1;
+  {
+    const double inv = 1.0 / S;
+    const double REL = (double)(N + 33) * 0x1p-50;   /* + the byte tables' own rounding (<= 16 ulp per entry) */
+    const double ABS = (double)(N + 1) * 0x1p-39;
+    /* the words before the window hold S = 0 (< u S), so counting k < khi finds the word */
+    const double uS = u * S;
+    int j = 0;
+#pragma unroll
+    for (int k = 0; k < NWM; ++k) j += (k < khi && ckr[k] < uS) ? 1 : 0;
+    j = max(j, klo);   /* (u = 0) */
+    double Sp0 = 0.0, y = yst[0];
+    uint32_t ww = wk[0];
+    [[maybe_unused]] int Oj = 0, Ok = 0;   /* ones among walk entries [0, 32 j) (9-word walks) */
+#pragma unroll
+    for (int k = 0; k < NWM; ++k) {
+      if (k == j) { y = yst[k]; ww = wk[k]; Oj = Ok; }
+      if (k + 1 == j) Sp0 = ckr[k];   /* ckr[klo - 1] = 0 */
+      if constexpr (NWM <= 9) Ok += __popc(wk[k]);
+    }
+    const int w0 = 32 * j;
+    const int nb = min(32, L + 1 - w0);   /* walk entries in word j */
+    /* byte level: the word's whole bytes from the 8-entry tables (the walk's partial last byte,
+       if any, is the last candidate: its end is S itself); then the nibble, then the entry */
+    const int nfb = nb >> 3, nlb = (nb + 7) >> 3;
+    double2 tb8[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) tb8[g] = *reinterpret_cast<const double2 *>(T8 + 2 * ((ww >> (8 * g)) & 255u));
+    double Bg[4], Yg[4];
+    int nbc = 0;
+    {
+      double acc = Sp0, yy = y;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        Yg[g] = yy;
+        acc = __builtin_fma(yy, tb8[g].x, acc);
+        Bg[g] = acc;
+        yy = yy * tb8[g].y;
+        nbc += (g < nfb && acc < uS) ? 1 : 0;
+      }
+    }
+    const int bsel = min(nbc, nlb - 1);
+    double base_b = Sp0, y_b = y;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      if (g == bsel) y_b = Yg[g];
+      if (g + 1 == bsel) base_b = Bg[g];
+    }
+    const uint32_t bv = (ww >> (8 * bsel)) & 255u;
+    const int ce = min(nb - 8 * bsel, 8), c_lo = min(ce, 4), c_hi = ce - c_lo;
+    const double2 tlo = t4sp(T4, c_lo, bv & 15u);
+    const double N0 = __builtin_fma(y_b, tlo.x, base_b);
+    const bool nsel = c_hi > 0 && N0 < uS;
+    const int gsel = 2 * bsel + (nsel ? 1 : 0);
+    const double base = nsel ? N0 : base_b, ys = nsel ? y_b * tlo.y : y_b;
+    const uint32_t nibs = nsel ? (bv >> 4) : (bv & 15u);
+    const int cmax = nsel ? c_hi : c_lo;
+    const double P1 = __builtin_fma(ys, t4s(T4, 1, nibs), base), P2 = __builtin_fma(ys, t4s(T4, 2, nibs), base);
+    const double P3 = __builtin_fma(ys, t4s(T4, 3, nibs), base), P4 = __builtin_fma(ys, t4s(T4, 4, nibs), base);
+    const int nc = ((cmax > 1 && P1 < uS) ? 1 : 0) + ((cmax > 2 && P2 < uS) ? 1 : 0) + ((cmax > 3 && P3 < uS) ? 1 : 0);
+    const double Ph = (nc == 0) ? P1 : (nc == 1) ? P2 : (nc == 2) ? P3 : P4;
+    const double Pp = (nc == 0) ? base : (nc == 1) ? P1 : (nc == 2) ? P2 : P3;
+    const int w = w0 + 4 * gsel + nc;
+    const double t = u - Ph * inv, tprev = u - Pp * inv;
+    const double e = 2.0 * REL * fmin(Ph, S - Ph) * inv + ABS;
+    const double eprev = 2.0 * REL * fmin(Pp, S - Pp) * inv + ABS;
+    const bool prev_ok = (w == 0) || (tprev > eprev);
+    const bool here_ok = (w == L) || (t < -e);
+#ifndef SR_FORCE_EXACT
+    if (prev_ok && here_ok) {
+      res = w;
+      if constexpr (NWM <= 9) POp = Oj + __popc(ww & ((1u << (w & 31)) - 1u));
+      else POp = walk_prefix_s<NWM>(wk, res);   /* (the tracked form spills in the 17-word kernel) */
+    }
+#else   /* test build: every Gibbs draw takes the exact three-pass walk */
+    (void)prev_ok; (void)here_ok; (void)w;
+#endif
+  }
+  return res;
+}
+
 /* draw_fast with the walk words in registers, fully unrolled and branch-free (the measured cost
  * of a loop trip with a taken branch on gfx950 is ~36 cycles, more than the work it guards).
  * Same approximation and certification as draw_fast; fallback to draw_exact on failure. */
@@ -1089,94 +1187,16 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
      2 % of the 9-word kernel, profiles/r03n_ab_yguard.json). */
   bool yok = true;
   if constexpr (NWM > 9) yok = klo > khi || (lowm & ((2u << khi) - 1u) & ~((1u << klo) - 1u)) == 0u;
-  if (S > 0.0 && S < 0x1p1000 && yok) {
-    const double inv = 1.0 / S;
-    const double REL = (double)(N + 33) * 0x1p-50;   /* + the byte tables' own rounding (<= 16 ulp per entry) */
-    const double ABS = (double)(N + 1) * 0x1p-39;
-    /* the words before the window hold S = 0 (< u S), so counting k < khi finds the word */
-    const double uS = u * S;
-    int j = 0;
-#pragma unroll
-    for (int k = 0; k < NWM; ++k) j += (k < khi && ckr[k] < uS) ? 1 : 0;
-    j = max(j, klo);   /* (u = 0) */
-    double Sp0 = 0.0, y = yst[0];
-    uint32_t ww = wk[0];
-    [[maybe_unused]] int Oj = 0, Ok = 0;   /* ones among walk entries [0, 32 j) (9-word walks) */
-#pragma unroll
-    for (int k = 0; k < NWM; ++k) {
-      if (k == j) { y = yst[k]; ww = wk[k]; Oj = Ok; }
-      if (k + 1 == j) Sp0 = ckr[k];   /* ckr[klo - 1] = 0 */
-      if constexpr (NWM <= 9) Ok += __popc(wk[k]);
-    }
-    const int w0 = 32 * j;
-    const int nb = min(32, L + 1 - w0);   /* walk entries in word j */
-    /* byte level: the word's whole bytes from the 8-entry tables (the walk's partial last byte,
-       if any, is the last candidate: its end is S itself); then the nibble, then the entry */
-    const int nfb = nb >> 3, nlb = (nb + 7) >> 3;
-    double2 tb8[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) tb8[g] = *reinterpret_cast<const double2 *>(T8 + 2 * ((ww >> (8 * g)) & 255u));
-    double Bg[4], Yg[4];
-    int nbc = 0;
-    {
-      double acc = Sp0, yy = y;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        Yg[g] = yy;
-        acc = __builtin_fma(yy, tb8[g].x, acc);
-        Bg[g] = acc;
-        yy = yy * tb8[g].y;
-        nbc += (g < nfb && acc < uS) ? 1 : 0;
-      }
-    }
-    const int bsel = min(nbc, nlb - 1);
-    double base_b = Sp0, y_b = y;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      if (g == bsel) y_b = Yg[g];
-      if (g + 1 == bsel) base_b = Bg[g];
-    }
-    const uint32_t bv = (ww >> (8 * bsel)) & 255u;
-    const int ce = min(nb - 8 * bsel, 8), c_lo = min(ce, 4), c_hi = ce - c_lo;
-    const double2 tlo = t4sp(T4, c_lo, bv & 15u);
-    const double N0 = __builtin_fma(y_b, tlo.x, base_b);
-    const bool nsel = c_hi > 0 && N0 < uS;
-    const int gsel = 2 * bsel + (nsel ? 1 : 0);
-    const double base = nsel ? N0 : base_b, ys = nsel ? y_b * tlo.y : y_b;
-    const uint32_t nibs = nsel ? (bv >> 4) : (bv & 15u);
-    const int cmax = nsel ? c_hi : c_lo;
-    const double P1 = __builtin_fma(ys, t4s(T4, 1, nibs), base), P2 = __builtin_fma(ys, t4s(T4, 2, nibs), base);
-    const double P3 = __builtin_fma(ys, t4s(T4, 3, nibs), base), P4 = __builtin_fma(ys, t4s(T4, 4, nibs), base);
-    const int nc = ((cmax > 1 && P1 < uS) ? 1 : 0) + ((cmax > 2 && P2 < uS) ? 1 : 0) + ((cmax > 3 && P3 < uS) ? 1 : 0);
-    const double Ph = (nc == 0) ? P1 : (nc == 1) ? P2 : (nc == 2) ? P3 : P4;
-    const double Pp = (nc == 0) ? base : (nc == 1) ? P1 : (nc == 2) ? P2 : P3;
-    const int w = w0 + 4 * gsel + nc;
-    const double t = u - Ph * inv, tprev = u - Pp * inv;
-    const double e = 2.0 * REL * fmin(Ph, S - Ph) * inv + ABS;
-    const double eprev = 2.0 * REL * fmin(Pp, S - Pp) * inv + ABS;
-    const bool prev_ok = (w == 0) || (tprev > eprev);
-    const bool here_ok = (w == L) || (t < -e);
-#ifndef SR_FORCE_EXACT
-    if (prev_ok && here_ok) {
-      res = w;
-      if constexpr (NWM <= 9) POp = Oj + __popc(ww & ((1u << (w & 31)) - 1u));
-      else POp = walk_prefix_s<NWM>(wk, res);   /* (the tracked form spills in the 17-word kernel) */
-    }
-#else   /* test build: every Gibbs draw takes the exact three-pass walk */
-    (void)prev_ok; (void)here_ok; (void)w;
-#endif
-  }
+  if (S > 0.0 && S < 0x1p1000 && yok) res = walk_pick_s<NWM>(wk, ckr, yst, S, klo, khi, L, N, u, T4, T8, POp);
   if (res < 0) {
     atomicAdd((unsigned long long *)fbk, 1ull);   /* exact-walk fallbacks (rare: counted always) */
     res = draw_exact(Pm, M, N, rev, o, L, u, K, tb);
     POp = walk_prefix_s<NWM>(wk, res);
   }
-  /* count deltas at the pick (the dt arrays of mcmc_auxa) */
-  if (res == o) { dt0 = df0 = dt1 = df1 = 0; }
-  else if (res < o) { int O = POo - POp; int Z = (o - res) - O; dt0 = -Z; df0 = Z; dt1 = O; df1 = -O; }
-  else { int O = POp - POo; int Z = (res - o) - O; dt0 = Z; df0 = -Z; dt1 = -O; df1 = O; }
+  pick_counts(res, o, POo, POp, dt0, df0, dt1, df1);
   return res;
 }
+
 
 /* ---- pair kernels: two lanes per taxon ---------------------------------------------------
  * Lanes 2t and 2t+1 of a wave share taxon t; the even lane ("lo") holds walk words 0..4 of a

@@ -648,6 +648,15 @@ __device__ __noinline__ int draw_exact(const uint32_t *Pm, int M, int N, bool re
 }
 
 
+/* ones of column m at positions [0, x) from the per-word prefix table (pre: column m's entries,
+ * stride M; row k = ones in [0, 32k)) and one partial word */
+__device__ __forceinline__ int col_pre(const uint16_t *prem, const uint32_t *Pm, int M, int x)
+{
+  const int w = x >> 5, bits = x & 31;
+  const uint32_t word = bits ? Pm[w * M] : 0u;
+  return (int)prem[w * M] + __popc(word & ((1u << bits) - 1u));
+}
+
 /* 32 walk bits [32k, 32k+32): fwd = positions, rev = positions N-1-w (bit i = walk 32k+i) */
 __device__ __forceinline__ uint32_t walk_word(const uint32_t *Pm, int M, int N, int NW, bool rev, int k)
 {
@@ -719,8 +728,8 @@ __device__ __forceinline__ double exp2_split(double q)
 #define SR_WCH 8   /* walk words read together: one memory round trip per 8 words (HBM columns: L2 / MALL latency) */
 #endif
 #define SR_QSPAN 600.0   /* window trim below the largest word-start q (log2 units), draw_fast */
-__device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int NW, bool rev, int o, int L, int POo, double u,
-                                         const CD &K, const sr_mtab &tb, double vA, double vB, double rA, double rB,
+__device__ __forceinline__ int draw_fast(const uint32_t *Pm, const uint16_t *prem, int M, int N, int NW, bool rev, int o, int L,
+                                         int POo, double u, const CD &K, const sr_mtab &tb, double vA, double vB, double rA, double rB,
                                          const double *T4, double *ck, int ckstride, uint64_t *fbk, int &dt0, int &df0,
                                          int &dt1, int &df1 GSTAMP_ARGS)
 {
@@ -730,8 +739,7 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
      its first word are kept for the pick's count (no prefix walk afterwards).  Long walks (N up to
      4095) can span q ranges far beyond the f64 exponent range: the chain is scaled by the largest
      word-start q of the window (qmx), and window words whose start q lies more than SR_QSPAN below it
-     are dropped from the ends (their entries hold < 2^-(SR_QSPAN-75) of the mass each; ABS covers it);
-     ck[k] keeps O(32k) of every word for that trim. */
+     are dropped from the ends (their entries hold < 2^-(SR_QSPAN-75) of the mass each; ABS covers it). */
   int klo = nk, khi = -1, Oklo = 0;
   double qlo = 0.0, qmx = -__builtin_inf(), qmn = __builtin_inf();
   {
@@ -759,28 +767,30 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
             qmx = fmax(qmx, qs);
             qmn = fmin(qmn, qs);
           }
-          ck[k * ckstride] = __builtin_bit_cast(double, (uint64_t)(uint32_t)O);
           O += __popc(ww);
         }
       }
     }
   }
-  if (klo <= khi && qmx - qmn > SR_QSPAN) {   /* trim the window's ends to start q >= qmx - SR_QSPAN */
+  if (klo <= khi && qmx - qmn > SR_QSPAN) {   /* trim the window's ends to start q >= qmx - SR_QSPAN (rare:
+                                                 the word-start counts are recounted from the words) */
     const int k1 = klo, k2 = khi;
+    int O = Oklo;
     klo = nk; khi = -1;
     for (int k0 = k1; k0 <= k2; k0 += SR_WCH) {
-      int Ov[SR_WCH];
+      uint32_t wv[SR_WCH];
 #pragma unroll
-      for (int t = 0; t < SR_WCH; ++t) Ov[t] = (k0 + t <= k2) ? (int)__builtin_bit_cast(uint64_t, ck[(k0 + t) * ckstride]) : 0;
+      for (int t = 0; t < SR_WCH; ++t) wv[t] = (k0 + t <= k2) ? walk_word(Pm, M, N, NW, rev, k0 + t) : 0u;
 #pragma unroll
       for (int t = 0; t < SR_WCH; ++t) {
-        const int k = k0 + t, O = Ov[t], w0 = 32 * k;
+        const int k = k0 + t, w0 = 32 * k;
         const double qs = (w0 <= o) ? ((double)((o - w0) - (POo - O)) * vA + (double)(POo - O) * vB)
                                     : -((double)((w0 - o) - (O - POo)) * vA + (double)(O - POo) * vB);
         if (k <= k2 && qs >= qmx - SR_QSPAN) {
           if (k < klo) { klo = k; qlo = qs; Oklo = O; }
           khi = k;
         }
+        O += __popc(wv[t]);
       }
     }
   }
@@ -831,12 +841,17 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
     }
   }
   GSTAMP(2);
-  /* pass 2: locate the word, replay the chain to it, certify inside it */
+  /* pass 2: locate the word; y at its start from its own sum (no replay of the chain): the word's
+     partial sums are Sp0 + y gs1[g] with gs1 its unscaled group-end sums (y = 1 at the word start)
+     and y = (ck[j] - Sp0) / gs1[7], exact for j = klo (y0).  The reconstruction moves each partial
+     sum by at most ~9 2^-53 S (the subtraction and the word's fma roundings in pass 1): the extra
+     absolute slack 2^-46 in u covers it; the unscaled sums' own rounding is inside REL's + 32.
+     Ones before the word from the column prefix table. */
   int res = -1, POp = 0;
   if (S > 0.0 && S < 0x1p1000 && !uf) {
     const double inv = 1.0 / S;
-    const double REL = (double)(N + 1) * 0x1p-50;
-    const double ABS = (double)(N + 1) * 0x1p-39;
+    const double REL = (double)(N + 33) * 0x1p-50;
+    const double ABS = (double)(N + 1) * 0x1p-39 + 0x1p-46;
     int j = klo;   /* first window word whose checkpoint reaches u (checkpoints ascend) */
     for (int k0 = klo; k0 < khi; k0 += SR_WCH) {
       double cv[SR_WCH];
@@ -845,22 +860,14 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
 #pragma unroll
       for (int t = 0; t < SR_WCH; ++t) j += (k0 + t < khi && cv[t] * inv < u) ? 1 : 0;
     }
-    double y = y0;
-    int Oj = Oklo;   /* ones among walk entries [0, 32 j) */
-    for (int k0 = klo; k0 < j; k0 += SR_WCH) {   /* words before j are full (only the walk's last word is partial) */
-      uint32_t wv[SR_WCH];
-#pragma unroll
-      for (int t = 0; t < SR_WCH; ++t) wv[t] = (k0 + t < j) ? walk_word(Pm, M, N, NW, rev, k0 + t) : 0u;
-#pragma unroll
-      for (int t = 0; t < SR_WCH; ++t) {
-        if (k0 + t < j) {
-#pragma unroll
-          for (int g = 0; g < 8; ++g) y = y * t4p(T4, (wv[t] >> (4 * g)) & 15u);
-          Oj += __popc(wv[t]);
-        }
-      }
-    }
     const double Sp0 = (j == klo) ? 0.0 : ck[(j - 1) * ckstride];
+    const double Sj = (j == khi) ? S : ck[j * ckstride];
+    int Oj;   /* ones among walk entries [0, 32 j) */
+    if (!rev) Oj = (int)prem[j * M];
+    else {    /* positions [N - 32 j, N) */
+      const int x = N - 32 * j;
+      Oj = (int)prem[NW * M] - col_pre(prem, Pm, M, x);
+    }
     const int w0 = 32 * j;
     const uint32_t ww = walk_word(Pm, M, N, NW, rev, j);
     const int nb = min(32, L + 1 - w0);
@@ -869,9 +876,9 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
     double gsum[8], gy[8];
     int ng = 0;
     {
-      double yy = y, acc = Sp0;
+      double yy = 1.0, acc = 0.0;
 #pragma unroll
-      for (int g = 0; g < 8; ++g) {
+      for (int g = 0; g < 8; ++g) {   /* unscaled */
         const uint32_t nib = (ww >> (4 * g)) & 15u;
         const int c = min(max(nb - 4 * g, 0), 4);
         gy[g] = yy;
@@ -880,11 +887,16 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, int M, int N, int N
         gsum[g] = acc;
         yy = yy * t.y;
       }
+      const double y = (j == klo) ? y0 : (Sj - Sp0) / acc;
 #pragma unroll
-      for (int g = 0; g < 8; ++g) ng += (g < nvg && gsum[g] * inv < u) ? 1 : 0;
+      for (int g = 0; g < 8; ++g) {
+        gsum[g] = __builtin_fma(y, gsum[g], Sp0);
+        gy[g] = y * gy[g];
+        ng += (g < nvg && gsum[g] * inv < u) ? 1 : 0;
+      }
     }
     const int gsel = min(ng, nvg - 1);
-    double base = Sp0, ys = y;
+    double base = Sp0, ys = gy[0];
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
       if (g == gsel) ys = gy[g];
@@ -1471,14 +1483,6 @@ __device__ __forceinline__ void ones_split(const uint32_t *Pm, int M, int lo, in
   }
 }
 
-/* ones of column m at positions [0, x) from the per-word prefix table (pre: column m's entries,
- * stride M; row k = ones in [0, 32k)) and one partial word */
-__device__ __forceinline__ int col_pre(const uint16_t *prem, const uint32_t *Pm, int M, int x)
-{
-  const int w = x >> 5, bits = x & 31;
-  const uint32_t word = bits ? Pm[w * M] : 0u;
-  return (int)prem[w * M] + __popc(word & ((1u << bits) - 1u));
-}
 /* recompute column m's prefix table (rows 0..NW) */
 __device__ __forceinline__ void col_pre_build(uint16_t *prem, const uint32_t *Pm, int M, int NW)
 {
@@ -2078,7 +2082,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           for (int pass = 0; pass < 2; ++pass) {
             int d0, e0, d1, e1;
             const bool rev = pass != 0;
-            const int res = draw_fast(Pm, M, N, NW, rev, rev ? N - b0 : a0, rev ? N - na : b0, rev ? POb : POa,
+            const int res = draw_fast(Pm, prem, M, N, NW, rev, rev ? N - b0 : a0, rev ? N - na : b0, rev ? POb : POa,
                                       rev ? ub : ua, K, tb, vA, vB, rA, rB, T4w, ckb + ckslot, CKS, &misc[MS_FBK], d0, e0,
                                       d1, e1 GSTAMP_PASS);
             GSTAMP_K4();

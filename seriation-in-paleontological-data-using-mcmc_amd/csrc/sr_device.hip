@@ -108,7 +108,7 @@ __host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB, bo
   L.hpw = o;   o = sr_al16(o + (size_t)NWV * SR_NHMAX * 4);           /* per wave: hard positions */
   L.hbw = o;   o = sr_al16(o + (size_t)NWV * NW * 4);                 /* per wave: hard bitmap */
   L.t4 = o;    o = sr_al16(o + NT * 160 * 8);                         /* per wave: 4-entry step tables (T4STRIDE) */
-  L.t8 = o;    o = sr_al16(o + rw * NT * T8STRIDE * 8);               /* per wave: 8-entry step tables (T8STRIDE) */
+  L.t8 = o;    o = sr_al16(o + (rw ? NT : (gm ? 1 : 0)) * T8STRIDE * 8);   /* per wave (gm: one shared copy): 8-entry step tables */
   L.pre = o;   o = sr_al16(o + g * (NW + 1) * M * 2);                 /* column prefix ones per word boundary */
   L.part = o;  o = sr_al16(o + (size_t)2 * 16 * NWV * 8 * 4);         /* [2][proposal][wave] count sums */
   L.tot = o;   o = sr_al16(o + (size_t)2 * NWV * 4 * 4);               /* [2][wave] t0, f0, t1, f1 */
@@ -728,9 +728,10 @@ __device__ __forceinline__ double exp2_split(double q)
 #define SR_WCH 8   /* walk words read together: one memory round trip per 8 words (HBM columns: L2 / MALL latency) */
 #endif
 #define SR_QSPAN 600.0   /* window trim below the largest word-start q (log2 units), draw_fast */
+template <bool B8>
 __device__ __forceinline__ int draw_fast(const uint32_t *Pm, const uint16_t *prem, int M, int N, int NW, bool rev, int o, int L,
                                          int POo, double u, const CD &K, const sr_mtab &tb, double vA, double vB, double rA, double rB,
-                                         const double *T4, double *ck, int ckstride, uint64_t *fbk, int &dt0, int &df0,
+                                         const double *T4, const double *T8, double *ck, int ckstride, uint64_t *fbk, int &dt0, int &df0,
                                          int &dt1, int &df1 GSTAMP_ARGS)
 {
   /* POo: ones among walk entries [0, o), from the caller's column prefix table */
@@ -825,15 +826,40 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, const uint16_t *pre
           const uint32_t ww = wv[t];
           const int nb = min(32, L + 1 - 32 * k);
           uf |= y < 0x1p-700;
-          /* 4 entries per step: T4[c][nibble] = sum of the first c prefix products of the nibble's
-             ratios (c = valid entries of the group, 0..4), T4[5][nibble] = product of all four */
+          if constexpr (B8) {
+            /* (HBM columns) the word's whole bytes from the shared 8-entry tables in Horner form (one
+               multiply per word on the y chain, draw_fast_s); the walk's partial last byte from T4 */
+            const int nfk = nb >> 3, c8 = nb & 7;
+            double2 t8[4];
 #pragma unroll
-          for (int g = 0; g < 8; ++g) {
-            const uint32_t nib = (ww >> (4 * g)) & 15u;
-            const int c = min(max(nb - 4 * g, 0), 4);
-            const double2 t4 = t4sp(T4, c, nib);
-            S = __builtin_fma(y, t4.x, S);
-            y = y * t4.y;
+            for (int g = 0; g < 4; ++g) {
+              const uint32_t e = (g < nfk) ? ((ww >> (8 * g)) & 255u) : 256u;
+              t8[g] = *reinterpret_cast<const double2 *>(T8 + 2 * e);
+            }
+            const double w23 = __builtin_fma(t8[2].y, t8[3].x, t8[2].x);
+            const double w13 = __builtin_fma(t8[1].y, w23, t8[1].x);
+            const double W = __builtin_fma(t8[0].y, w13, t8[0].x);
+            const double pw = (t8[0].y * t8[1].y) * (t8[2].y * t8[3].y);
+            S = __builtin_fma(y, W, S);
+            y = y * pw;
+            if (c8 > 0) {   /* only the walk's last word (y is not used after it) */
+              const uint32_t eb = (ww >> (8 * nfk)) & 255u;
+              const double2 tlo = t4sp(T4, min(c8, 4), eb & 15u);
+              const double shi = t4s(T4, max(c8 - 4, 0), eb >> 4);
+              S = __builtin_fma(y, tlo.x, S);
+              S = __builtin_fma(y * tlo.y, shi, S);
+            }
+          } else {
+            /* 4 entries per step: T4[c][nibble] = sum of the first c prefix products of the nibble's
+               ratios (c = valid entries of the group, 0..4), T4[5][nibble] = product of all four */
+#pragma unroll
+            for (int g = 0; g < 8; ++g) {
+              const uint32_t nib = (ww >> (4 * g)) & 15u;
+              const int c = min(max(nb - 4 * g, 0), 4);
+              const double2 t4 = t4sp(T4, c, nib);
+              S = __builtin_fma(y, t4.x, S);
+              y = y * t4.y;
+            }
           }
           ck[k * ckstride] = S;
         }
@@ -845,7 +871,8 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, const uint16_t *pre
      partial sums are Sp0 + y gs1[g] with gs1 its unscaled group-end sums (y = 1 at the word start)
      and y = (ck[j] - Sp0) / gs1[7], exact for j = klo (y0).  The reconstruction moves each partial
      sum by at most ~9 2^-53 S (the subtraction and the word's fma roundings in pass 1): the extra
-     absolute slack 2^-46 in u covers it; the unscaled sums' own rounding is inside REL's + 32.
+     absolute slack 2^-46 in u covers it; the unscaled sums' own rounding (and, with the byte tables in
+     pass 1, the relative difference of the two table forms, <= 2 x 16 ulp) is inside REL's + 32.
      Ones before the word from the column prefix table. */
   int res = -1, POp = 0;
   if (S > 0.0 && S < 0x1p1000 && !uf) {
@@ -1830,7 +1857,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   int *hp = (int *)(smem + L.hpw) + wave * SR_NHMAX;   /* this wave's copy of the hard positions */
   uint32_t *hbw = (uint32_t *)(smem + L.hbw) + wave * NW;   /* this wave's hard bitmap */
   double *T4w = (double *)(smem + L.t4) + (PR ? 0 : wave) * T4STRIDE;   /* this wave's (PR: the block's) 4-step tables */
-  double *T8w = (double *)(smem + L.t8) + (PR ? 0 : wave) * T8STRIDE;   /* this wave's (PR: the block's) 8-step tables */
+  constexpr bool SH8 = PR || GM;   /* one shared copy of the 8-step tables (built by waves 0-3, then a barrier) */
+  double *T8w = (double *)(smem + L.t8) + (SH8 ? 0 : wave) * T8STRIDE;   /* this wave's (SH8: the block's) 8-step tables */
   int *part = (int *)(smem + L.part);
   int *tot = (int *)(smem + L.tot);
   double *xs = (double *)(smem + L.xs) + wave;
@@ -1994,19 +2022,19 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 #pragma unroll
         for (int c = 0; c < 5; ++c) { T4w[2 * (c * 16 + lane)] = sc[c]; T4w[2 * (c * 16 + lane) + 1] = pr; }
       }
-      if constexpr (NWM > 0) {   /* per-wave tables for 8 walk entries with bits = e: {sum of the 8 prefix
-                                    products, product of all 8}; 4 entries per lane */
+      if constexpr (NWM > 0 || GM) {   /* tables for 8 walk entries with bits = e: {sum of the 8 prefix products,
+                                          product of all 8}; per wave 4 entries per lane, shared 1 per lane */
 #pragma unroll
-        for (int q = 0; q < (PR ? 1 : 4); ++q) {
-          const int e = lane + 64 * (PR ? wave : q);
+        for (int q = 0; q < (SH8 ? 1 : 4); ++q) {
+          const int e = lane + 64 * (SH8 ? wave : q);
           double pr = 1.0, sm = 0.0;
 #pragma unroll
           for (int k = 0; k < 8; ++k) { sm = sm + pr; pr = pr * (((e >> k) & 1) ? rB : rA); }
-          if (!PR || wave < 4) *reinterpret_cast<double2 *>(T8w + 2 * e) = make_double2(sm, pr);
+          if (!SH8 || wave < 4) *reinterpret_cast<double2 *>(T8w + 2 * e) = make_double2(sm, pr);
         }
-        if (lane == 0 && (!PR || wave == 4)) *reinterpret_cast<double2 *>(T8w + 2 * 256) = make_double2(0.0, 1.0);
+        if (lane == 0 && (!SH8 || wave == (PR ? 4 : 0))) *reinterpret_cast<double2 *>(T8w + 2 * 256) = make_double2(0.0, 1.0);
       }
-      if constexpr (PR) __syncthreads(); else wsync();
+      if constexpr (SH8) __syncthreads(); else wsync();
 
 #ifdef SR_STAMP_GIBBS
       STAMP(5);
@@ -2082,8 +2110,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           for (int pass = 0; pass < 2; ++pass) {
             int d0, e0, d1, e1;
             const bool rev = pass != 0;
-            const int res = draw_fast(Pm, prem, M, N, NW, rev, rev ? N - b0 : a0, rev ? N - na : b0, rev ? POb : POa,
-                                      rev ? ub : ua, K, tb, vA, vB, rA, rB, T4w, ckb + ckslot, CKS, &misc[MS_FBK], d0, e0,
+            const int res = draw_fast<GM>(Pm, prem, M, N, NW, rev, rev ? N - b0 : a0, rev ? N - na : b0, rev ? POb : POa,
+                                      rev ? ub : ua, K, tb, vA, vB, rA, rB, T4w, T8w, ckb + ckslot, CKS, &misc[MS_FBK], d0, e0,
                                       d1, e1 GSTAMP_PASS);
             GSTAMP_K4();
             t0 += d0; f0 += e0; t1 += d1; f1 += e1;

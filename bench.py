@@ -158,6 +158,8 @@ def main():
     ap.add_argument("--block-threads", type=int, default=0)
     ap.add_argument("--rng", default="mt", choices=("mt", "philox"), help="philox: the opt-in counter-based stream "
                     "(SR_F_RNG_PHILOX; not the reference's, so never the headline line)")
+    ap.add_argument("--generic", action="store_true", help="the generic kernel (shape from the launch "
+                    "arguments) instead of the one compiled at session creation for the dataset's shape (SR_JIT=1)")
     ap.add_argument("--no-save", action="store_true", help="sample without saving records (SURVEY.md 8(d) "
                     "asks for both; the default saves one record per call, as the reference's sampling phase)")
     args = ap.parse_args()
@@ -205,6 +207,9 @@ def main():
         assert dist.get_world_size() == args.gpus, "RCCL world does not match --gpus"
         world = dist.get_world_size()
 
+    # the sweep kernel specialised for this dataset's shape at session creation (compiled once per shape
+    # from the package's csrc/ and cached under <package>/build/jit/; identical results)
+    os.environ["SR_JIT"] = "0" if args.generic else "1"
     ds = sa.Dataset.load(args.dataset, maxs=0)
     C = args.chains_per_gpu
     # weak scaling: C chains per rank, rank r owns chains [r*C, (r+1)*C) (sd.shard), seed = id + 1
@@ -312,6 +317,7 @@ def main():
             "sites": ds.N, "taxa": ds.M, "chains": total_chains, "chains_per_gpu": C,
             "sweeps_per_step": sweeps_per_step, "block_threads": sess.block_threads, "columns": sess.variant,
             "kernel": sess.kernel,   # "split": two workgroups per chain (HBM columns)
+            "kernel_build": "specialized" if sess.specialized else "generic",
             "rng": "GSL MT19937 (the reference's stream)" if args.rng == "mt" else "Philox4x32-10 (opt-in)",
             "parallelism": "chains sharded over %d GPU(s), RCCL all-gather at end" % world,
         },

@@ -167,6 +167,10 @@ int32_t sr_session_block_threads(const sr_session *s);
  * 3 = columns in HBM, split chains: two co-resident workgroups per chain, each owning half of the
  * taxa (1024 threads, 1025..2048 taxa, grid co-resident; SR_SPLIT=0 in the environment disables it). */
 int32_t sr_session_variant(const sr_session *s);
+/* 1 when the session's launches use a kernel compiled at session creation for its exact shape
+ * (sites, taxa, hard sites fixed at compile time; SR_JIT=1 in the environment, cached under
+ * <package>/build/jit/), 0 for the generic kernel.  Results are identical either way. */
+int32_t sr_session_specialized(const sr_session *s);
 /* Checkpoint / resume (the reference has none): the full chain state (columns, pi,
    limits, counts, c/d/loglik, MT19937 ring and cursor, acceptance counters) to a file; restoring
    it over the same dataset continues every chain exactly where it stopped.  Records are not kept. */

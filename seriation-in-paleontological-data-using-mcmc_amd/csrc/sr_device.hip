@@ -44,6 +44,20 @@ __constant__ double c_log_tab[256] = SR_LOG_TAB_INIT;
 
 #define SR_ZIGR 3.44428647676   /* GSL gaussian_ziggurat PARAM_R */
 
+/* Shape specialisation (the run-time-compiled kernels, srk_jit_load): SR_FN / SR_FM / SR_FH fix the
+ * dataset's sites, taxa and hard sites at compile time, so the layout offsets, strides, loop bounds and
+ * the uniform_int divisors fold into immediates (the generic kernel holds them in ~600 spilled SGPRs).
+ * 0 / 0 / -1 (the default): taken from the launch arguments. */
+#ifndef SR_FN
+#define SR_FN 0
+#endif
+#ifndef SR_FM
+#define SR_FM 0
+#endif
+#ifndef SR_FH
+#define SR_FH (-1)
+#endif
+
 struct KArgs {
   int N, M, NW, nh, nchains;
   int calls, spc, save, rec_base, rec_cap;
@@ -1831,7 +1845,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   const int chain = SP ? (int)((blockIdx.x >> 4) << 3) + (int)(blockIdx.x & 7) : (int)blockIdx.x;
   const int half = SP ? (int)((blockIdx.x >> 3) & 1) : 0;
   if (SP && chain >= A.nchains) return;   /* grid padding (whole blocks) */
-  const int N = A.N, M = A.M, NW = A.NW, nh = A.nh;
+  const int N = SR_FN > 0 ? SR_FN : A.N, M = SR_FM > 0 ? SR_FM : A.M;
+  const int NW = SR_FN > 0 ? (SR_FN + 31) / 32 : A.NW, nh = SR_FH >= 0 ? SR_FH : A.nh;
   const int olo = SP ? half * sr_sp_half(M) : 0, ohi = SP ? min(M, olo + sr_sp_half(M)) : M;   /* own taxa */
   const int mt = olo + tx;   /* own taxon, one-taxon-per-thread kernels */
   const int KTC = (M + sr_chunk(PR) - 1) / sr_chunk(PR);   /* exact-delta chunks */
@@ -2922,12 +2937,28 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   }
 }
 
+#ifdef SR_JIT
+/* run-time compilation (srk_jit_load): this one instantiation, specialised by SR_FN / SR_FM / SR_FH */
+template __global__ void sr_sweep_kernel<SR_JIT_TB, SR_JIT_NWM, SR_JIT_GM, false, SR_JIT_SP>(KArgs);
+#else
 /* ================================================================ session layer */
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
   fprintf(stderr, "seriation: HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); return -5; } } while (0)
 
+#include <dlfcn.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <spawn.h>
+#include <sys/stat.h>
+#include <sys/wait.h>
+#include <unistd.h>
+extern char **environ;
+
 struct srk_dev {
   int device, N, M, NW, nh, nchains, TB, TPT, rec_cap, gm, pr, sp, grid, coop;
+  int jit;                 /* the launch uses the run-time specialised kernel (srk_jit_load) */
+  hipModule_t mod;
+  hipFunction_t jfn;
   size_t lds;
   hipStream_t stream;
   int own_stream;
@@ -2978,6 +3009,138 @@ static sr_kfn sr_pick_kernel(int TB, int N, int M, bool gm, bool pr, int nh, boo
   if (TB == 512) return nwm == 9 ? (sr_kfn)sr_sweep_kernel<512, 9, false> : nwm == 17 ? (sr_kfn)sr_sweep_kernel<512, 17, false> : (sr_kfn)sr_sweep_kernel<512, 0, false>;
   if (TB == 1024) return (sr_kfn)sr_sweep_kernel<1024, 0, false>;
   return nullptr;
+}
+
+/* ---- run-time specialisation (SR_JIT=1 in the environment; bench.py sets it) ------------------
+ * The generic kernels take N, M and the hard-site count from their arguments; this compiles the
+ * session's one kernel with them fixed (SR_FN / SR_FM / SR_FH: the layout offsets, strides, loop
+ * bounds and uniform_int divisors become immediates; the bench kernel's SGPR spills fall from ~590 to
+ * ~170) from the package's own csrc/ with the library's flags, once per shape: hipcc --genco in a
+ * child process (output to a log file, never to the caller's stdout), the code object cached under
+ * <package>/build/jit/ keyed by an FNV-1a hash of the sources and the definitions.  Same source, same
+ * -ffp-contract=off: the same arithmetic in the same order, bit-identical results (tests/
+ * test_gpu_jit.py).  Any failure (no sources, no compiler, compile error, occupancy) leaves the
+ * generic HIP kernel in place; there is no CPU path either way. */
+static uint64_t sr_fnv(uint64_t h, const void *p, size_t n)
+{
+  const unsigned char *b = (const unsigned char *)p;
+  for (size_t i = 0; i < n; ++i) { h ^= b[i]; h *= 1099511628211ull; }
+  return h;
+}
+
+static int sr_hash_file(const char *path, uint64_t *h)
+{
+  FILE *f = fopen(path, "rb");
+  if (!f) return -1;
+  unsigned char buf[65536];
+  size_t n;
+  while ((n = fread(buf, 1, sizeof buf, f)) > 0) *h = sr_fnv(*h, buf, n);
+  fclose(f);
+  return 0;
+}
+
+static int srk_jit_load(srk_dev *d)
+{
+#if defined(SR_STAMPS)
+  (void)d;
+  return -1;   /* (stamp builds: generic kernels only) */
+#else
+  Dl_info info;
+  if (!dladdr((void *)&srk_jit_load, &info) || !info.dli_fname) return -1;
+  /* the package directory: the first ancestor of the library holding csrc/sr_device.hip */
+  char pkg[4096], src[4200], probe[4300];
+  snprintf(pkg, sizeof pkg, "%s", info.dli_fname);
+  bool found = false;
+  for (int up = 0; up < 4 && !found; ++up) {
+    char *sl = strrchr(pkg, '/');
+    if (!sl) break;
+    *sl = 0;
+    snprintf(probe, sizeof probe, "%s/csrc/sr_device.hip", pkg);
+    found = access(probe, R_OK) == 0;
+  }
+  if (!found) return -1;
+  snprintf(src, sizeof src, "%s/csrc/sr_device.hip", pkg);
+  const int nwm = d->gm ? 0 : (sr_regwalk(d->N, d->M, d->TB, false, d->nh) ? sr_nwm(d->N) : 0);
+  char defs[512];
+  snprintf(defs, sizeof defs, "-DSR_JIT -DSR_JIT_TB=%d -DSR_JIT_NWM=%d -DSR_JIT_GM=%s -DSR_JIT_SP=%s -DSR_FN=%d -DSR_FM=%d -DSR_FH=%d%s",
+           d->TB, nwm, d->gm ? "true" : "false", d->sp ? "true" : "false", d->N, d->M, d->nh,
+#ifdef SR_FORCE_EXACT
+           " -DSR_FORCE_EXACT"
+#else
+           ""
+#endif
+  );
+  const char *flags = "--genco --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-fast-math";
+  uint64_t h = 1469598103934665603ull;
+  h = sr_fnv(h, defs, strlen(defs));
+  h = sr_fnv(h, flags, strlen(flags));
+  static const char *deps[] = {"csrc/sr_device.hip", "csrc/sr_math.h", "csrc/sr_rng.h", "csrc/sr_tables.h",
+                               "csrc/sr_internal.h", "../include/seriation.h"};
+  for (const char *f : deps) {
+    snprintf(probe, sizeof probe, "%s/%s", pkg, f);
+    if (sr_hash_file(probe, &h) != 0) return -1;
+  }
+  char dir[4300], co[4400], tmp[4500], log[4400], inc[4300], csrc[4300];
+  snprintf(dir, sizeof dir, "%s/build/jit", pkg);
+  snprintf(co, sizeof co, "%s/sr_%016llx.co", dir, (unsigned long long)h);
+  if (access(co, R_OK) != 0) {
+    snprintf(probe, sizeof probe, "%s/build", pkg);
+    (void)mkdir(probe, 0755);
+    (void)mkdir(dir, 0755);
+    snprintf(tmp, sizeof tmp, "%s.%d.tmp", co, (int)getpid());
+    snprintf(log, sizeof log, "%s/sr_%016llx.log", dir, (unsigned long long)h);
+    snprintf(inc, sizeof inc, "-I%s/../include", pkg);
+    snprintf(csrc, sizeof csrc, "-I%s/csrc", pkg);
+    const char *e = getenv("SR_HIPCC");
+    const char *hipcc = e ? e : "/opt/rocm/bin/hipcc";
+    if (access(hipcc, X_OK) != 0) return -1;
+    /* argv: the compiler, the flags and definitions split at spaces, includes, output, source */
+    char fl[1024];
+    snprintf(fl, sizeof fl, "%s %s", flags, defs);
+    char *argv[48];
+    int na = 0;
+    argv[na++] = (char *)hipcc;
+    for (char *t = strtok(fl, " "); t && na < 40; t = strtok(nullptr, " ")) argv[na++] = t;
+    argv[na++] = inc; argv[na++] = csrc;
+    argv[na++] = (char *)"-o"; argv[na++] = tmp;
+    argv[na++] = src; argv[na] = nullptr;
+    posix_spawn_file_actions_t fa;
+    posix_spawn_file_actions_init(&fa);
+    posix_spawn_file_actions_addopen(&fa, 0, "/dev/null", O_RDONLY, 0);
+    posix_spawn_file_actions_addopen(&fa, 1, log, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    posix_spawn_file_actions_adddup2(&fa, 1, 2);
+    pid_t pid;
+    const int sr = posix_spawn(&pid, hipcc, &fa, nullptr, argv, environ);
+    posix_spawn_file_actions_destroy(&fa);
+    if (sr != 0) return -1;
+    int st = 0;
+    while (waitpid(pid, &st, 0) < 0) {
+      if (errno != EINTR) return -1;
+    }
+    if (!WIFEXITED(st) || WEXITSTATUS(st) != 0 || rename(tmp, co) != 0) {
+      (void)unlink(tmp);
+      fprintf(stderr, "seriation: run-time specialisation failed (%s); the generic kernel runs\n", log);
+      return -1;
+    }
+  }
+  char name[128];
+  snprintf(name, sizeof name, "_Z15sr_sweep_kernelILi%dELi%dELb%dELb0ELb%dEEv5KArgs", d->TB, nwm, d->gm ? 1 : 0, d->sp ? 1 : 0);
+  if (hipModuleLoad(&d->mod, co) != hipSuccess) { d->mod = nullptr; return -1; }
+  if (hipModuleGetFunction(&d->jfn, d->mod, name) != hipSuccess) {
+    (void)hipModuleUnload(d->mod); d->mod = nullptr; d->jfn = nullptr;
+    return -1;
+  }
+  if (d->sp) {   /* the split grid must stay co-resident with the specialised kernel's resources */
+    int occ = 0, cus = 0;
+    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&occ, d->jfn, d->TB, d->lds) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d->device) != hipSuccess || d->grid > occ * cus) {
+      (void)hipModuleUnload(d->mod); d->mod = nullptr; d->jfn = nullptr;
+      return -1;
+    }
+  }
+  d->jit = 1;
+  return 0;
+#endif
 }
 
 extern "C" int srk_device_count(void)
@@ -3093,6 +3256,10 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
   if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) { srk_destroy(d); return -5; }
   d->own_stream = 1;
   if (hipEventCreate(&d->ev0) == hipSuccess && hipEventCreate(&d->ev1) == hipSuccess) d->have_events = 1;
+  {
+    const char *e = getenv("SR_JIT");
+    if (e && atoi(e) == 1 && !d->pr) (void)srk_jit_load(d);
+  }
   *out = d;
   return 0;
 }
@@ -3118,7 +3285,12 @@ extern "C" int srk_run(srk_dev *d, int calls, int spc, int save, int rec_base)
   sr_kfn k = sr_pick_kernel(d->TB, d->N, d->M, d->gm != 0, d->pr != 0, d->nh, d->sp != 0);
   if (d->sp) HIPCHK(hipMemsetAsync(A.xflag, 0, (size_t)d->nchains * 2 * sizeof(int), d->stream));   /* exchange sequence restarts */
   if (d->have_events) HIPCHK(hipEventRecord(d->ev0, d->stream));
-  if (d->sp && d->coop) {   /* both halves of every chain must be resident together */
+  if (d->jit) {   /* the run-time specialised kernel (same arguments) */
+    void *kp[] = {&A};
+    const unsigned g = d->sp ? (unsigned)d->grid : (unsigned)d->nchains;
+    if (d->sp && d->coop) HIPCHK(hipModuleLaunchCooperativeKernel(d->jfn, g, 1, 1, d->TB, 1, 1, (unsigned)d->lds, d->stream, kp));
+    else HIPCHK(hipModuleLaunchKernel(d->jfn, g, 1, 1, d->TB, 1, 1, (unsigned)d->lds, d->stream, kp, nullptr));
+  } else if (d->sp && d->coop) {   /* both halves of every chain must be resident together */
     void *kargs[] = {&A};
     HIPCHK(hipLaunchCooperativeKernel((const void *)k, dim3(d->grid), dim3(d->TB), kargs, (unsigned)d->lds, d->stream));
   } else if (d->sp) {
@@ -3159,6 +3331,7 @@ extern "C" double srk_last_ms(srk_dev *d)
 
 extern "C" int srk_block_threads(const srk_dev *d) { return d->TB; }
 extern "C" int srk_variant(const srk_dev *d) { return d->gm ? (d->sp ? 3 : 1) : (d->pr ? 2 : 0); }
+extern "C" int srk_specialized(const srk_dev *d) { return d->jit; }
 
 extern "C" int srk_fetch_dbg(srk_dev *d, unsigned long long *out)
 {
@@ -3303,6 +3476,7 @@ extern "C" void srk_destroy(srk_dev *d)
   for (int i = 0; i < d->nbufs; ++i) (void)hipFree(d->bufs[i]);
   if (d->have_events) { (void)hipEventDestroy(d->ev0); (void)hipEventDestroy(d->ev1); }
   if (d->own_stream && d->stream) (void)hipStreamDestroy(d->stream);
+  if (d->mod) (void)hipModuleUnload(d->mod);
   delete d;
 }
 
@@ -3342,3 +3516,4 @@ extern "C" __attribute__((visibility("default"))) int sr_device_selftest_math(in
   (void)hipFree(din); (void)hipFree(de); (void)hipFree(dl);
   return 0;
 }
+#endif   /* !SR_JIT */

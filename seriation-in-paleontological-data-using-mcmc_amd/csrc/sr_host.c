@@ -550,6 +550,7 @@ SR_API int32_t sr_session_records(const sr_session *s) { return s ? s->nrec : 0;
 SR_API int32_t sr_session_record_capacity(const sr_session *s) { return s ? s->rec_cap : 0; }
 SR_API int32_t sr_session_block_threads(const sr_session *s) { return s ? srk_block_threads(s->dev) : 0; }
 SR_API int32_t sr_session_variant(const sr_session *s) { return s ? srk_variant(s->dev) : -1; }
+SR_API int32_t sr_session_specialized(const sr_session *s) { return s ? srk_specialized(s->dev) : 0; }
 SR_API double sr_session_last_kernel_ms(sr_session *s) { return s ? srk_last_ms(s->dev) : -1.0; }
 
 SR_API int sr_session_fetch_records(sr_session *s, int32_t first, int32_t count, int16_t *ab_pi, double *cdl)

@@ -51,6 +51,7 @@ int srk_sync(srk_dev *d);
 double srk_last_ms(srk_dev *d);
 int srk_block_threads(const srk_dev *d);
 int srk_variant(const srk_dev *d);   /* 0 LDS columns, 1 HBM columns */
+int srk_specialized(const srk_dev *d);   /* 1: the run-time specialised kernel */
 int srk_fetch_dbg(srk_dev *d, unsigned long long *out);
 int srk_fetch_records(srk_dev *d, int first, int count, int16_t *ab_pi, double *cdl);
 int srk_fetch_chain_records(srk_dev *d, int chain, int first, int count, int16_t *ab_pi, double *cdl);

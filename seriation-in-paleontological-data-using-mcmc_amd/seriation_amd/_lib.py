@@ -82,7 +82,7 @@ PUBLIC_SYMBOLS = [
     "sr_session_run", "sr_session_sync", "sr_session_records", "sr_session_record_capacity",
     "sr_session_fetch_records", "sr_session_reset_records", "sr_session_fetch_chain_records", "sr_session_summaries",
     "sr_session_state",
-    "sr_session_accept_counts", "sr_session_fallback_counts", "sr_session_debug_flagged", "sr_session_last_kernel_ms", "sr_session_block_threads", "sr_session_variant",
+    "sr_session_accept_counts", "sr_session_fallback_counts", "sr_session_debug_flagged", "sr_session_last_kernel_ms", "sr_session_block_threads", "sr_session_variant", "sr_session_specialized",
     "sr_session_checkpoint", "sr_session_restore",
     "sr_session_destroy", "sr_posterior", "sr_session_posterior", "sr_strerror", "sr_device_count", "sr_version",
 ]
@@ -131,6 +131,7 @@ def _lib():
         "sr_session_last_kernel_ms": (c_double, [c_void_p]),
         "sr_session_block_threads": (c_i32, [c_void_p]),
         "sr_session_variant": (c_i32, [c_void_p]),
+        "sr_session_specialized": (c_i32, [c_void_p]),
         "sr_session_checkpoint": (c_int, [c_void_p, ctypes.c_char_p]),
         "sr_session_restore": (c_int, [P(sr_dataset), ctypes.c_char_p, P(sr_run_opts), P(c_void_p)]),
         "sr_session_destroy": (None, [c_void_p]),

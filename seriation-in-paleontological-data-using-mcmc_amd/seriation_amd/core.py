@@ -163,6 +163,12 @@ class Session:
         (one workgroup per chain, one thread per taxon or several)."""
         return {2: "pair", 3: "split"}.get(L.lib().sr_session_variant(self.h), "single")
 
+    @property
+    def specialized(self):
+        """True when the launches use the kernel compiled at session creation for this dataset's
+        exact shape (SR_JIT=1 in the environment), False for the generic one."""
+        return bool(L.lib().sr_session_specialized(self.h))
+
     def set_stream(self, stream_handle):
         _check(L.lib().sr_session_set_stream(self.h, ctypes.c_void_p(stream_handle)), "set_stream")
 

@@ -87,6 +87,7 @@ int srk_sync(srk_dev *d) { (void)d; return 0; }
 double srk_last_ms(srk_dev *d) { (void)d; return 0.0; }
 int srk_block_threads(const srk_dev *d) { (void)d; return 64; }
 int srk_variant(const srk_dev *d) { (void)d; return 0; }
+int srk_specialized(const srk_dev *d) { (void)d; return 0; }
 int srk_fetch_dbg(srk_dev *d, unsigned long long *o) { memset(o, 0, (size_t)d->st.nchains * 17 * 8 * 8); return 0; }
 
 int srk_fetch_records(srk_dev *d, int first, int count, int16_t *ab_pi, double *cdl)

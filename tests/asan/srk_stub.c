@@ -19,6 +19,7 @@ int srk_sync(srk_dev *d) { (void)d; return -5; }
 double srk_last_ms(srk_dev *d) { (void)d; return -1.0; }
 int srk_block_threads(const srk_dev *d) { (void)d; return 0; }
 int srk_variant(const srk_dev *d) { (void)d; return -1; }
+int srk_specialized(const srk_dev *d) { (void)d; return 0; }
 int srk_fetch_dbg(srk_dev *d, unsigned long long *o) { (void)d; (void)o; return -5; }
 int srk_fetch_records(srk_dev *d, int f, int c, int16_t *a, double *b) { (void)d; (void)f; (void)c; (void)a; (void)b; return -5; }
 int srk_download_state(srk_dev *d, sr_state_host *st) { (void)d; (void)st; return -5; }

@@ -2939,7 +2939,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 
 #ifdef SR_JIT
 /* run-time compilation (srk_jit_load): this one instantiation, specialised by SR_FN / SR_FM / SR_FH */
-template __global__ void sr_sweep_kernel<SR_JIT_TB, SR_JIT_NWM, SR_JIT_GM, false, SR_JIT_SP>(KArgs);
+template __global__ void sr_sweep_kernel<SR_JIT_TB, SR_JIT_NWM, false>(KArgs);
 #else
 /* ================================================================ session layer */
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
@@ -3015,7 +3015,7 @@ static sr_kfn sr_pick_kernel(int TB, int N, int M, bool gm, bool pr, int nh, boo
  * The generic kernels take N, M and the hard-site count from their arguments; this compiles the
  * session's one kernel with them fixed (SR_FN / SR_FM / SR_FH: the layout offsets, strides, loop
  * bounds and uniform_int divisors become immediates; the bench kernel's SGPR spills fall from ~590 to
- * ~170) from the package's own csrc/ with the library's flags, once per shape: hipcc --genco in a
+ * ~170; LDS-column kernels) from the package's own csrc/ with the library's flags, once per shape: hipcc --genco in a
  * child process (output to a log file, never to the caller's stdout), the code object cached under
  * <package>/build/jit/ keyed by an FNV-1a hash of the sources and the definitions.  Same source, same
  * -ffp-contract=off: the same arithmetic in the same order, bit-identical results (tests/
@@ -3045,6 +3045,9 @@ static int srk_jit_load(srk_dev *d)
   (void)d;
   return -1;   /* (stamp builds: generic kernels only) */
 #else
+  /* LDS-column kernels only: the HBM-column split kernel measured 4.4 % slower specialised (its
+     register allocation shifts; profiles/r03z6_ab_jit.json) */
+  if (d->gm) return -1;
   Dl_info info;
   if (!dladdr((void *)&srk_jit_load, &info) || !info.dli_fname) return -1;
   /* the package directory: the first ancestor of the library holding csrc/sr_device.hip */
@@ -3060,10 +3063,10 @@ static int srk_jit_load(srk_dev *d)
   }
   if (!found) return -1;
   snprintf(src, sizeof src, "%s/csrc/sr_device.hip", pkg);
-  const int nwm = d->gm ? 0 : (sr_regwalk(d->N, d->M, d->TB, false, d->nh) ? sr_nwm(d->N) : 0);
+  const int nwm = sr_regwalk(d->N, d->M, d->TB, false, d->nh) ? sr_nwm(d->N) : 0;
   char defs[512];
-  snprintf(defs, sizeof defs, "-DSR_JIT -DSR_JIT_TB=%d -DSR_JIT_NWM=%d -DSR_JIT_GM=%s -DSR_JIT_SP=%s -DSR_FN=%d -DSR_FM=%d -DSR_FH=%d%s",
-           d->TB, nwm, d->gm ? "true" : "false", d->sp ? "true" : "false", d->N, d->M, d->nh,
+  snprintf(defs, sizeof defs, "-DSR_JIT -DSR_JIT_TB=%d -DSR_JIT_NWM=%d -DSR_FN=%d -DSR_FM=%d -DSR_FH=%d%s",
+           d->TB, nwm, d->N, d->M, d->nh,
 #ifdef SR_FORCE_EXACT
            " -DSR_FORCE_EXACT"
 #else
@@ -3124,19 +3127,11 @@ static int srk_jit_load(srk_dev *d)
     }
   }
   char name[128];
-  snprintf(name, sizeof name, "_Z15sr_sweep_kernelILi%dELi%dELb%dELb0ELb%dEEv5KArgs", d->TB, nwm, d->gm ? 1 : 0, d->sp ? 1 : 0);
+  snprintf(name, sizeof name, "_Z15sr_sweep_kernelILi%dELi%dELb0ELb0ELb0EEv5KArgs", d->TB, nwm);
   if (hipModuleLoad(&d->mod, co) != hipSuccess) { d->mod = nullptr; return -1; }
   if (hipModuleGetFunction(&d->jfn, d->mod, name) != hipSuccess) {
     (void)hipModuleUnload(d->mod); d->mod = nullptr; d->jfn = nullptr;
     return -1;
-  }
-  if (d->sp) {   /* the split grid must stay co-resident with the specialised kernel's resources */
-    int occ = 0, cus = 0;
-    if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&occ, d->jfn, d->TB, d->lds) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d->device) != hipSuccess || d->grid > occ * cus) {
-      (void)hipModuleUnload(d->mod); d->mod = nullptr; d->jfn = nullptr;
-      return -1;
-    }
   }
   d->jit = 1;
   return 0;
@@ -3285,11 +3280,9 @@ extern "C" int srk_run(srk_dev *d, int calls, int spc, int save, int rec_base)
   sr_kfn k = sr_pick_kernel(d->TB, d->N, d->M, d->gm != 0, d->pr != 0, d->nh, d->sp != 0);
   if (d->sp) HIPCHK(hipMemsetAsync(A.xflag, 0, (size_t)d->nchains * 2 * sizeof(int), d->stream));   /* exchange sequence restarts */
   if (d->have_events) HIPCHK(hipEventRecord(d->ev0, d->stream));
-  if (d->jit) {   /* the run-time specialised kernel (same arguments) */
+  if (d->jit) {   /* the run-time specialised kernel (same arguments; LDS columns: one workgroup per chain) */
     void *kp[] = {&A};
-    const unsigned g = d->sp ? (unsigned)d->grid : (unsigned)d->nchains;
-    if (d->sp && d->coop) HIPCHK(hipModuleLaunchCooperativeKernel(d->jfn, g, 1, 1, d->TB, 1, 1, (unsigned)d->lds, d->stream, kp));
-    else HIPCHK(hipModuleLaunchKernel(d->jfn, g, 1, 1, d->TB, 1, 1, (unsigned)d->lds, d->stream, kp, nullptr));
+    HIPCHK(hipModuleLaunchKernel(d->jfn, (unsigned)d->nchains, 1, 1, d->TB, 1, 1, (unsigned)d->lds, d->stream, kp, nullptr));
   } else if (d->sp && d->coop) {   /* both halves of every chain must be resident together */
     void *kargs[] = {&A};
     HIPCHK(hipLaunchCooperativeKernel((const void *)k, dim3(d->grid), dim3(d->TB), kargs, (unsigned)d->lds, d->stream));

@@ -229,6 +229,10 @@ def main():
     for _ in range(args.warmup):
         sess.run(cps, save=False)
     sess.reset_records()
+    # pinned host workspace for the selected chains' records (allocated before the timed region)
+    nrec_ws = args.steps * cps if not args.no_save else 1
+    pin_ab = torch.empty((CHAINS_SELECTED, nrec_ws, 2 * ds.M + ds.N), dtype=torch.int16, pin_memory=True).numpy()
+    pin_cd = torch.empty((CHAINS_SELECTED, nrec_ws, 3), dtype=torch.float64, pin_memory=True).numpy()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -247,6 +251,7 @@ def main():
     # (compute_exp_data, mcmc.c:53-67, in C) -> ONE all-gather of the summaries -> the one-sigma
     # selection on every rank -> the selected chains' saved samples gathered from their owners
     rows = sess.summaries()
+    t_summ = time.perf_counter()
     nrec = int(sess.fetch_cdl().shape[1]) if args.no_save else args.steps * cps
     if dist:
         gathered = sd.gather_summaries(rows, C * world, device="cuda")
@@ -254,10 +259,16 @@ def main():
         gathered = rows
     selected = sd.select_chains(gathered, CHAINS_SELECTED)
     mine = [c for c in selected if c in set(chain_ids)]
-    loc = [sess.fetch_chain_records(chain_ids.index(c)) for c in mine]
+    t_sel = time.perf_counter()
     W = 2 * ds.M + ds.N
-    loc_ab = np.stack([a for a, _ in loc]) if loc else np.zeros((0, nrec, W), np.int16)
-    loc_cd = np.stack([c for _, c in loc]) if loc else np.zeros((0, nrec, 3))
+    if len(mine) <= pin_ab.shape[0]:   # straight into the pinned workspace (one DMA copy per chain)
+        loc_ab, loc_cd = pin_ab[:len(mine)], pin_cd[:len(mine)]
+        for k, c in enumerate(mine):
+            sess.fetch_chain_records(chain_ids.index(c), out=(loc_ab[k], loc_cd[k]))
+    else:
+        loc = [sess.fetch_chain_records(chain_ids.index(c)) for c in mine]
+        loc_ab, loc_cd = np.stack([a for a, _ in loc]), np.stack([c for _, c in loc])
+    t_fetch = time.perf_counter()
     if dist:
         sel_ab, sel_cdl = sd.gather_selected_records(selected, C * world, mine, loc_ab, loc_cd, device="cuda")
     else:
@@ -267,6 +278,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     tail_ms = (time.perf_counter() - t_kernels) * 1e3
+    tail_parts = {"summaries_ms": (t_summ - t_kernels) * 1e3, "gather_select_ms": (t_sel - t_summ) * 1e3,
+                  "fetch_selected_ms": (t_fetch - t_sel) * 1e3, "gather_records_ms": (time.perf_counter() - t_fetch) * 1e3}
     # posterior statistics of the selected chains (script.py:100-152), outside the timed region
     ec, ed, corr = sd.selection_statistics(sel_ab, sel_cdl, ds.N, ds.M, CHAINS_SELECTED)
     if dist:
@@ -338,7 +351,7 @@ def main():
         "limiter": limiter,
         "cpu_baseline": cpu,
         "cpu_baseline_O0": cpu_o0,
-        "timing": {"kernel_ms_per_step": kernel_ms, "gather_select_ms": tail_ms,
+        "timing": {"kernel_ms_per_step": kernel_ms, "gather_select_ms": tail_ms, "tail_parts": tail_parts,
                    "note": "gather_select_ms: after the last kernel, the record fetch, summary all-gather, "
                            "one-sigma selection and the gather of the selected chains' records (inside the "
                            "timed region)"},

@@ -2957,6 +2957,7 @@ extern char **environ;
 struct srk_dev {
   int device, N, M, NW, nh, nchains, TB, TPT, rec_cap, gm, pr, sp, grid, coop;
   int jit;                 /* the launch uses the run-time specialised kernel (srk_jit_load) */
+  double *dsum;            /* srk_exp_data's per-chain sums (device) */
   hipModule_t mod;
   hipFunction_t jfn;
   size_t lds;
@@ -3354,6 +3355,60 @@ extern "C" int srk_fetch_records(srk_dev *d, int first, int count, int16_t *ab_p
                        rows * 3 * sizeof(double), hipMemcpyDeviceToHost));
   }
   return 0;
+}
+
+/* compute_exp_data's sums (mcmc.c:53-58) over record rows [first, first + count) of every chain:
+   ls = sum of -loglik, cs = sum of exp(c), ds = sum of exp(d), in row order.  One block per chain: the
+   exps of a chunk of rows in parallel into LDS (sr_exp_m is glibc's exp bit for bit), then thread 0
+   adds the chunk in row order (the reference's sequential sums).  Only 3 doubles per chain leave the
+   GPU (the row data stay in HBM). */
+#define SR_XD_CHUNK 1024
+__global__ __launch_bounds__(256) void sr_exp_data_kernel(const double *rec_cdl, int rec_cap, int first, int count,
+                                                          double *out)
+{
+  __shared__ double tabs[512];
+  __shared__ double ce[SR_XD_CHUNK], de[SR_XD_CHUNK], le[SR_XD_CHUNK];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    ((uint64_t *)tabs)[i] = c_exp_tab[i];
+    tabs[256 + i] = c_log_tab[i];
+  }
+  sr_mtab tb;
+  tb.exp_tab = (const uint64_t *)tabs; tb.log_tab = tabs + 256;
+  const int c = blockIdx.x;
+  const double *r = rec_cdl + ((size_t)c * rec_cap + first) * 3;
+  double ls = 0., cs = 0., ds = 0.;
+  for (int t0 = 0; t0 < count; t0 += SR_XD_CHUNK) {
+    const int n = min(SR_XD_CHUNK, count - t0);
+    __syncthreads();   /* tables loaded / the previous chunk summed */
+    for (int t = threadIdx.x; t < n; t += blockDim.x) {
+      const double *rr = r + 3 * (size_t)(t0 + t);
+      ce[t] = sr_exp_m(rr[0], &tb);
+      de[t] = sr_exp_m(rr[1], &tb);
+      le[t] = rr[2];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int t = 0; t < n; ++t) { ls += -(le[t]); cs += ce[t]; ds += de[t]; }
+  }
+  if (threadIdx.x == 0) { out[3 * c] = ls; out[3 * c + 1] = cs; out[3 * c + 2] = ds; }
+}
+
+extern "C" int srk_exp_data(srk_dev *d, int first, int count, double *sums)
+{
+  if (first < 0 || count < 0 || first + count > d->rec_cap) return -1;
+  HIPCHK(hipSetDevice(d->device));
+  if (!d->dsum) {
+    void *p = nullptr;
+    HIPCHK(hipMalloc(&p, (size_t)d->nchains * 3 * sizeof(double)));
+    d->bufs[d->nbufs++] = p;
+    d->dsum = (double *)p;
+  }
+  hipLaunchKernelGGL(sr_exp_data_kernel, dim3(d->nchains), dim3(256), 0, d->stream, d->args.rec_cdl, d->rec_cap, first, count,
+                     d->dsum);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(sums, d->dsum, (size_t)d->nchains * 3 * sizeof(double), hipMemcpyDeviceToHost, d->stream));
+  HIPCHK(hipStreamSynchronize(d->stream));
+  return sp_check(d);
 }
 
 /* one chain's rows [first, first + count) of its record slab */

@@ -572,25 +572,19 @@ SR_API int sr_session_fetch_chain_records(sr_session *s, int32_t chain, int32_t 
 SR_API int sr_session_summaries(sr_session *s, int32_t first, int32_t count, sr_chain_summary *out)
 {
   if (!s || !out || first < 0 || count < 0 || first + count > s->nrec) return SR_EINVAL;
-  double *cd = (double *)malloc(sizeof(double) * 3 * ((size_t)count > 0 ? (size_t)count : 1) * s->nchains);
-  if (!cd) return SR_ENOMEM;
-  int rc = count ? srk_fetch_records(s->dev, first, count, NULL, cd) : 0;
-  if (rc) { free(cd); return SR_EDEVICE; }
+  /* the sums on the device, in the reference's row order (srk_exp_data); only they are copied back */
+  double *sm = (double *)calloc((size_t)3 * s->nchains, sizeof(double));
+  if (!sm) return SR_ENOMEM;
+  int rc = count ? srk_exp_data(s->dev, first, count, sm) : 0;
+  if (rc) { free(sm); return SR_EDEVICE; }
   for (int c = 0; c < s->nchains; c++) {
-    double ls = 0., cs = 0., ds = 0.;
-    for (int t = 0; t < count; t++) {
-      const double *r = cd + ((size_t)c * count + t) * 3;
-      ls += -(r[2]);
-      cs += exp(r[0]);
-      ds += exp(r[1]);
-    }
     out[c].chain_id = s->specs[c].chain_id;
     out[c].consistent = 0;
-    out[c].exp_loglik = ls / 1000;
-    out[c].exp_c = cs / 1000;
-    out[c].exp_d = ds / 1000;
+    out[c].exp_loglik = sm[3 * c] / 1000;   /* print_exp_data divides by 1000 (mcmc.c:62-64) */
+    out[c].exp_c = sm[3 * c + 1] / 1000;
+    out[c].exp_d = sm[3 * c + 2] / 1000;
   }
-  free(cd);
+  free(sm);
   return SR_OK;
 }
 

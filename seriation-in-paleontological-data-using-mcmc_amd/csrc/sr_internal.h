@@ -54,6 +54,8 @@ int srk_variant(const srk_dev *d);   /* 0 LDS columns, 1 HBM columns */
 int srk_specialized(const srk_dev *d);   /* 1: the run-time specialised kernel */
 int srk_fetch_dbg(srk_dev *d, unsigned long long *out);
 int srk_fetch_records(srk_dev *d, int first, int count, int16_t *ab_pi, double *cdl);
+/* per chain {sum -loglik, sum exp(c), sum exp(d)} over record rows [first, first + count) (compute_exp_data) */
+int srk_exp_data(srk_dev *d, int first, int count, double *sums);
 int srk_fetch_chain_records(srk_dev *d, int chain, int first, int count, int16_t *ab_pi, double *cdl);
 int srk_download_state(srk_dev *d, sr_state_host *st);
 int srk_run_pipelined(srk_dev *d, int total_calls, int cpl, int spc,

@@ -204,13 +204,22 @@ class Session:
                                                     cdl.ctypes.data_as(ctypes.POINTER(ctypes.c_double))), "fetch")
         return cdl
 
-    def fetch_chain_records(self, chain, first=0, count=None):
-        """One chain's buffered records: (ab_pi int16 [count, 2M+N], cdl float64 [count, 3])."""
+    def fetch_chain_records(self, chain, first=0, count=None, out=None):
+        """One chain's buffered records: (ab_pi int16 [count, 2M+N], cdl float64 [count, 3]); out: a
+        caller-owned pair of C-contiguous arrays of those shapes to fill (e.g. views of pinned host
+        memory, so the copy runs at DMA speed without page faults)."""
         k = L.lib().sr_session_records(self.h)
         count = k - first if count is None else count
         N, M = self.ds.N, self.ds.M
-        ab = np.zeros((count, 2 * M + N), np.int16)
-        cdl = np.zeros((count, 3), np.float64)
+        if out is not None:
+            ab, cdl = out
+            if ab.shape != (count, 2 * M + N) or ab.dtype != np.int16 or not ab.flags.c_contiguous or \
+                    cdl.shape != (count, 3) or cdl.dtype != np.float64 or not cdl.flags.c_contiguous:
+                raise ValueError("fetch_chain_records: out arrays must be C-contiguous int16 [%d, %d] and "
+                                 "float64 [%d, 3]" % (count, 2 * M + N, count))
+        else:
+            ab = np.zeros((count, 2 * M + N), np.int16)
+            cdl = np.zeros((count, 3), np.float64)
         if count:
             _check(L.lib().sr_session_fetch_chain_records(self.h, chain, first, count,
                                                           ab.ctypes.data_as(ctypes.POINTER(ctypes.c_int16)),

@@ -9,6 +9,7 @@
  * matches count01: mcmc_consistent must flag it).  Never linked by the product. */
 #include <stdio.h>
 #include <stdlib.h>
+#include <math.h>
 #include <string.h>
 #include "sr_internal.h"
 
@@ -97,6 +98,20 @@ int srk_fetch_records(srk_dev *d, int first, int count, int16_t *ab_pi, double *
   for (int c = 0; c < d->st.nchains; c++) {
     if (ab_pi) memcpy(ab_pi + (size_t)c * count * W, d->rec + ((size_t)c * d->rec_cap + first) * W, (size_t)count * W * 2);
     if (cdl) memcpy(cdl + (size_t)c * count * 3, d->rcd + ((size_t)c * d->rec_cap + first) * 3, (size_t)count * 24);
+  }
+  return 0;
+}
+
+int srk_exp_data(srk_dev *d, int first, int count, double *sums)
+{
+  if (first < 0 || count < 0 || first + count > d->rec_cap) return -1;
+  for (int c = 0; c < d->st.nchains; c++) {
+    double ls = 0., cs = 0., ds = 0.;
+    for (int t = 0; t < count; t++) {
+      const double *r = d->rcd + ((size_t)c * d->rec_cap + first + t) * 3;
+      ls += -(r[2]); cs += exp(r[0]); ds += exp(r[1]);
+    }
+    sums[3 * c] = ls; sums[3 * c + 1] = cs; sums[3 * c + 2] = ds;
   }
   return 0;
 }

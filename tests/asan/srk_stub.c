@@ -22,6 +22,7 @@ int srk_variant(const srk_dev *d) { (void)d; return -1; }
 int srk_specialized(const srk_dev *d) { (void)d; return 0; }
 int srk_fetch_dbg(srk_dev *d, unsigned long long *o) { (void)d; (void)o; return -5; }
 int srk_fetch_records(srk_dev *d, int f, int c, int16_t *a, double *b) { (void)d; (void)f; (void)c; (void)a; (void)b; return -5; }
+int srk_exp_data(srk_dev *d, int f, int c, double *s) { (void)d; (void)f; (void)c; (void)s; return -5; }
 int srk_download_state(srk_dev *d, sr_state_host *st) { (void)d; (void)st; return -5; }
 int srk_fetch_chain_records(srk_dev *d, int ch, int f, int c, int16_t *a, double *b)
 {

@@ -3091,7 +3091,7 @@ static int srk_jit_load(srk_dev *d)
     snprintf(probe, sizeof probe, "%s/build", pkg);
     (void)mkdir(probe, 0755);
     (void)mkdir(dir, 0755);
-    snprintf(tmp, sizeof tmp, "%s.%d.tmp", co, (int)getpid());
+    snprintf(tmp, sizeof tmp, "%s.%d.%p.tmp", co, (int)getpid(), (void *)d);   /* (shard threads may compile together) */
     snprintf(log, sizeof log, "%s/sr_%016llx.log", dir, (unsigned long long)h);
     snprintf(inc, sizeof inc, "-I%s/../include", pkg);
     snprintf(csrc, sizeof csrc, "-I%s/csrc", pkg);
@@ -3104,7 +3104,8 @@ static int srk_jit_load(srk_dev *d)
     char *argv[48];
     int na = 0;
     argv[na++] = (char *)hipcc;
-    for (char *t = strtok(fl, " "); t && na < 40; t = strtok(nullptr, " ")) argv[na++] = t;
+    char *sv = nullptr;
+    for (char *t = strtok_r(fl, " ", &sv); t && na < 40; t = strtok_r(nullptr, " ", &sv)) argv[na++] = t;
     argv[na++] = inc; argv[na++] = csrc;
     argv[na++] = (char *)"-o"; argv[na++] = tmp;
     argv[na++] = src; argv[na] = nullptr;

@@ -95,3 +95,19 @@ def test_hbm_columns_stay_generic(monkeypatch, kw, env):
     ds = sa.Dataset.parse(make_text(64, 1100, 6, seed=64 * 1000 + 1100), maxs=0)
     with sa.Session(ds, [1, 2], **kw) as s:
         assert s.variant == "hbm" and not s.specialized
+
+
+def test_specialized_shards_compile_together(monkeypatch):
+    """Two shards on one device (sr_run_chains_multi: one host thread and session each) create their
+    sessions together and both compile the same new shape: same records as the generic single session."""
+    text = make_text(70, 90, 3, seed=70 * 1000 + 90 + 1)   # a shape no other test compiles
+    ds = sa.Dataset.parse(text, maxs=0)
+    seeds = [2, 5, 8, 11]
+    monkeypatch.setenv("SR_JIT", "0")
+    _, (rig, rdg) = sa.run_chains(ds, seeds, burnin_calls=2, sample_calls=4, keep_records=True)
+    monkeypatch.setenv("SR_JIT", "1")
+    _, (rij, rdj) = sa.run_chains(ds, seeds, burnin_calls=2, sample_calls=4, keep_records=True, devices=[0, 0])
+    np.testing.assert_array_equal(rij, rig)
+    assert np.array_equal(rdj.view(np.uint64), rdg.view(np.uint64))
+    with sa.Session(ds, seeds) as s:
+        assert s.specialized

@@ -159,7 +159,17 @@ def main():
     ap.add_argument("--rng", default="mt", choices=("mt", "philox"), help="philox: the opt-in counter-based stream "
                     "(SR_F_RNG_PHILOX; not the reference's, so never the headline line)")
     ap.add_argument("--generic", action="store_true", help="the generic kernel (shape from the launch "
-                    "arguments) instead of the one compiled at session creation for the dataset's shape (SR_JIT=1)")
+                    "arguments) instead of the default one compiled for the dataset's shape (SR_F_GENERIC_KERNEL)")
+    ap.add_argument("--parity-chains", type=int, default=2, help="after the timed region, rerun this many of the "
+                    "selected chains on the CPU oracle (burn-in = the warm-up calls) and require every saved record "
+                    "of the timed region to match bit for bit (0: skip)")
+    ap.add_argument("--parity-calls", type=int, default=0, help="compare only the first K saved records of each "
+                    "checked chain (0: all; the HBM-column workloads take minutes per chain on the CPU)")
+    ap.add_argument("--device-of-rank", default="", help="comma-separated HIP ordinal per local rank (default: the "
+                    "local rank), e.g. 0,0 to rehearse two ranks on one GPU")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"), help="torch.distributed backend under "
+                    "a launcher: nccl = RCCL over xGMI (one rank per GPU); gloo = host collectives (rehearsals with "
+                    "several ranks on one GPU, which RCCL does not allow)")
     ap.add_argument("--no-save", action="store_true", help="sample without saving records (SURVEY.md 8(d) "
                     "asks for both; the default saves one record per call, as the reference's sampling phase)")
     args = ap.parse_args()
@@ -200,16 +210,22 @@ def main():
     from seriation_amd import dist as sd
 
     dist = None
-    torch.cuda.set_device(local_rank)
+    device = local_rank
+    if args.device_of_rank:
+        device = [int(x) for x in args.device_of_rank.split(",")][local_rank]
+    torch.cuda.set_device(device)
+    coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"   # where the end-of-run collectives' tensors live
     if "WORLD_SIZE" in os.environ:   # under a launcher: the RCCL path, also at world 1
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        assert dist.get_world_size() == args.gpus, "RCCL world does not match --gpus"
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group("gloo")
+        assert dist.get_world_size() == args.gpus, "torch.distributed world does not match --gpus"
         world = dist.get_world_size()
 
-    # the sweep kernel specialised for this dataset's shape at session creation (compiled once per shape
-    # from the package's csrc/ and cached under <package>/build/jit/; identical results)
-    os.environ["SR_JIT"] = "0" if args.generic else "1"
+    # the session runs the sweep kernel compiled for this dataset's shape (the library's default for LDS
+    # columns; cached, identical results) unless --generic
     ds = sa.Dataset.load(args.dataset, maxs=0)
     C = args.chains_per_gpu
     # weak scaling: C chains per rank, rank r owns chains [r*C, (r+1)*C) (sd.shard), seed = id + 1
@@ -218,8 +234,9 @@ def main():
     cps = args.calls_per_step
     # records of every timed step are kept (steps x calls-per-step saved samples per chain: 1000 at the
     # driver's --steps 20, the reference's sampling window ts = 1000, mcmc.c:180-185)
-    sess = sa.Session(ds, seeds, device=local_rank, calls_per_launch=max(1, args.steps * cps),
-                      block_threads=args.block_threads, chain_ids=chain_ids, columns=args.columns, rng=args.rng)
+    sess = sa.Session(ds, seeds, device=device, calls_per_launch=max(1, args.steps * cps),
+                      block_threads=args.block_threads, chain_ids=chain_ids, columns=args.columns, rng=args.rng,
+                      generic=args.generic)
     stream = torch.cuda.current_stream()
     sess.set_stream(stream.cuda_stream)
 
@@ -254,7 +271,7 @@ def main():
     t_summ = time.perf_counter()
     nrec = int(sess.fetch_cdl().shape[1]) if args.no_save else args.steps * cps
     if dist:
-        gathered = sd.gather_summaries(rows, C * world, device="cuda")
+        gathered = sd.gather_summaries(rows, C * world, device=coll_dev)
     else:
         gathered = rows
     selected = sd.select_chains(gathered, CHAINS_SELECTED)
@@ -270,7 +287,7 @@ def main():
         loc_ab, loc_cd = np.stack([a for a, _ in loc]), np.stack([c for _, c in loc])
     t_fetch = time.perf_counter()
     if dist:
-        sel_ab, sel_cdl = sd.gather_selected_records(selected, C * world, mine, loc_ab, loc_cd, device="cuda")
+        sel_ab, sel_cdl = sd.gather_selected_records(selected, C * world, mine, loc_ab, loc_cd, device=coll_dev)
     else:
         sel_ab, sel_cdl = loc_ab, loc_cd
     torch.cuda.synchronize()
@@ -283,12 +300,23 @@ def main():
     # posterior statistics of the selected chains (script.py:100-152), outside the timed region
     ec, ed, corr = sd.selection_statistics(sel_ab, sel_cdl, ds.N, ds.M, CHAINS_SELECTED)
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
     assert len(gathered) == C * world and np.isfinite(gathered).all() and selected
     assert sel_ab.shape[0] == len(selected) and (sel_ab[:, :, 2 * ds.M:] >= 0).all()
+
+    # parity leg (after the timed region, rank 0): the CPU oracle reruns some selected chains and every saved
+    # record of the timed region must match bit for bit (tests/bench_parity.py; the checker, not measured)
+    parity = None
+    if rank == 0 and args.parity_chains > 0 and not args.no_save and args.rng == "mt":
+        import bench_parity
+        with open(args.dataset, "rb") as fh:
+            text = fh.read()
+        k = min(args.parity_chains, len(selected))
+        parity = bench_parity.check_selected(text, selected[:k], [c + 1 for c in selected[:k]], args.warmup * cps,
+                                             sel_ab[:k], sel_cdl[:k], calls=args.parity_calls or None)
 
     total_chains = C * world
     sweeps_per_step = cps * 10
@@ -330,9 +358,10 @@ def main():
             "sites": ds.N, "taxa": ds.M, "chains": total_chains, "chains_per_gpu": C,
             "sweeps_per_step": sweeps_per_step, "block_threads": sess.block_threads, "columns": sess.variant,
             "kernel": sess.kernel,   # "split": two workgroups per chain (HBM columns)
-            "kernel_build": "specialized" if sess.specialized else "generic",
+            "kernel_build": "specialized" if sess.specialized else "generic",   # the default is specialized
             "rng": "GSL MT19937 (the reference's stream)" if args.rng == "mt" else "Philox4x32-10 (opt-in)",
-            "parallelism": "chains sharded over %d GPU(s), RCCL all-gather at end" % world,
+            "parallelism": "chains sharded over %d GPU(s), %s all-gather at end" % (
+                world, "RCCL" if args.dist_backend == "nccl" else "gloo (host)"),
         },
         "roofline": {
             "bound": "hbm",
@@ -361,12 +390,15 @@ def main():
                                                        np.ascontiguousarray(sel_cdl).tobytes()).hexdigest(),
                       "note": "script.py:70-152 over every timed step's saved samples of the selected chains (the "
                               "reference divides by 1000: exact means at --steps 20 x 50 calls = 1000 samples)"},
+        "parity": parity,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
     sess.close()
     if dist:
         dist.destroy_process_group()
+    if parity is not None and not parity["match"]:
+        raise SystemExit("bench.py: the timed records differ from the CPU oracle: %s" % parity["mismatch"])
 
 
 if __name__ == "__main__":

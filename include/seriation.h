@@ -80,6 +80,9 @@ typedef struct {
 #define SR_F_DIAG 64         /* the reference's stderr diagnostics during initialisation: "mcmc_initab: zero column
                                 at %d, continuing." per all-zero column, from mcmc_readmodel's and mcmc_randomize's
                                 mcmc_initab (mcmc.c:457); the drop-in CLI sets it */
+#define SR_F_GENERIC_KERNEL 128  /* run the generic sweep kernel (shape from the launch arguments) instead of the
+                                    default shape-specialised one (sr_session_specialized); SR_JIT=0 in the
+                                    environment does the same.  Results are identical either way. */
 
 typedef struct {
   int32_t chain_id;
@@ -167,10 +170,17 @@ int32_t sr_session_block_threads(const sr_session *s);
  * 3 = columns in HBM, split chains: two co-resident workgroups per chain, each owning half of the
  * taxa (1024 threads, 1025..2048 taxa, grid co-resident; SR_SPLIT=0 in the environment disables it). */
 int32_t sr_session_variant(const sr_session *s);
-/* 1 when the session's launches use a kernel compiled at session creation for its exact shape
- * (sites, taxa, hard sites fixed at compile time; SR_JIT=1 in the environment, cached under
- * <package>/build/jit/), 0 for the generic kernel.  Results are identical either way. */
+/* 1 when the session's launches use the sweep kernel compiled for its exact shape (sites, taxa, hard
+ * sites fixed at compile time) -- the default for sessions with occurrence columns in LDS (variant 0) --
+ * 0 for the generic kernel (HBM columns, the pair kernel, SR_F_GENERIC_KERNEL / SR_JIT=0, or the
+ * specialised code object unavailable: one stderr line says why).  Results are identical either way. */
 int32_t sr_session_specialized(const sr_session *s);
+/* Prepare the shape-specialised kernel a session of this dataset and opts (block_threads, SR_F_*_COLUMNS,
+ * SR_F_GENERIC_KERNEL) would run, without a GPU: compiled from the source snapshot the library was built
+ * from (build/spec/) with hipcc into the cache ($SR_JIT_CACHE, else build/jit/ next to the library), so
+ * that session creation finds it.  1 ready, 0 the session runs no specialised kernel, SR_EIO the code
+ * object could not be produced (stderr says why), SR_EUNSUPPORTED / SR_EINVAL as sr_session_create. */
+int sr_specialize(const sr_dataset *ds, const sr_run_opts *opts);
 /* Checkpoint / resume (the reference has none): the full chain state (columns, pi,
    limits, counts, c/d/loglik, MT19937 ring and cursor, acceptance counters) to a file; restoring
    it over the same dataset continues every chain exactly where it stopped.  Records are not kept. */

@@ -35,6 +35,7 @@
 #include "sr_math.h"
 #include "sr_rng.h"
 #include "sr_internal.h"
+#include "seriation.h"
 
 __constant__ double c_zig_y[128] = SR_ZIG_YTAB_INIT;
 __constant__ unsigned int c_zig_k[128] = SR_ZIG_KTAB_INIT;
@@ -44,7 +45,7 @@ __constant__ double c_log_tab[256] = SR_LOG_TAB_INIT;
 
 #define SR_ZIGR 3.44428647676   /* GSL gaussian_ziggurat PARAM_R */
 
-/* Shape specialisation (the run-time-compiled kernels, srk_jit_load): SR_FN / SR_FM / SR_FH fix the
+/* Shape specialisation (the session's kernel compiled for its shape, sr_spec.c): SR_FN / SR_FM / SR_FH fix the
  * dataset's sites, taxa and hard sites at compile time, so the layout offsets, strides, loop bounds and
  * the uniform_int divisors fold into immediates (the generic kernel holds them in ~600 spilled SGPRs).
  * 0 / 0 / -1 (the default): taken from the launch arguments. */
@@ -79,28 +80,28 @@ struct KArgs {
 struct Lay {
   size_t tab, cbuf, lbuf, mt, P, rpi0, rpi1, ht, ck, ccnt, sab, scnt, hpw, hbw, t4, t8, pre, part, tot, xs, ptab, misc, total;
 };
-__host__ __device__ static inline size_t sr_al16(size_t x) { return (x + 15) & ~(size_t)15; }
+__host__ __device__ static constexpr inline size_t sr_al16(size_t x) { return (x + 15) & ~(size_t)15; }
 /* walk words held in registers by the register-column kernels (NWM template argument): 9 for
  * N <= 287, 17 for N <= 543, else 0 (columns walked in LDS, Gibbs checkpoints in LDS) */
-__host__ __device__ static inline int sr_nwm(int N) { const int nk = (N >> 5) + 1; return nk <= 9 ? 9 : (nk <= 17 ? 17 : 0); }
+__host__ __device__ static constexpr inline int sr_nwm(int N) { const int nk = (N >> 5) + 1; return nk <= 9 ? 9 : (nk <= 17 ? 17 : 0); }
 /* the register-column kernels exist for TB 256 and 512 (LDS columns only) */
 /* (and their 32-bit hard-site masks: more than 32 hard sites take the LDS-walk kernels, 64-bit masks;
  * one taxon per thread, M <= TB: the several-taxa branches are compiled out of them) */
-__host__ __device__ static inline bool sr_regwalk(int N, int M, int TB, bool gm, int nh)
+__host__ __device__ static constexpr inline bool sr_regwalk(int N, int M, int TB, bool gm, int nh)
 {
   return !gm && TB <= 512 && M <= TB && sr_nwm(N) > 0 && nh <= 32;
 }
 #define T8STRIDE 514   /* doubles per wave: 256 byte entries {sum, product} + the dead entry {0, 1} */
 /* Gibbs checkpoint slots per word: one per thread that owns a taxon */
-__host__ __device__ static inline int sr_ckstride(int M, int TB) { return M >= TB ? TB : ((M + 63) & ~63); }
+__host__ __device__ static constexpr inline int sr_ckstride(int M, int TB) { return M >= TB ? TB : ((M + 63) & ~63); }
 /* gm: the global-memory variant (columns too large for LDS, e.g. 1024 x 2048): the per-taxon
  * arrays (P, pre, ck, a/b, counts, logl terms, exact-delta terms) live in HBM (chain-private,
  * owner-thread access, L2/MALL-resident) and get no LDS slot */
 /* taxa per exact-delta chunk (one wave's taxa): 64, or 32 in the pair kernels (two lanes per taxon) */
-__host__ __device__ static inline int sr_chunk(bool pr) { return pr ? 32 : 64; }
-__host__ __device__ static inline Lay sr_layout(int N, int M, int NW, int TB, bool gm, bool pr = false, int nh = 0)
+__host__ __device__ static constexpr inline int sr_chunk(bool pr) { return pr ? 32 : 64; }
+__host__ __device__ static constexpr inline Lay sr_layout(int N, int M, int NW, int TB, bool gm, bool pr = false, int nh = 0)
 {
-  Lay L;
+  Lay L{};
   size_t o = 0;
   const int CH = sr_chunk(pr), KT = (M + CH - 1) / CH, NWV = TB / 64;
   const size_t g = gm ? 0 : 1;
@@ -2938,25 +2939,22 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 }
 
 #ifdef SR_JIT
-/* run-time compilation (srk_jit_load): this one instantiation, specialised by SR_FN / SR_FM / SR_FH */
+/* the shape-specialised build (sr_spec.c): this one instantiation, specialised by SR_FN / SR_FM / SR_FH, and
+   its ABI record, which the loader compares with its own before launching (srk_spec_load) */
 template __global__ void sr_sweep_kernel<SR_JIT_TB, SR_JIT_NWM, false>(KArgs);
+__constant__ unsigned long long sr_spec_abi[4] = {
+    sizeof(KArgs), (unsigned long long)SR_JIT_TB | ((unsigned long long)SR_JIT_NWM << 16),
+    (unsigned long long)SR_FN | ((unsigned long long)SR_FM << 16) | ((unsigned long long)(SR_FH & 0xffff) << 32),
+    (unsigned long long)sr_layout(SR_FN, SR_FM, (SR_FN + 31) / 32, SR_JIT_TB, false, false, SR_FH).total};
 #else
 /* ================================================================ session layer */
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
   fprintf(stderr, "seriation: HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); return -5; } } while (0)
 
-#include <dlfcn.h>
-#include <errno.h>
-#include <fcntl.h>
-#include <spawn.h>
-#include <sys/stat.h>
-#include <sys/wait.h>
-#include <unistd.h>
-extern char **environ;
 
 struct srk_dev {
   int device, N, M, NW, nh, nchains, TB, TPT, rec_cap, gm, pr, sp, grid, coop;
-  int jit;                 /* the launch uses the run-time specialised kernel (srk_jit_load) */
+  int jit;                 /* the launch uses the shape-specialised kernel (srk_spec_load) */
   double *dsum;            /* srk_exp_data's per-chain sums (device) */
   hipModule_t mod;
   hipFunction_t jfn;
@@ -3012,132 +3010,143 @@ static sr_kfn sr_pick_kernel(int TB, int N, int M, bool gm, bool pr, int nh, boo
   return nullptr;
 }
 
-/* ---- run-time specialisation (SR_JIT=1 in the environment; bench.py sets it) ------------------
- * The generic kernels take N, M and the hard-site count from their arguments; this compiles the
- * session's one kernel with them fixed (SR_FN / SR_FM / SR_FH: the layout offsets, strides, loop
- * bounds and uniform_int divisors become immediates; the bench kernel's SGPR spills fall from ~590 to
- * ~170; LDS-column kernels) from the package's own csrc/ with the library's flags, once per shape: hipcc --genco in a
- * child process (output to a log file, never to the caller's stdout), the code object cached under
- * <package>/build/jit/ keyed by an FNV-1a hash of the sources and the definitions.  Same source, same
- * -ffp-contract=off: the same arithmetic in the same order, bit-identical results (tests/
- * test_gpu_jit.py).  Any failure (no sources, no compiler, compile error, occupancy) leaves the
- * generic HIP kernel in place; there is no CPU path either way. */
-static uint64_t sr_fnv(uint64_t h, const void *p, size_t n)
-{
-  const unsigned char *b = (const unsigned char *)p;
-  for (size_t i = 0; i < n; ++i) { h ^= b[i]; h *= 1099511628211ull; }
-  return h;
-}
+/* ---- the kernel a session runs ----------------------------------------------------------------
+ * Block size, variant (LDS columns / HBM columns / pair kernel) and LDS bytes from the shape alone (no
+ * HIP call): srk_create launches this plan, srk_plan / sr_specialize report it without a GPU. */
+struct srk_kplan { int TB, pr, gm; size_t lds; };
 
-static int sr_hash_file(const char *path, uint64_t *h)
+static int plan_kernel(int N, int M, int nh, int block_threads, int gm_force, srk_kplan *kp)
 {
-  FILE *f = fopen(path, "rb");
-  if (!f) return -1;
-  unsigned char buf[65536];
-  size_t n;
-  while ((n = fread(buf, 1, sizeof buf, f)) > 0) *h = sr_fnv(*h, buf, n);
-  fclose(f);
+  if (nh > SR_NHMAX || N > 32767 || M > 32767) return -6;
+  const int NW = (N + 31) / 32;
+  int TB = block_threads;
+  /* the pair kernel where it was asked for (two lanes per taxon, 1024 threads), else one thread per
+     taxon in the smallest block of 256..1024 threads that covers M */
+  int pr = (TB <= 0 && gm_force != 1 && nh <= 32 && sr_pair_ok(N, M)) ? 1 : 0;
+  if (pr) TB = 1024;
+  if (TB <= 0) { TB = 256; while (TB < M && TB < 1024) TB *= 2; }
+  /* columns in LDS when the whole layout fits, else the HBM-column variant */
+  int gm = 0;
+  Lay L = sr_layout(N, M, NW, TB, false, pr != 0, nh);
+  if (L.total > 160 * 1024) { gm = 1; L = sr_layout(N, M, NW, TB, true, false, nh); }
+  if (gm_force >= 0 && gm_force != gm) {   /* explicit variant request (tests) */
+    gm = gm_force;
+    L = sr_layout(N, M, NW, TB, gm != 0, pr != 0, nh);
+  }
+  if (gm) pr = 0;
+  if (!sr_pick_kernel(TB, N, M, gm != 0, pr != 0, nh) || L.total > 160 * 1024) return -6;
+  kp->TB = TB; kp->pr = pr; kp->gm = gm; kp->lds = L.total;
   return 0;
 }
 
-static int srk_jit_load(srk_dev *d)
+/* the specialised kernel's shape: LDS-column sessions of the one-thread-per-taxon kernels (the HBM-column
+   split kernel measured 4.4 % slower specialised, profiles/r03z6_ab_jit.json; the pair kernel is opt-in) */
+static bool spec_shape_of(int N, int M, int nh, const srk_kplan &kp, sr_spec_shape *s)
+{
+  if (kp.gm || kp.pr) return false;
+  s->TB = kp.TB;
+  s->NWM = sr_regwalk(N, M, kp.TB, false, nh) ? sr_nwm(N) : 0;
+  s->N = N; s->M = M; s->NH = nh;
+#ifdef SR_FORCE_EXACT
+  s->force = 1;
+#else
+  s->force = 0;
+#endif
+  return true;
+}
+
+extern "C" int srk_plan(int N, int M, int nh, int block_threads, int gm_force, sr_spec_shape *shape)
+{
+  srk_kplan kp;
+  if (int e = plan_kernel(N, M, nh, block_threads, gm_force, &kp)) return e;
+  return spec_shape_of(N, M, nh, kp, shape) ? 1 : 0;
+}
+
+/* ---- shape-specialised kernels (the default for LDS-column sessions; sr_spec.c) -----------------
+ * The generic kernels take N, M and the hard-site count from their launch arguments; at 256 VGPRs and
+ * two waves per SIMD the bench kernel then holds layout offsets, strides, loop bounds and the five
+ * uniform_int divisors' magic numbers in ~590 spilled SGPRs.  The session's kernel compiled with them
+ * fixed (sr_spec.c: from the source snapshot the library was built from, cached) spills ~170.  Same
+ * source and -ffp-contract=off: the same arithmetic in the same order, bit-identical results
+ * (tests/test_gpu_jit.py, and every GPU parity test runs it by default).  The code object's ABI record
+ * (sizeof KArgs, block, walk words, shape, LDS bytes) must equal this library's, else it is not used.
+ * Any failure leaves the generic HIP kernel in place, with one stderr line per reason; there is no CPU
+ * path either way. */
+static int srk_spec_load(srk_dev *d)
 {
 #if defined(SR_STAMPS)
   (void)d;
   return -1;   /* (stamp builds: generic kernels only) */
 #else
-  /* LDS-column kernels only: the HBM-column split kernel measured 4.4 % slower specialised (its
-     register allocation shifts; profiles/r03z6_ab_jit.json) */
-  if (d->gm) return -1;
-  Dl_info info;
-  if (!dladdr((void *)&srk_jit_load, &info) || !info.dli_fname) return -1;
-  /* the package directory: the first ancestor of the library holding csrc/sr_device.hip */
-  char pkg[4096], src[4200], probe[4300];
-  snprintf(pkg, sizeof pkg, "%s", info.dli_fname);
-  bool found = false;
-  for (int up = 0; up < 4 && !found; ++up) {
-    char *sl = strrchr(pkg, '/');
-    if (!sl) break;
-    *sl = 0;
-    snprintf(probe, sizeof probe, "%s/csrc/sr_device.hip", pkg);
-    found = access(probe, R_OK) == 0;
-  }
-  if (!found) return -1;
-  snprintf(src, sizeof src, "%s/csrc/sr_device.hip", pkg);
-  const int nwm = sr_regwalk(d->N, d->M, d->TB, false, d->nh) ? sr_nwm(d->N) : 0;
-  char defs[512];
-  snprintf(defs, sizeof defs, "-DSR_JIT -DSR_JIT_TB=%d -DSR_JIT_NWM=%d -DSR_FN=%d -DSR_FM=%d -DSR_FH=%d%s",
-           d->TB, nwm, d->N, d->M, d->nh,
-#ifdef SR_FORCE_EXACT
-           " -DSR_FORCE_EXACT"
-#else
-           ""
-#endif
-  );
-  const char *flags = "--genco --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-fast-math";
-  uint64_t h = 1469598103934665603ull;
-  h = sr_fnv(h, defs, strlen(defs));
-  h = sr_fnv(h, flags, strlen(flags));
-  static const char *deps[] = {"csrc/sr_device.hip", "csrc/sr_math.h", "csrc/sr_rng.h", "csrc/sr_tables.h",
-                               "csrc/sr_internal.h", "../include/seriation.h"};
-  for (const char *f : deps) {
-    snprintf(probe, sizeof probe, "%s/%s", pkg, f);
-    if (sr_hash_file(probe, &h) != 0) return -1;
-  }
-  char dir[4300], co[4400], tmp[4500], log[4400], inc[4300], csrc[4300];
-  snprintf(dir, sizeof dir, "%s/build/jit", pkg);
-  snprintf(co, sizeof co, "%s/sr_%016llx.co", dir, (unsigned long long)h);
-  if (access(co, R_OK) != 0) {
-    snprintf(probe, sizeof probe, "%s/build", pkg);
-    (void)mkdir(probe, 0755);
-    (void)mkdir(dir, 0755);
-    snprintf(tmp, sizeof tmp, "%s.%d.%p.tmp", co, (int)getpid(), (void *)d);   /* (shard threads may compile together) */
-    snprintf(log, sizeof log, "%s/sr_%016llx.log", dir, (unsigned long long)h);
-    snprintf(inc, sizeof inc, "-I%s/../include", pkg);
-    snprintf(csrc, sizeof csrc, "-I%s/csrc", pkg);
-    const char *e = getenv("SR_HIPCC");
-    const char *hipcc = e ? e : "/opt/rocm/bin/hipcc";
-    if (access(hipcc, X_OK) != 0) return -1;
-    /* argv: the compiler, the flags and definitions split at spaces, includes, output, source */
-    char fl[1024];
-    snprintf(fl, sizeof fl, "%s %s", flags, defs);
-    char *argv[48];
-    int na = 0;
-    argv[na++] = (char *)hipcc;
-    char *sv = nullptr;
-    for (char *t = strtok_r(fl, " ", &sv); t && na < 40; t = strtok_r(nullptr, " ", &sv)) argv[na++] = t;
-    argv[na++] = inc; argv[na++] = csrc;
-    argv[na++] = (char *)"-o"; argv[na++] = tmp;
-    argv[na++] = src; argv[na] = nullptr;
-    posix_spawn_file_actions_t fa;
-    posix_spawn_file_actions_init(&fa);
-    posix_spawn_file_actions_addopen(&fa, 0, "/dev/null", O_RDONLY, 0);
-    posix_spawn_file_actions_addopen(&fa, 1, log, O_WRONLY | O_CREAT | O_TRUNC, 0644);
-    posix_spawn_file_actions_adddup2(&fa, 1, 2);
-    pid_t pid;
-    const int sr = posix_spawn(&pid, hipcc, &fa, nullptr, argv, environ);
-    posix_spawn_file_actions_destroy(&fa);
-    if (sr != 0) return -1;
-    int st = 0;
-    while (waitpid(pid, &st, 0) < 0) {
-      if (errno != EINTR) return -1;
-    }
-    if (!WIFEXITED(st) || WEXITSTATUS(st) != 0 || rename(tmp, co) != 0) {
-      (void)unlink(tmp);
-      fprintf(stderr, "seriation: run-time specialisation failed (%s); the generic kernel runs\n", log);
-      return -1;
-    }
+  srk_kplan kp = {d->TB, d->pr, d->gm, d->lds};
+  sr_spec_shape s;
+  if (!spec_shape_of(d->N, d->M, d->nh, kp, &s)) return -1;
+  char path[4608], log[4700];
+  const int rc = sr_spec_object(&s, path, sizeof path);
+  if (rc) {
+    sr_spec_note(rc, rc == SR_SPEC_ECC ? path : nullptr);
+    return rc;
   }
   char name[128];
-  snprintf(name, sizeof name, "_Z15sr_sweep_kernelILi%dELi%dELb0ELb0ELb0EEv5KArgs", d->TB, nwm);
-  if (hipModuleLoad(&d->mod, co) != hipSuccess) { d->mod = nullptr; return -1; }
-  if (hipModuleGetFunction(&d->jfn, d->mod, name) != hipSuccess) {
-    (void)hipModuleUnload(d->mod); d->mod = nullptr; d->jfn = nullptr;
-    return -1;
+  snprintf(name, sizeof name, "_Z15sr_sweep_kernelILi%dELi%dELb0ELb0ELb0EEv5KArgs", s.TB, s.NWM);
+  unsigned long long abi[4] = {0, 0, 0, 0};
+  const unsigned long long want[4] = {
+      sizeof(KArgs), (unsigned long long)s.TB | ((unsigned long long)s.NWM << 16),
+      (unsigned long long)s.N | ((unsigned long long)s.M << 16) | ((unsigned long long)(s.NH & 0xffff) << 32),
+      (unsigned long long)d->lds};
+  hipDeviceptr_t ga = nullptr;
+  size_t gbytes = 0;
+  const char *what = nullptr;
+  if (hipModuleLoad(&d->mod, path) != hipSuccess) { d->mod = nullptr; what = "hipModuleLoad"; }
+  else if (hipModuleGetFunction(&d->jfn, d->mod, name) != hipSuccess) what = "hipModuleGetFunction";
+  else if (hipModuleGetGlobal(&ga, &gbytes, d->mod, "sr_spec_abi") != hipSuccess || gbytes != sizeof abi ||
+           hipMemcpyDtoH(abi, ga, sizeof abi) != hipSuccess) what = "no ABI record";
+  else if (memcmp(abi, want, sizeof abi) != 0) what = "ABI record differs";
+  if (what) {
+    snprintf(log, sizeof log, "%s (%s)", path, what);
+    sr_spec_note(SR_SPEC_ELOAD, log);
+    if (d->mod) (void)hipModuleUnload(d->mod);
+    d->mod = nullptr; d->jfn = nullptr;
+    return SR_SPEC_ELOAD;
   }
   d->jit = 1;
   return 0;
 #endif
+}
+
+/* public (include/seriation.h): fill the specialised-kernel cache for a dataset without a GPU */
+extern "C" int sr_specialize(const sr_dataset *ds, const sr_run_opts *opts)
+{
+  if (!ds || ds->N <= 0 || ds->M <= 0 || ds->nh < 0) return SR_EINVAL;
+  sr_run_opts o;
+  if (opts) o = *opts;
+  else sr_default_opts(&o);
+  if (o.flags & SR_F_GENERIC_KERNEL) return 0;
+  const int gm_force = (o.flags & SR_F_HBM_COLUMNS) ? 1 : ((o.flags & SR_F_LDS_COLUMNS) ? 0 : -1);
+  sr_spec_shape s;
+  const int r = srk_plan(ds->N, ds->M, ds->nh, o.block_threads, gm_force, &s);
+  if (r <= 0) return r < 0 ? SR_EUNSUPPORTED : 0;
+#if defined(SR_STAMPS)
+  return 0;
+#else
+  char path[4608];
+  const int rc = sr_spec_object(&s, path, sizeof path);
+  if (rc) {
+    sr_spec_note(rc, rc == SR_SPEC_ECC ? path : nullptr);
+    return SR_EIO;
+  }
+  return 1;
+#endif
+}
+
+/* test hook: the cache path of the specialised kernel a session of this shape would load (0), else the
+   sr_spec.c reason or 1 when the session would run no specialised kernel */
+extern "C" int sr_spec_cache_path(int N, int M, int nh, int block_threads, char *path, size_t len)
+{
+  sr_spec_shape s;
+  const int r = srk_plan(N, M, nh, block_threads, -1, &s);
+  if (r <= 0) return 1;
+  return sr_spec_path(&s, path, len);
 }
 
 extern "C" int srk_device_count(void)
@@ -3160,32 +3169,17 @@ static int dev_alloc_copy(srk_dev *d, T **dst, const T *src, size_t n)
 }
 
 extern "C" int srk_create(const sr_state_host *st, int device, int block_threads, int rec_cap_calls, int gm_force,
-                          const uint32_t *pkey, srk_dev **out)
+                          const uint32_t *pkey, int spec, srk_dev **out)
 {
+  srk_kplan kp;
+  if (plan_kernel(st->N, st->M, st->nh, block_threads, gm_force, &kp)) return -6;
   int ndev = srk_device_count();
   if (ndev <= 0 || device < 0 || device >= ndev) return -5;
-  if (st->nh > SR_NHMAX || st->N > 32767 || st->M > 32767) return -6;
   HIPCHK(hipSetDevice(device));
   srk_dev *d = new srk_dev();
   d->device = device; d->N = st->N; d->M = st->M; d->NW = st->NW; d->nh = st->nh; d->nchains = st->nchains;
-  int TB = block_threads;
-  /* default: the pair kernel where it applies (two lanes per taxon, 1024 threads), else one thread
-     per taxon in the smallest block of 256..1024 threads that covers M */
-  d->pr = (TB <= 0 && gm_force != 1 && st->nh <= 32 && sr_pair_ok(st->N, st->M)) ? 1 : 0;
-  if (d->pr) TB = 1024;
-  if (TB <= 0) { TB = 256; while (TB < st->M && TB < 1024) TB *= 2; }
-  d->TB = TB; d->TPT = 1;
-  /* columns in LDS when the whole layout fits, else the HBM-column variant */
-  d->gm = 0;
-  Lay L = sr_layout(st->N, st->M, st->NW, TB, false, d->pr != 0, st->nh);
-  if (L.total > 160 * 1024) { d->gm = 1; L = sr_layout(st->N, st->M, st->NW, TB, true, false, st->nh); }
-  if (gm_force >= 0 && gm_force != d->gm) {   /* explicit variant request (tests) */
-    d->gm = gm_force;
-    L = sr_layout(st->N, st->M, st->NW, TB, d->gm != 0, d->pr != 0, st->nh);
-  }
-  if (d->gm) d->pr = 0;
-  d->lds = L.total;
-  if (!sr_pick_kernel(TB, st->N, st->M, d->gm != 0, d->pr != 0, st->nh) || d->lds > 160 * 1024) { delete d; return -6; }
+  const int TB = kp.TB;
+  d->TB = TB; d->TPT = 1; d->pr = kp.pr; d->gm = kp.gm; d->lds = kp.lds;
   /* split chains (two co-resident workgroups per chain, one taxon per thread): HBM columns at 1024
      threads when the taxa exceed one block but each half fits it, and the whole grid (16 blocks per
      8 chains) is co-resident -- launched cooperatively.  SR_SPLIT=0 disables it, SR_SPLIT=1 also
@@ -3253,10 +3247,7 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
   if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) { srk_destroy(d); return -5; }
   d->own_stream = 1;
   if (hipEventCreate(&d->ev0) == hipSuccess && hipEventCreate(&d->ev1) == hipSuccess) d->have_events = 1;
-  {
-    const char *e = getenv("SR_JIT");
-    if (e && atoi(e) == 1 && !d->pr) (void)srk_jit_load(d);
-  }
+  if (spec) (void)srk_spec_load(d);
   *out = d;
   return 0;
 }

@@ -412,6 +412,15 @@ static int auto_calls_per_launch(const sr_run_opts *o)
   return o->calls_per_launch > 0 ? o->calls_per_launch : 100;
 }
 
+/* The shape-specialised sweep kernel is the default (sr_spec.c; identical results); SR_F_GENERIC_KERNEL or
+   SR_JIT=0 in the environment select the generic one. */
+static int sr_want_specialized(const sr_run_opts *o)
+{
+  if (o->flags & SR_F_GENERIC_KERNEL) return 0;
+  const char *e = getenv("SR_JIT");
+  return !(e && e[0] == '0' && e[1] == 0);
+}
+
 /* A session over `ds`: every chain initialised as main() does (restore == NULL), or its state
    filled by restore(ctx, st) (a checkpoint). */
 static int session_new(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n_chains, const sr_run_opts *opts,
@@ -469,7 +478,7 @@ static int session_new(const sr_dataset *ds, const sr_chain_spec *specs, int32_t
   }
   s->rec_cap = auto_calls_per_launch(&o);
   const int gm_force = (o.flags & SR_F_HBM_COLUMNS) ? 1 : ((o.flags & SR_F_LDS_COLUMNS) ? 0 : -1);
-  rc = srk_create(&st, o.device, o.block_threads, s->rec_cap, gm_force, pkey, &s->dev);
+  rc = srk_create(&st, o.device, o.block_threads, s->rec_cap, gm_force, pkey, sr_want_specialized(&o), &s->dev);
   free(pkey);
   state_free(&st);
   if (rc) { sr_session_destroy(s); return rc == -6 ? SR_EUNSUPPORTED : SR_EDEVICE; }

@@ -39,11 +39,34 @@ typedef struct srk_dev srk_dev;
 extern "C" {
 #endif
 
+/* shape-specialised kernels (sr_spec.c): the code object of sr_sweep_kernel<TB, NWM, false> compiled with
+ * SR_FN = N, SR_FM = M, SR_FH = NH (and SR_FORCE_EXACT when force) */
+typedef struct { int TB, NWM, N, M, NH, force; } sr_spec_shape;
+#define SR_SPEC_ENOSRC (-1)
+#define SR_SPEC_ESTALE (-2)
+#define SR_SPEC_ENOCC (-3)
+#define SR_SPEC_ECC (-4)
+#define SR_SPEC_EPROF (-5)
+#define SR_SPEC_ELOAD (-6)
+/* the cache path of the shape's code object (0), or a reason code */
+int sr_spec_path(const sr_spec_shape *s, char *path, size_t len);
+/* the path of the shape's code object, compiled into the cache first if it is missing (0), or a reason */
+int sr_spec_object(const sr_spec_shape *s, char *path, size_t len);
+const char *sr_spec_reason(int code);
+/* one stderr line per reason and process: the session falls back to the generic kernel */
+void sr_spec_note(int code, const char *detail);
+
 int srk_device_count(void);
 /* gm_force: -1 auto (LDS columns when they fit, else HBM columns), 0 LDS, 1 HBM;
  * pkey: [nchains][2] Philox keys (the SR_F_RNG_PHILOX stream), NULL = MT19937 */
+/* spec: 1 the shape-specialised kernel when the session runs LDS columns (sr_spec.c; the default),
+ * 0 the generic kernel (SR_F_GENERIC_KERNEL, or SR_JIT=0 in the environment) */
 int srk_create(const sr_state_host *st, int device, int block_threads, int rec_cap_calls, int gm_force,
-               const uint32_t *pkey, srk_dev **out);
+               const uint32_t *pkey, int spec, srk_dev **out);
+/* the kernel a session of this shape would run, without a GPU: *lds_cols 1 for LDS columns, *shape the
+ * specialised kernel's shape (valid when the function returns 1); 0 no specialised kernel (HBM columns,
+ * pair kernel), negative: unsupported */
+int srk_plan(int N, int M, int nh, int block_threads, int gm_force, sr_spec_shape *shape);
 int srk_set_stream(srk_dev *d, void *stream);
 /* calls*spc sweeps for all chains; save -> records appended at slot rec_base.. */
 int srk_run(srk_dev *d, int calls, int spc, int save, int rec_base);

@@ -8,7 +8,7 @@ Layers (reference file in parentheses):
   analysis  E[c], E[d], CORRMN, pair-order matrix          (script.py:102-189)
 """
 from ._lib import SrError, LIB_PATH, lib  # noqa: F401
-from .core import Dataset, Session, run_chains, run_to_dirs  # noqa: F401
+from .core import Dataset, Session, run_chains, run_to_dirs, specialize  # noqa: F401
 from . import launcher, analysis, dist  # noqa: F401
 
-__all__ = ["Dataset", "Session", "run_chains", "run_to_dirs", "launcher", "analysis", "dist", "SrError", "lib", "LIB_PATH"]
+__all__ = ["Dataset", "Session", "run_chains", "run_to_dirs", "specialize", "launcher", "analysis", "dist", "SrError", "lib", "LIB_PATH"]

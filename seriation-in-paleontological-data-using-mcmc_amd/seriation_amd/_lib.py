@@ -27,6 +27,7 @@ SR_F_DEBUG_CHECK = 8
 SR_F_DEBUG_PRINT = 16
 SR_F_RNG_PHILOX = 32
 SR_F_DIAG = 64
+SR_F_GENERIC_KERNEL = 128
 
 
 class SrError(RuntimeError):
@@ -84,7 +85,7 @@ PUBLIC_SYMBOLS = [
     "sr_session_state",
     "sr_session_accept_counts", "sr_session_fallback_counts", "sr_session_debug_flagged", "sr_session_last_kernel_ms", "sr_session_block_threads", "sr_session_variant", "sr_session_specialized",
     "sr_session_checkpoint", "sr_session_restore",
-    "sr_session_destroy", "sr_posterior", "sr_session_posterior", "sr_strerror", "sr_device_count", "sr_version",
+    "sr_session_destroy", "sr_specialize", "sr_posterior", "sr_session_posterior", "sr_strerror", "sr_device_count", "sr_version",
 ]
 
 _LIB = None
@@ -135,6 +136,7 @@ def _lib():
         "sr_session_checkpoint": (c_int, [c_void_p, ctypes.c_char_p]),
         "sr_session_restore": (c_int, [P(sr_dataset), ctypes.c_char_p, P(sr_run_opts), P(c_void_p)]),
         "sr_session_destroy": (None, [c_void_p]),
+        "sr_specialize": (c_int, [P(sr_dataset), P(sr_run_opts)]),
         "sr_posterior": (c_int, [P(sr_dataset), P(ctypes.c_int16), c_i32, c_i32, c_i32, c_i32, P(sr_posterior_out)]),
         "sr_session_posterior": (c_int, [c_void_p, P(c_i32), c_i32, c_i32, c_i32, c_i32, P(sr_posterior_out)]),
         "sr_strerror": (ctypes.c_char_p, [c_int]),
@@ -149,6 +151,7 @@ def _lib():
         "sr_host_initial_checkpoint": (c_int, [P(sr_dataset), P(sr_chain_spec), c_i32, ctypes.c_char_p]),
         "sr_host_init_chain": (c_int, [P(sr_dataset), ctypes.c_uint64, P(c_i32), P(c_i32), P(c_i32),
                                        P(c_double), P(ctypes.c_uint64)]),
+        "sr_spec_cache_path": (c_int, [c_int, c_int, c_int, c_int, ctypes.c_char_p, ctypes.c_size_t]),
         "sr_session_debug_counters": (c_int, [c_void_p, P(ctypes.c_ulonglong)]),
         "sr_device_selftest_math": (c_int, [c_int, P(c_double), ctypes.c_long, P(c_double), P(c_double)]),
     }

@@ -73,12 +73,15 @@ class Dataset:
 
 
 def make_opts(burnin_calls=1000, sample_calls=1000, sweeps_per_call=10, device=0, block_threads=0,
-              calls_per_launch=0, check=True, columns="auto", debug_check=False, debug_print=False, rng="mt"):
+              calls_per_launch=0, check=True, columns="auto", debug_check=False, debug_print=False, rng="mt",
+              generic=False):
     """columns: "auto" (LDS when the layout fits, else HBM), "lds" or "hbm" (SR_F_*_COLUMNS).
     debug_check: mcmc_consistent after every mcmc_sample call (the reference's MCMCDEBUG,
     mcmc.c:249-255; SR_F_DEBUG_CHECK), debug_print: its acceptance-rate lines on stderr.
     rng: "mt" (the reference's GSL MT19937 stream, bit-exact) or "philox" (opt-in SR_F_RNG_PHILOX:
-    counter-based Philox4x32-10 per chain for the sampling phase; statistically equivalent only)."""
+    counter-based Philox4x32-10 per chain for the sampling phase; statistically equivalent only).
+    generic: the generic sweep kernel instead of the default shape-specialised one (SR_F_GENERIC_KERNEL;
+    identical results)."""
     o = L.sr_run_opts()
     L.lib().sr_default_opts(ctypes.byref(o))
     o.burnin_calls = burnin_calls
@@ -95,7 +98,19 @@ def make_opts(burnin_calls=1000, sample_calls=1000, sweeps_per_call=10, device=0
         raise ValueError("rng must be 'mt' or 'philox'")
     if rng == "philox":
         o.flags |= L.SR_F_RNG_PHILOX
+    if generic:
+        o.flags |= L.SR_F_GENERIC_KERNEL
     return o
+
+
+def specialize(dataset, block_threads=0, columns="auto"):
+    """sr_specialize: compile (or find cached) the shape-specialised sweep kernel a session over `dataset`
+    would run, without a GPU.  True: ready; False: such a session runs no specialised kernel (HBM columns)."""
+    o = make_opts(block_threads=block_threads, columns=columns)
+    rc = L.lib().sr_specialize(ctypes.byref(dataset.c), ctypes.byref(o))
+    if rc < 0:
+        raise L.SrError(rc, "sr_specialize")
+    return rc == 1
 
 
 def make_specs(seeds, chain_ids=None):
@@ -112,12 +127,13 @@ class Session:
     ``calls`` mcmc_sample calls (mcmc.c:214-258) for every chain."""
 
     def __init__(self, dataset, seeds, device=0, sweeps_per_call=10, calls_per_launch=0, block_threads=0,
-                 chain_ids=None, columns="auto", debug_check=False, rng="mt"):
+                 chain_ids=None, columns="auto", debug_check=False, rng="mt", generic=False):
         self.ds = dataset
         self.n = len(seeds)
         self.specs = make_specs(seeds, chain_ids)
         self.opts = make_opts(sweeps_per_call=sweeps_per_call, device=device, block_threads=block_threads,
-                              calls_per_launch=calls_per_launch, columns=columns, debug_check=debug_check, rng=rng)
+                              calls_per_launch=calls_per_launch, columns=columns, debug_check=debug_check, rng=rng,
+                              generic=generic)
         h = ctypes.c_void_p()
         _check(L.lib().sr_session_create(ctypes.byref(dataset.c), self.specs, self.n, ctypes.byref(self.opts),
                                          ctypes.byref(h)), "sr_session_create")
@@ -165,8 +181,9 @@ class Session:
 
     @property
     def specialized(self):
-        """True when the launches use the kernel compiled at session creation for this dataset's
-        exact shape (SR_JIT=1 in the environment), False for the generic one."""
+        """True when the launches use the sweep kernel compiled for this dataset's exact shape (the default
+        for LDS-column sessions), False for the generic one (HBM columns, generic=True,
+        SR_JIT=0 in the environment, or the specialised code object unavailable)."""
         return bool(L.lib().sr_session_specialized(self.h))
 
     def set_stream(self, stream_handle):
@@ -289,14 +306,15 @@ def _devices(devices):
 
 def run_chains(dataset, seeds, burnin_calls=1000, sample_calls=1000, sweeps_per_call=10, device=0,
                chain_ids=None, keep_records=False, calls_per_launch=0, block_threads=0, columns="auto",
-               devices=None, debug_check=False, rng="mt"):
+               devices=None, debug_check=False, rng="mt", generic=False):
     """sr_run_chains: returns (summaries list of dicts, records or None).
     records = (ab_pi int32 [n, ts, 2M+N], cdl [n, ts, 3]) when keep_records.
     devices: a list of HIP ordinals (may repeat) -> sr_run_chains_multi, chains sharded over them."""
     n = len(seeds)
     specs = make_specs(seeds, chain_ids)
     opts = make_opts(burnin_calls, sample_calls, sweeps_per_call, device, block_threads=block_threads,
-                     calls_per_launch=calls_per_launch, columns=columns, debug_check=debug_check, rng=rng)
+                     calls_per_launch=calls_per_launch, columns=columns, debug_check=debug_check, rng=rng,
+                     generic=generic)
     out = (L.sr_chain_summary * n)()
     N, M = dataset.N, dataset.M
     recs = None

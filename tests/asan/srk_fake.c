@@ -33,9 +33,9 @@ static void *dup(const void *p, size_t n)
 }
 
 int srk_create(const sr_state_host *st, int device, int block_threads, int rec_cap_calls, int gm_force,
-               const uint32_t *pkey, srk_dev **out)
+               const uint32_t *pkey, int spec, srk_dev **out)
 {
-  (void)block_threads; (void)gm_force; (void)pkey;
+  (void)block_threads; (void)gm_force; (void)pkey; (void)spec;
   if (device < 0 || device >= 2) return -5;
   srk_dev *d = (srk_dev *)calloc(1, sizeof(*d));
   if (!d) return -5;

@@ -8,9 +8,9 @@
 
 int srk_device_count(void) { return 0; }
 int srk_create(const sr_state_host *st, int device, int block_threads, int rec_cap_calls, int gm_force,
-               const uint32_t *pkey, srk_dev **out)
+               const uint32_t *pkey, int spec, srk_dev **out)
 {
-  (void)st; (void)device; (void)block_threads; (void)rec_cap_calls; (void)gm_force; (void)pkey; (void)out;
+  (void)st; (void)device; (void)block_threads; (void)rec_cap_calls; (void)gm_force; (void)pkey; (void)spec; (void)out;
   return -5;
 }
 int srk_set_stream(srk_dev *d, void *s) { (void)d; (void)s; return -5; }

@@ -71,3 +71,40 @@ def test_config5_parity_one_workgroup(config5, monkeypatch):
         assert rc == 0
         np.testing.assert_array_equal(ri[k], oi, err_msg="seed %d" % s)
         assert np.array_equal(rd[k].view(np.uint64), od.view(np.uint64)), s
+
+
+def test_config5_100_chains_split_grid(config5):
+    """The benched config-5 grid: 100 chains on the split kernel = 13 block groups of 8 chains (blocks
+    16 g + 8 h + x hold chain 8 g + x, half h), the last group ragged (4 chains).  (a) Sharded == unsharded:
+    the 100-chain session's records equal those of two sessions of 37 and 63 chains (other groups, other
+    ragged tails) for every chain; (b) one chain of every block group, the ragged group's first and last
+    included, equals the oracle for 10 saved calls (oracle on 13 threads).  mcmc.c:918-996, 1127-1682."""
+    from concurrent.futures import ThreadPoolExecutor
+    ds = sa.Dataset.parse(config5, maxs=0)
+    ids = list(range(100))
+    calls = 10
+    with sa.Session(ds, [i + 1 for i in ids], chain_ids=ids, calls_per_launch=calls) as s:
+        assert s.kernel == "split"
+        s.run(calls, save=True)
+        ab, cdl = s.fetch_records()
+    parts = []
+    for lo, hi in ((0, 37), (37, 100)):
+        with sa.Session(ds, [i + 1 for i in ids[lo:hi]], chain_ids=ids[lo:hi], calls_per_launch=calls) as s:
+            assert s.kernel == "split"
+            s.run(calls, save=True)
+            parts.append(s.fetch_records())
+    np.testing.assert_array_equal(np.concatenate([p[0] for p in parts]), ab)
+    assert np.array_equal(np.concatenate([p[1] for p in parts]).view(np.uint64), cdl.view(np.uint64))
+    picks = [0, 9, 17, 25, 34, 42, 50, 59, 67, 75, 84, 96, 99]   # groups 0..12; 96 and 99 in the ragged group
+
+    def one(i):
+        o = oracle_ref.run_chain(config5, i + 1, 0, calls, maxs=0)
+        return o["rc"], o["rec_int"].copy(), o["rec_dbl"].copy()
+
+    with ThreadPoolExecutor(len(picks)) as ex:
+        ref = list(ex.map(one, picks))
+    assert sorted({i // 8 for i in picks}) == list(range(13))
+    for i, (rc, ri, rdb) in zip(picks, ref):
+        assert rc == 0
+        assert np.array_equal(ab[i].astype(np.int32), ri), "chain %d: integers differ from the oracle" % i
+        assert np.array_equal(cdl[i].view(np.uint64), rdb.view(np.uint64)), "chain %d: c/d/loglik differ" % i

@@ -87,25 +87,51 @@ def test_parity_synth_256x512():
     _compare_chains("synth_256x512.txt", [1, 2], tb=1, ts=3)
 
 
-def test_parity_config3_100_chains_200_calls():
-    """BASELINE config 3's workload (synthetic 256x512, 100 chains) for 200 saved calls (2000
-    sweeps) per chain: every saved sample of every chain against the oracle (run on 16 threads)."""
+_ORACLE = {}
+
+
+def _oracle_runs(text, seeds, tb, ts):
+    """The oracle's (rc, sha256 of the integer records, c/d/loglik records, exp_data) per seed, on 16 threads;
+    kept for the second kernel build of the same case."""
     import hashlib
     from concurrent.futures import ThreadPoolExecutor
+    key = (hashlib.sha256(text).hexdigest(), tuple(seeds), tb, ts)
+    if key not in _ORACLE:
+        def one(s):
+            o = oracle_ref.run_chain(text, s, tb, ts, maxs=0)
+            return (o["rc"], hashlib.sha256(np.ascontiguousarray(o["rec_int"], "<i4").tobytes()).hexdigest(),
+                    o["rec_dbl"].copy(), np.asarray(o["exp"]).copy())
+
+        with ThreadPoolExecutor(min(16, os.cpu_count() or 1)) as ex:
+            _ORACLE.clear()   # one case at a time: the 100-chain records are large
+            _ORACLE[key] = list(ex.map(one, seeds))
+    return _ORACLE[key]
+
+
+def _run_build(ds, seeds, tb, ts, kernel):
+    """sr_run_chains with the shape-specialised kernel (the default) or the generic one; asserts the build ran."""
+    generic = kernel == "generic"
+    with sa.Session(ds, seeds[:1], generic=generic) as s:
+        assert s.specialized == (not generic), "%s leg: specialized=%s" % (kernel, s.specialized)
+    return sa.run_chains(ds, seeds, burnin_calls=tb, sample_calls=ts, keep_records=True, generic=generic)
+
+
+KERNELS = pytest.mark.parametrize("kernel", ["specialized", "generic"])
+
+
+@KERNELS
+def test_parity_config3_100_chains_200_calls(kernel):
+    """BASELINE config 3's workload (synthetic 256x512, 100 chains) for 200 saved calls (2000
+    sweeps) per chain: every saved sample of every chain against the oracle (run on 16 threads), on the
+    default shape-specialised kernel (the benched one) and on the generic kernel."""
+    import hashlib
     text = _text("synth_256x512.txt")
     ds = sa.Dataset.parse(text, maxs=0)
     seeds = list(range(1, 101))
-    summ, (ri, rd) = sa.run_chains(ds, seeds, burnin_calls=0, sample_calls=200, keep_records=True)
-
-    def one(s):
-        o = oracle_ref.run_chain(text, s, 0, 200, maxs=0)
-        return (o["rc"], hashlib.sha256(np.ascontiguousarray(o["rec_int"], "<i4").tobytes()).hexdigest(),
-                o["rec_dbl"].copy())
-
-    with ThreadPoolExecutor(min(16, os.cpu_count() or 1)) as ex:
-        ref = list(ex.map(one, seeds))
+    summ, (ri, rd) = _run_build(ds, seeds, 0, 200, kernel)
+    ref = _oracle_runs(text, seeds, 0, 200)
     bad = []
-    for k, (rc, dig, od) in enumerate(ref):
+    for k, (rc, dig, od, _) in enumerate(ref):
         assert rc == 0
         if hashlib.sha256(np.ascontiguousarray(ri[k], "<i4").tobytes()).hexdigest() != dig or \
                 not np.array_equal(rd[k].view(np.uint64), od.view(np.uint64)):
@@ -114,25 +140,18 @@ def test_parity_config3_100_chains_200_calls():
     assert not bad, "chains differing from the oracle: %s" % bad
 
 
-def test_parity_config3_reference_protocol():
+@KERNELS
+def test_parity_config3_reference_protocol(kernel):
     """The reference CLI's own protocol (tb = 1000 burn-in calls, then ts = 1000 saved calls, mcmc.c:
     140-185) at BASELINE config 3's size (synthetic 256x512): 16 chains, i.e. 20 000 sweeps each, well
     into the converged regime; every one of the 1000 saved samples of every chain and its exp_data
-    summary against the oracle, bit for bit (oracle on 16 threads, ~30 s)."""
+    summary against the oracle, bit for bit (oracle on 16 threads, ~30 s), on both kernel builds."""
     import hashlib
-    from concurrent.futures import ThreadPoolExecutor
     text = _text("synth_256x512.txt")
     ds = sa.Dataset.parse(text, maxs=0)
     seeds = list(range(201, 217))
-    summ, (ri, rd) = sa.run_chains(ds, seeds, burnin_calls=1000, sample_calls=1000, keep_records=True)
-
-    def one(s):
-        o = oracle_ref.run_chain(text, s, 1000, 1000, maxs=0)
-        return (o["rc"], hashlib.sha256(np.ascontiguousarray(o["rec_int"], "<i4").tobytes()).hexdigest(),
-                o["rec_dbl"].copy(), np.asarray(o["exp"]).copy())
-
-    with ThreadPoolExecutor(min(16, os.cpu_count() or 1)) as ex:
-        ref = list(ex.map(one, seeds))
+    summ, (ri, rd) = _run_build(ds, seeds, 1000, 1000, kernel)
+    ref = _oracle_runs(text, seeds, 1000, 1000)
     bad = []
     for k, (rc, dig, od, oexp) in enumerate(ref):
         assert rc == 0

@@ -58,3 +58,23 @@ def test_bench_under_launcher_equals_single_process():
     for k in ("exp_c", "exp_d", "corr_mn"):
         assert a[k] == b[k], k
     assert a["samples_per_chain"] == b["samples_per_chain"] == 40
+
+
+def test_bench_two_ranks_on_one_gpu_equals_single_process():
+    """bench.py's N>1 path end to end on the one-GPU box: `--gpus 2` launches two ranks itself
+    (torch.distributed.run children), both on device 0 (--device-of-rank 0,0) with gloo collectives (RCCL
+    cannot host two ranks on one GPU); rank 1 owns chains 24..47, the summary all-gather, the one-sigma
+    selection on every rank, the record gather from non-zero owners and the max-over-ranks timing all run.
+    The selection, the gathered records and E[c] / E[d] / CORRMN must equal a single process running all
+    48 chains (script.py:55-99), and both lines' parity legs must match the oracle."""
+    common = ["--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--calls-per-step", "20"]
+    single = _bench_line([sys.executable, "bench.py", "--gpus", "1", "--chains-per-gpu", "48"] + common)
+    two = _bench_line([sys.executable, "bench.py", "--gpus", "2", "--chains-per-gpu", "24", "--device-of-rank", "0,0",
+                       "--dist-backend", "gloo"] + common)
+    assert two["n_gpus"] == 2 and two["config"]["chains"] == 48 and "gloo" in two["config"]["parallelism"]
+    a, b = single["selection"], two["selection"]
+    assert a["chains_selected"] == b["chains_selected"] and len(a["chains_selected"]) >= 1
+    assert a["records_sha256"] == b["records_sha256"]
+    for k in ("exp_c", "exp_d", "corr_mn"):
+        assert a[k] == b[k], k
+    assert single["parity"]["match"] and two["parity"]["match"]

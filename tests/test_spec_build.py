@@ -1,0 +1,139 @@
+"""Shape-specialised sweep kernels at the boundary (csrc/sr_spec.c, sr_specialize; CPU only, no GPU):
+the code object is compiled from the source snapshot taken with the library (build/spec/), cached under a
+key that covers the snapshot, the definitions, the flags, the target and the compiler's ROCm version, and
+never compiled from a snapshot that differs from the one the library was built from or while a profiler
+tool library is preloaded.  Each scenario runs in a fresh interpreter (the library resolves its snapshot
+and compiler version once per process).  On the GPU, tests/test_gpu_jit.py loads and runs these objects."""
+import json
+import os
+import shutil
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "seriation-in-paleontological-data-using-mcmc_amd")
+LIBDIR = os.path.join(PKG, "build")
+SYNTH = os.path.join(ROOT, "tests", "golden", "datasets", "synth_256x512.txt")
+HIPCC = "/opt/rocm/bin/hipcc"
+BENCH_KERNEL = b"_Z15sr_sweep_kernelILi512ELi9ELb0ELb0ELb0EEv5KArgs"
+
+needs_hipcc = pytest.mark.skipif(not os.access(HIPCC, os.X_OK), reason="no hipcc")
+
+# runs in a child: prints one JSON line {"rc": sr_specialize's result, "path": the cache path (or reason)}
+CHILD = textwrap.dedent("""
+    import ctypes, json, sys
+    sys.path.insert(0, %r)
+    import seriation_amd as sa
+    from seriation_amd import _lib as L
+    ds = sa.Dataset.load(sys.argv[1], maxs=0)
+    buf = ctypes.create_string_buffer(4096)
+    prc = sa.lib().sr_spec_cache_path(ds.N, ds.M, ds.nh, int(sys.argv[2]), buf, 4096)
+    o = sa.core.make_opts(block_threads=int(sys.argv[2]))
+    rc = sa.lib().sr_specialize(ctypes.byref(ds.c), ctypes.byref(o))
+    print(json.dumps({"rc": rc, "path_rc": prc, "path": buf.value.decode()}))
+""" % PKG)
+
+
+def child(env_extra, dataset=SYNTH, block_threads=0, lib=None):
+    env = dict(os.environ)
+    env.pop("SR_JIT_CACHE", None)
+    env.update(env_extra)
+    if lib:
+        env["SERIATION_LIB"] = lib
+    r = subprocess.run([sys.executable, "-c", CHILD, dataset, str(block_threads)], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1]), r.stderr
+
+
+def test_snapshot_matches_sources_and_library_hash():
+    """build/spec/ holds exactly the kernel sources, and the hash tool's value is the one compiled in."""
+    for name, src in [("sr_device.hip", "csrc"), ("sr_math.h", "csrc"), ("sr_rng.h", "csrc"), ("sr_tables.h", "csrc"),
+                      ("sr_internal.h", "csrc"), ("seriation.h", os.path.join("..", "include"))]:
+        with open(os.path.join(PKG, src, name), "rb") as a, open(os.path.join(LIBDIR, "spec", name), "rb") as b:
+            assert a.read() == b.read(), "%s: snapshot differs from the sources (run make)" % name
+    h = subprocess.check_output([os.path.join(LIBDIR, "srhash"), os.path.join(LIBDIR, "spec")], text=True).strip()
+    with open(os.path.join(LIBDIR, "spec.hash")) as fh:
+        assert fh.read().strip() == h
+
+
+@needs_hipcc
+def test_specialize_compiles_once_into_the_cache(tmp_path):
+    out, err = child({"SR_JIT_CACHE": str(tmp_path)})
+    assert out["rc"] == 1 and out["path_rc"] == 0, (out, err)
+    assert os.path.dirname(out["path"]) == str(tmp_path)
+    blob = open(out["path"], "rb").read()
+    assert BENCH_KERNEL in blob and b"sr_spec_abi" in blob
+    # one kernel only: the specialised build excludes the session layer and every other instantiation
+    assert blob.count(b"_Z15sr_sweep_kernelILi") == blob.count(BENCH_KERNEL)
+    mtime = os.stat(out["path"]).st_mtime_ns
+    out2, _ = child({"SR_JIT_CACHE": str(tmp_path)})
+    assert out2 == out and os.stat(out["path"]).st_mtime_ns == mtime   # a cache hit, not a recompile
+    assert not [f for f in os.listdir(tmp_path) if f.endswith(".tmp")]
+
+
+def test_key_covers_shape_block_and_compiler_version(tmp_path, datasets_dir):
+    base, _ = child({"SR_JIT_CACHE": str(tmp_path), "SR_HIPCC": "/nonexistent/bin/hipcc"})
+    g10, _ = child({"SR_JIT_CACHE": str(tmp_path), "SR_HIPCC": "/nonexistent/bin/hipcc"},
+                   dataset=os.path.join(datasets_dir, "g10s10.txt"))
+    tb512, _ = child({"SR_JIT_CACHE": str(tmp_path), "SR_HIPCC": "/nonexistent/bin/hipcc"},
+                     dataset=os.path.join(datasets_dir, "g10s10.txt"), block_threads=512)
+    # a compiler of another ROCm release: <hipcc>/../.info/version
+    fake = tmp_path / "rocm"
+    (fake / "bin").mkdir(parents=True)
+    (fake / ".info").mkdir()
+    (fake / ".info" / "version").write_text("9.9.9-test\n")
+    cc = fake / "bin" / "hipcc"
+    cc.write_text("#!/bin/sh\nexit 3\n")
+    cc.chmod(0o755)
+    other, err = child({"SR_JIT_CACHE": str(tmp_path), "SR_HIPCC": str(cc)})
+    assert all(o["path_rc"] == 0 for o in (base, g10, tb512, other))
+    paths = {base["path"], g10["path"], tb512["path"], other["path"]}
+    assert len(paths) == 4, paths
+    # no compiler: nothing cached -> SR_EIO and one line on stderr; a failing compiler likewise
+    assert base["rc"] == -7 and other["rc"] == -7
+    assert "compile failed" in err and ".log" in err
+    assert not os.path.exists(other["path"])
+
+
+@needs_hipcc
+def test_entry_under_another_key_is_not_used(tmp_path, datasets_dir):
+    """A code object cached under another shape's key is never picked up: the bench shape compiles its own."""
+    other, _ = child({"SR_JIT_CACHE": str(tmp_path)}, dataset=os.path.join(datasets_dir, "g10s10.txt"))
+    assert other["rc"] == 1
+    junk = open(other["path"], "rb").read()
+    out, _ = child({"SR_JIT_CACHE": str(tmp_path)})
+    assert out["rc"] == 1 and out["path"] != other["path"]
+    blob = open(out["path"], "rb").read()
+    assert blob != junk and BENCH_KERNEL in blob
+
+
+def test_profiler_preload_never_compiles(tmp_path):
+    # (rocprofv3 exports ROCPROF_* settings for its tool library; the variable alone loads nothing)
+    out, err = child({"SR_JIT_CACHE": str(tmp_path), "ROCPROF_OUTPUT_PATH": str(tmp_path / "prof")})
+    assert out["rc"] == -7 and "profiler" in err
+    assert os.listdir(tmp_path) == [] or not [f for f in os.listdir(tmp_path) if f.endswith(".co")]
+
+
+def test_stale_snapshot_is_refused(tmp_path):
+    """A library whose snapshot was edited after the build (sources changed without a rebuild) compiles
+    nothing: the kernel it would compile would not match its KArgs / LDS layout."""
+    lib = tmp_path / "libseriation.so"
+    shutil.copy(os.path.join(LIBDIR, "libseriation.so"), lib)
+    shutil.copytree(os.path.join(LIBDIR, "spec"), tmp_path / "spec")
+    with open(tmp_path / "spec" / "sr_internal.h", "a") as fh:
+        fh.write("\n/* edited after the build */\n")
+    out, err = child({"SR_JIT_CACHE": str(tmp_path / "cache")}, lib=str(lib))
+    assert out["path_rc"] == -2 and out["rc"] == -7
+    assert "differs from the sources the library was built from" in err
+    assert not (tmp_path / "cache").exists()
+
+
+def test_hbm_sessions_have_no_specialised_kernel(tmp_path):
+    import seriation_amd as sa
+    from test_gpu_edge import make_text
+    ds = sa.Dataset.parse(make_text(64, 1100, 6, seed=64 * 1000 + 1100), maxs=0)
+    assert sa.specialize(ds, columns="hbm") is False

@@ -61,7 +61,10 @@ typedef struct {
   int32_t burnin_calls;      /* tb: mcmc_sample calls before saving (mcmc.c:107, default 1000) */
   int32_t sample_calls;      /* ts: saved mcmc_sample calls (default 1000) */
   int32_t sweeps_per_call;   /* sweeps per mcmc_sample (mcmc.c:225, default 10) */
-  int32_t manycd;            /* 0 only: the reference CLI cannot reach manycd=1 */
+  int32_t manycd;            /* mcmc_readmodel's manycd (mcmc.h:40, mcmc.c:118): 0 = c, d shared by all taxa (the
+                                reference CLI's default and script.py's); nonzero = per-taxon c[m], d[m] drawn one
+                                after another each sweep (mcmc.c:777-786, 807-816) -- the exact (slower) kernel
+                                paths, block_threads 0 or 1024 */
   int32_t device;            /* HIP device ordinal */
   int32_t block_threads;     /* threads per chain workgroup, 0 = auto */
   int32_t calls_per_launch;  /* mcmc_sample calls per kernel launch, 0 = auto */
@@ -93,7 +96,8 @@ typedef struct {
 typedef struct {
   int32_t N, M;
   const int32_t *a, *b, *pi;  /* M, M, N: one mcmc_save_chain line */
-  double c, d, loglik;        /* log P(false 1), log P(false 0) (all taxa share them), loglik */
+  double c, d, loglik;        /* log P(false 1), log P(false 0) (manycd: taxon 0's), loglik */
+  const double *cv, *dv;      /* manycd: every taxon's c[M], d[M]; NULL when all taxa share c, d */
 } sr_record;
 
 /* Called once per saved sample, per chain in sample order; return nonzero to abort. */
@@ -144,6 +148,10 @@ int sr_session_reset_records(sr_session *s);
    (either may be NULL). */
 int sr_session_fetch_chain_records(sr_session *s, int32_t chain, int32_t first, int32_t count, int16_t *ab_pi,
                                    double *cdl);
+/* manycd sessions: the per-taxon c, d of buffered records [first, first + count): cdv [n_chains][count][2M]
+   (c[M] then d[M], log values as mcmc_save_chain exponentiates them); SR_EINVAL for manycd = 0 sessions. */
+int sr_session_fetch_cd_vectors(sr_session *s, int32_t first, int32_t count, double *cdv);
+int32_t sr_session_manycd(const sr_session *s);
 /* compute_exp_data / print_exp_data (mcmc.c:53-67) of every chain over its buffered records [first,
    first + count): out[c] = {chain_id, 0, sum(-loglik) / 1000, sum(e^c) / 1000, sum(e^d) / 1000}, sums in
    sample order, the reference's hard-coded divisor (exact means when count = 1000). */

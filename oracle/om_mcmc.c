@@ -712,11 +712,28 @@ OM_API int oracle_parse(const char *text, long len, int maxs, int *N, int *M, in
 static int g_rng_philox = 0;
 OM_API void oracle_set_rng(int philox) { g_rng_philox = philox ? 1 : 0; }
 
+/* rec_cdv (optional, manycd runs): ts*2M doubles = every taxon's c then d per saved sample */
+OM_API int oracle_run_chain_v(const char *text, long len, int maxs, unsigned long seed, int manycd,
+                              int tb, int ts, int sweeps, int check,
+                              int32_t *init_out, double *init_dbl,
+                              int32_t *rec_int, double *rec_dbl, double *rec_cdv, double *exp_out,
+                              long long *acc_out, unsigned long long *rng_words);
+
 OM_API int oracle_run_chain(const char *text, long len, int maxs, unsigned long seed, int manycd,
                             int tb, int ts, int sweeps, int check,
                             int32_t *init_out, double *init_dbl,
                             int32_t *rec_int, double *rec_dbl, double *exp_out,
                             long long *acc_out, unsigned long long *rng_words)
+{
+  return oracle_run_chain_v(text, len, maxs, seed, manycd, tb, ts, sweeps, check, init_out, init_dbl, rec_int, rec_dbl,
+                            NULL, exp_out, acc_out, rng_words);
+}
+
+OM_API int oracle_run_chain_v(const char *text, long len, int maxs, unsigned long seed, int manycd,
+                              int tb, int ts, int sweeps, int check,
+                              int32_t *init_out, double *init_dbl,
+                              int32_t *rec_int, double *rec_dbl, double *rec_cdv, double *exp_out,
+                              long long *acc_out, unsigned long long *rng_words)
 {
   om_model x;
   int rc = om_readmodel(&x, text, (size_t)len, maxs, manycd);
@@ -745,6 +762,10 @@ OM_API int oracle_run_chain(const char *text, long len, int maxs, unsigned long 
       for (int n = 0; n < N; n++) r[2 * M + n] = x.pi[n];
     }
     if (rec_dbl) { rec_dbl[3 * i] = x.c[0]; rec_dbl[3 * i + 1] = x.d[0]; rec_dbl[3 * i + 2] = x.loglik; }
+    if (rec_cdv) {
+      memcpy(rec_cdv + (size_t)i * 2 * M, x.c, (size_t)M * sizeof(double));
+      memcpy(rec_cdv + (size_t)i * 2 * M + M, x.d, (size_t)M * sizeof(double));
+    }
     ls += -(x.loglik);                  /* compute_exp_data, mcmc.c:53-58 (libm exp there) */
     cs += exp(x.c[0]);
     ds += exp(x.d[0]);

@@ -2,7 +2,8 @@
  * mcmc_cli.c -- the drop-in `mcmc` executable (reference CLI, mcmc.c:102-210):
  *
  *   env GSL_RNG_SEED=42 ./mcmc <chain_index> < dataset.txt
- *   ./mcmc manycd Tburnin T < dataset.txt      (manycd must be 0; chain index 0)
+ *   ./mcmc manycd Tburnin T < dataset.txt      (chain index 0: Chains/chain_00; the reference's own binary
+ *                                             reads its unset chain index there and crashes, mcmc.c:153)
  *
  * Reads the dataset on stdin (fgets(MAXS) semantics), seeds MT19937 from GSL_RNG_SEED
  * (strtoul base 0, unset -> GSL default), runs the chain on the GPU and writes

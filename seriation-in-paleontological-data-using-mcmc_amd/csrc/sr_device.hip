@@ -74,6 +74,8 @@ struct KArgs {
   uint32_t *pkey;            /* [chain][2] Philox keys (SR_F_RNG_PHILOX), else null: MT19937 */
   double *gck, *glbuf, *gcbuf;   /* gm variant scratch: Gibbs checkpoints, logl terms, exact-delta terms */
   int *xflag, *xbuf, *xerr;      /* split chains (SP kernels): [chain][2] progress flags, exchange slots, timeout flag */
+  double *cdv, *cdx;   /* manycd (MCD kernels): [chain][2M] per-taxon c, d (state); [chain][2M] their cc, dd (scratch) */
+  double *rec_cdv;     /* manycd: [chain][rec_cap][2M] per-taxon c, d of every saved sample */
 };
 
 /* ---------------------------------------------------------------- LDS carve */
@@ -1790,11 +1792,14 @@ __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, 
 /* GM: terms in HBM (exact_sum_gm).  SP (split chains): this half evaluates its own taxa [olo, ohi)
  * (whole chunks), the terms and counts go through the exchange (xsync: both halves' writes done),
  * and both halves compute the same sum. */
+/* kv (manycd sessions, MCD kernels): per-taxon c, d ([2M]) and cc, dd ([2M]) replace K's shared ones in
+ * each taxon's term (mcmc.c:1212-1214 reads c, d per taxon) */
 template <bool PR, bool GM, bool SP, typename XSync>
 __device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const int32_t *sab, const uint32_t *P, const uint16_t *pre,
                                               int M, int KT, int olo, int ohi,
                                               int hl, int nh, const int16_t *hcnt, const int16_t *nhall, double *cb, int *cc, double *xs,
-                                              int lane, int wave, int TB, XSync &&xsync)
+                                              int lane, int wave, int TB, XSync &&xsync, const double *kv = nullptr,
+                                              const double *kx = nullptr)
 {
   constexpr int CH = PR ? 32 : 64;
   const bool ev = PR ? (lane & 1) == 0 : true;
@@ -1804,7 +1809,9 @@ __device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const i
     if (m < M && ev)
       taxon_dt(kind, q, sab[m], sab[M + m], P + m, pre + m, M, kind == PK_PI3 ? hard_bits_col<uint64_t>(P + m, M, hl, nh) : 0ull,
                hcnt, nhall, dt0, dt1);
-    const double tv = (m < M && ev) ? qval(dt0, -dt0, dt1, -dt1, K) : 0.0;
+    CD Km = K;
+    if (kv && m < M) { Km.c = kv[m]; Km.d = kv[M + m]; Km.cc = kx[m]; Km.dd = kx[M + m]; }
+    const double tv = (m < M && ev) ? qval(dt0, -dt0, dt1, -dt1, Km) : 0.0;
     const uint64_t msk = __ballot(tv != 0.0);
     const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
     if (tv != 0.0) { if constexpr (SP) xst(cb + ch * CH + pos, tv); else cb[ch * CH + pos] = tv; }
@@ -1829,10 +1836,15 @@ __device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const i
  *   B  Gibbs (a_m, b_m) of own taxa (mcmc_sampleab); [barrier + logl on the last sweep]
  *   C  16 MH permutation proposals: draws, own taxa's count deltas and terms, per-wave
  *      partial sums -> one barrier -> certified decision -> apply to own taxa. */
-template <int TB, int NWM, bool GM, bool PR = false, bool SP = false>
+/* MCD (manycd = 1, mcmc.c:777-786, 807-816): per-taxon c_m, d_m drawn one after another from Beta(1 + f1_m,
+ * 1 + t0_m) / Beta(1 + f0_m, 1 + t1_m), every Gibbs draw, logl term and proposal delta with its taxon's own
+ * coefficients -- the exact paths throughout (per-taxon step ratios leave nothing to share or certify by
+ * integer sums).  One taxon or more per thread, one workgroup per chain, LDS or HBM columns. */
+template <int TB, int NWM, bool GM, bool PR = false, bool SP = false, bool MCD = false>
 __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 {
   static_assert(!SP || (GM && !PR && NWM == 0), "split chains: HBM-column kernels only");
+  static_assert(!MCD || (!PR && !SP && NWM == 0), "manycd: generic one-workgroup kernels only");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NWV = TB / 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1933,6 +1945,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   wsync();
   double c = A.cdl[(size_t)chain * 4 + 0];
   double d = A.cdl[(size_t)chain * 4 + 1];
+  double *cv = MCD ? A.cdv + (size_t)chain * 2 * M : nullptr;   /* manycd: c[M], d[M] (HBM state, updated in place) */
+  double *cx = MCD ? A.cdx + (size_t)chain * 2 * M : nullptr;   /* manycd: log(1 - e^c[m]), log(1 - e^d[m]) */
   double loglik = A.cdl[(size_t)chain * 4 + 2];   /* identical in every thread */
   DRng R;
   R.ring = ring;
@@ -2002,7 +2016,25 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           s0 += xld(yt); s1 += xld(yt + 1); s2 += xld(yt + 2); s3 += xld(yt + 3);
         }
         /* mcmc_samplec then mcmc_sampled: Beta(1 + f1, 1 + t0), Beta(1 + f0, 1 + t1) */
-        if (!draw_cd_fast(R, c, d, s3, s0, s1, s2, tb, lane)) {
+        if constexpr (MCD) {
+          /* manycd: c_m for m = 0..M-1, then d_m, each a GSL beta of the taxon's own counts (mcmc.c:777-786,
+             807-816), in the reference's order from the one stream: every thread evaluates the same sequence
+             (block-wide ring refills), thread 0 stores; then each thread its taxa's log(1 - e^x) */
+          for (int k = 0; k < 2; ++k)
+            for (int m = 0; m < M; ++m) {
+              const double y = d_samplebeta<false>(R, cv[k * M + m], (double)(k ? scnt[M + m] : scnt[3 * M + m]),
+                                                   (double)(k ? scnt[2 * M + m] : scnt[m]), k ? SR_MIND : SR_MINC,
+                                                   k ? SR_MAXD : SR_MAXC, tid, TB, tb);
+              __syncthreads();   /* every thread has read cv[k M + m] */
+              if (tid == 0) cv[k * M + m] = y;
+            }
+          __syncthreads();
+          for (int m = tid; m < 2 * M; m += TB) cx[m] = sr_log_m(1. - sr_exp_m(cv[m], &tb), &tb);
+          __syncthreads();
+          c = cv[0];
+          d = cv[M];
+          if (tid == 0) { misc[MS_ACC + 0] += M - 1; misc[MS_ACC + 1] += M - 1; }   /* samplec returns M (mcmc.c:785) */
+        } else if (!draw_cd_fast(R, c, d, s3, s0, s1, s2, tb, lane)) {
           if (tid == 0) misc[MS_CDSEQ]++;
           double cd2[2] = {c, d};
           for (int k = 0; k < 2; ++k)
@@ -2097,6 +2129,21 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             nb = N - draw_pair9(wk, hf, Pm, M, N, NW, true, N - b0, N - na, POb, ub, K, tb, vA, vB, T4w, T8w, &misc[MS_FBK],
                                 d0, e0, d1, e1);
             t0 += d0; f0 += e0; t1 += d1; f1 += e1;
+          } else if constexpr (MCD) {   /* manycd: the taxon's own coefficients, the exact reference walk */
+            const uint16_t *prem = pre + m;
+            const int POa = col_pre(prem, Pm, M, a0);
+            const int POb = (int)prem[NW * M] - col_pre(prem, Pm, M, b0);
+            CD Km = K;
+            Km.c = cv[m]; Km.d = cv[M + m]; Km.cc = cx[m]; Km.dd = cx[M + m];
+            for (int pass = 0; pass < 2; ++pass) {
+              int d0, e0, d1, e1;
+              const bool rev = pass != 0;
+              const int o = rev ? N - b0 : a0, POo = rev ? POb : POa;
+              const int res = draw_exact(Pm, M, N, rev, o, rev ? N - na : b0, rev ? ub : ua, Km, tb);
+              pick_counts(res, o, POo, walk_prefix(Pm, M, N, NW, rev, res), d0, e0, d1, e1);
+              t0 += d0; f0 += e0; t1 += d1; f1 += e1;
+              if (rev) nb = N - res; else na = res;
+            }
           } else if constexpr (NWM > 0) {   /* column in registers, branch-free draws */
             uint32_t wk[NWM];   /* forward walk words, then (second trip) the reversed ones */
             load_fwd<NWM>(Pm, M, NW, wk);
@@ -2138,8 +2185,10 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             nchg += (na != a0) + (nb != b0);
             sab[m] = na; sab[M + m] = nb;
             scnt[m] = t0; scnt[M + m] = f0; scnt[2 * M + m] = t1; scnt[3 * M + m] = f1;
-            if (want_logl) {   /* mcmc_logl term (mcmc.c:643-644) */
-              const double lt = (double)t0 * K.cc + (double)f0 * K.d + (double)t1 * K.dd + (double)f1 * K.c;
+            if (want_logl) {   /* mcmc_logl term (mcmc.c:643-644); manycd: the taxon's c, d (mcmc.c:641-642) */
+              const double kcc = MCD ? cx[m] : K.cc, kd = MCD ? cv[M + m] : K.d, kdd = MCD ? cx[M + m] : K.dd,
+                           kc = MCD ? cv[m] : K.c;
+              const double lt = (double)t0 * kcc + (double)f0 * kd + (double)t1 * kdd + (double)f1 * kc;
               if constexpr (SP) xst(lbuf + m, lt); else lbuf[m] = lt;
             }
           }
@@ -2648,7 +2697,10 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 if (Knz == 0) cls = 1; else cls = 2;
                 Ebp = __builtin_inf();
 #else
-                if (Knz == 0 || Sp > Ebp) cls = 1;
+                if (MCD) {   /* manycd: per-taxon coefficients, the exact sequential delta decides */
+                  cls = (Knz == 0) ? 1 : 2;
+                  Ebp = __builtin_inf();
+                } else if (Knz == 0 || Sp > Ebp) cls = 1;
                 else if (Sp < -Ebp) {
                   const float uf = (float)((double)uwp / 4294967296.0);
                   const double lua = (double)__builtin_amdgcn_logf(uf) * 0.69314718055994531;
@@ -2695,7 +2747,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               else   /* (no exchange: the one-workgroup kernels never see the split machinery) */
                 dl = sr_exact_delta<PR, GM, SP>(kind, q, K, sab, P, pre, M, KTC, 0, M, hl, nh, hcnt, nhall,
                                                 cbuf + xpar * KTC * sr_chunk(PR), ccnt + xpar * KTC, xs, lane, wave, TB,
-                                                [] {});
+                                                [] {}, cv, cx);
               xpar ^= 1;
               if (!decided) {
                 if (tid == 0) misc[MS_NEXACT]++;
@@ -2884,6 +2936,10 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         double *rd = A.rec_cdl + ((size_t)chain * A.rec_cap + slot) * 3;
         rd[0] = c; rd[1] = d; rd[2] = loglik;
       }
+      if constexpr (MCD) {   /* every taxon's c, d (mcmc.c:86-90) */
+        double *rv = A.rec_cdv + ((size_t)chain * A.rec_cap + slot) * 2 * M;
+        for (int m = tid; m < 2 * M; m += TB) rv[m] = cv[m];
+      }
     }
   } /* calls */
 
@@ -2954,6 +3010,7 @@ __constant__ unsigned long long sr_spec_abi[4] = {
 
 struct srk_dev {
   int device, N, M, NW, nh, nchains, TB, TPT, rec_cap, gm, pr, sp, grid, coop;
+  int mcd;                 /* manycd: per-taxon c, d (MCD kernels) */
   int jit;                 /* the launch uses the shape-specialised kernel (srk_spec_load) */
   double *dsum;            /* srk_exp_data's per-chain sums (device) */
   hipModule_t mod;
@@ -2986,8 +3043,13 @@ static bool sr_pair_ok(int N, int M)
   return sr_nwm(N) == 9 && M > 256 && M <= 512;
 }
 
-static sr_kfn sr_pick_kernel(int TB, int N, int M, bool gm, bool pr, int nh, bool sp = false)
+static sr_kfn sr_pick_kernel(int TB, int N, int M, bool gm, bool pr, int nh, bool sp = false, bool mcd = false)
 {
+  if (mcd) {   /* manycd: the generic one-workgroup kernels at 1024 threads */
+    if (TB != 1024 || pr || sp) return nullptr;
+    return gm ? (sr_kfn)sr_sweep_kernel<1024, 0, true, false, false, true>
+              : (sr_kfn)sr_sweep_kernel<1024, 0, false, false, false, true>;
+  }
   if (pr) return (TB == 1024 && !gm) ? (sr_kfn)sr_sweep_kernel<1024, 9, false, true> : nullptr;
 #ifndef SR_STAMPS
   if (sp) return (TB == 1024 && gm) ? (sr_kfn)sr_sweep_kernel<1024, 0, true, false, true> : nullptr;
@@ -3013,16 +3075,20 @@ static sr_kfn sr_pick_kernel(int TB, int N, int M, bool gm, bool pr, int nh, boo
 /* ---- the kernel a session runs ----------------------------------------------------------------
  * Block size, variant (LDS columns / HBM columns / pair kernel) and LDS bytes from the shape alone (no
  * HIP call): srk_create launches this plan, srk_plan / sr_specialize report it without a GPU. */
-struct srk_kplan { int TB, pr, gm; size_t lds; };
+struct srk_kplan { int TB, pr, gm, mcd; size_t lds; };
 
-static int plan_kernel(int N, int M, int nh, int block_threads, int gm_force, srk_kplan *kp)
+static int plan_kernel(int N, int M, int nh, int block_threads, int gm_force, int mcd, srk_kplan *kp)
 {
   if (nh > SR_NHMAX || N > 32767 || M > 32767) return -6;
   const int NW = (N + 31) / 32;
   int TB = block_threads;
+  if (mcd) {   /* manycd: 1024 threads (one or more taxa per thread) */
+    if (TB > 0 && TB != 1024) return -6;
+    TB = 1024;
+  }
   /* the pair kernel where it was asked for (two lanes per taxon, 1024 threads), else one thread per
      taxon in the smallest block of 256..1024 threads that covers M */
-  int pr = (TB <= 0 && gm_force != 1 && nh <= 32 && sr_pair_ok(N, M)) ? 1 : 0;
+  int pr = (TB <= 0 && !mcd && gm_force != 1 && nh <= 32 && sr_pair_ok(N, M)) ? 1 : 0;
   if (pr) TB = 1024;
   if (TB <= 0) { TB = 256; while (TB < M && TB < 1024) TB *= 2; }
   /* columns in LDS when the whole layout fits, else the HBM-column variant */
@@ -3034,8 +3100,8 @@ static int plan_kernel(int N, int M, int nh, int block_threads, int gm_force, sr
     L = sr_layout(N, M, NW, TB, gm != 0, pr != 0, nh);
   }
   if (gm) pr = 0;
-  if (!sr_pick_kernel(TB, N, M, gm != 0, pr != 0, nh) || L.total > 160 * 1024) return -6;
-  kp->TB = TB; kp->pr = pr; kp->gm = gm; kp->lds = L.total;
+  if (!sr_pick_kernel(TB, N, M, gm != 0, pr != 0, nh, false, mcd != 0) || L.total > 160 * 1024) return -6;
+  kp->TB = TB; kp->pr = pr; kp->gm = gm; kp->mcd = mcd; kp->lds = L.total;
   return 0;
 }
 
@@ -3043,7 +3109,7 @@ static int plan_kernel(int N, int M, int nh, int block_threads, int gm_force, sr
    split kernel measured 4.4 % slower specialised, profiles/r03z6_ab_jit.json; the pair kernel is opt-in) */
 static bool spec_shape_of(int N, int M, int nh, const srk_kplan &kp, sr_spec_shape *s)
 {
-  if (kp.gm || kp.pr) return false;
+  if (kp.gm || kp.pr || kp.mcd) return false;
   s->TB = kp.TB;
   s->NWM = sr_regwalk(N, M, kp.TB, false, nh) ? sr_nwm(N) : 0;
   s->N = N; s->M = M; s->NH = nh;
@@ -3055,10 +3121,10 @@ static bool spec_shape_of(int N, int M, int nh, const srk_kplan &kp, sr_spec_sha
   return true;
 }
 
-extern "C" int srk_plan(int N, int M, int nh, int block_threads, int gm_force, sr_spec_shape *shape)
+extern "C" int srk_plan(int N, int M, int nh, int block_threads, int gm_force, int manycd, sr_spec_shape *shape)
 {
   srk_kplan kp;
-  if (int e = plan_kernel(N, M, nh, block_threads, gm_force, &kp)) return e;
+  if (int e = plan_kernel(N, M, nh, block_threads, gm_force, manycd, &kp)) return e;
   return spec_shape_of(N, M, nh, kp, shape) ? 1 : 0;
 }
 
@@ -3078,7 +3144,7 @@ static int srk_spec_load(srk_dev *d)
   (void)d;
   return -1;   /* (stamp builds: generic kernels only) */
 #else
-  srk_kplan kp = {d->TB, d->pr, d->gm, d->lds};
+  srk_kplan kp = {d->TB, d->pr, d->gm, d->mcd, d->lds};
   sr_spec_shape s;
   if (!spec_shape_of(d->N, d->M, d->nh, kp, &s)) return -1;
   char path[4608], log[4700];
@@ -3088,7 +3154,7 @@ static int srk_spec_load(srk_dev *d)
     return rc;
   }
   char name[128];
-  snprintf(name, sizeof name, "_Z15sr_sweep_kernelILi%dELi%dELb0ELb0ELb0EEv5KArgs", s.TB, s.NWM);
+  snprintf(name, sizeof name, "_Z15sr_sweep_kernelILi%dELi%dELb0ELb0ELb0ELb0EEv5KArgs", s.TB, s.NWM);
   unsigned long long abi[4] = {0, 0, 0, 0};
   const unsigned long long want[4] = {
       sizeof(KArgs), (unsigned long long)s.TB | ((unsigned long long)s.NWM << 16),
@@ -3124,7 +3190,7 @@ extern "C" int sr_specialize(const sr_dataset *ds, const sr_run_opts *opts)
   if (o.flags & SR_F_GENERIC_KERNEL) return 0;
   const int gm_force = (o.flags & SR_F_HBM_COLUMNS) ? 1 : ((o.flags & SR_F_LDS_COLUMNS) ? 0 : -1);
   sr_spec_shape s;
-  const int r = srk_plan(ds->N, ds->M, ds->nh, o.block_threads, gm_force, &s);
+  const int r = srk_plan(ds->N, ds->M, ds->nh, o.block_threads, gm_force, o.manycd != 0, &s);
   if (r <= 0) return r < 0 ? SR_EUNSUPPORTED : 0;
 #if defined(SR_STAMPS)
   return 0;
@@ -3144,7 +3210,7 @@ extern "C" int sr_specialize(const sr_dataset *ds, const sr_run_opts *opts)
 extern "C" int sr_spec_cache_path(int N, int M, int nh, int block_threads, char *path, size_t len)
 {
   sr_spec_shape s;
-  const int r = srk_plan(N, M, nh, block_threads, -1, &s);
+  const int r = srk_plan(N, M, nh, block_threads, -1, 0, &s);
   if (r <= 0) return 1;
   return sr_spec_path(&s, path, len);
 }
@@ -3172,14 +3238,14 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
                           const uint32_t *pkey, int spec, srk_dev **out)
 {
   srk_kplan kp;
-  if (plan_kernel(st->N, st->M, st->nh, block_threads, gm_force, &kp)) return -6;
+  if (plan_kernel(st->N, st->M, st->nh, block_threads, gm_force, st->manycd, &kp)) return -6;
   int ndev = srk_device_count();
   if (ndev <= 0 || device < 0 || device >= ndev) return -5;
   HIPCHK(hipSetDevice(device));
   srk_dev *d = new srk_dev();
   d->device = device; d->N = st->N; d->M = st->M; d->NW = st->NW; d->nh = st->nh; d->nchains = st->nchains;
   const int TB = kp.TB;
-  d->TB = TB; d->TPT = 1; d->pr = kp.pr; d->gm = kp.gm; d->lds = kp.lds;
+  d->TB = TB; d->TPT = 1; d->pr = kp.pr; d->gm = kp.gm; d->mcd = kp.mcd; d->lds = kp.lds;
   /* split chains (two co-resident workgroups per chain, one taxon per thread): HBM columns at 1024
      threads when the taxa exceed one block but each half fits it, and the whole grid (16 blocks per
      8 chains) is co-resident -- launched cooperatively.  SR_SPLIT=0 disables it, SR_SPLIT=1 also
@@ -3190,7 +3256,7 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
     const int want = e ? atoi(e) : -1;
     const int Mh = sr_sp_half(st->M);
     sr_kfn ks = sr_pick_kernel(TB, st->N, st->M, true, false, st->nh, true);
-    if (want != 0 && d->gm && ks && Mh <= TB && st->M > 128 && (st->M > TB || want == 1)) {
+    if (want != 0 && !d->mcd && d->gm && ks && Mh <= TB && st->M > 128 && (st->M > TB || want == 1)) {
       int cus = 0, occ = 0, coop = 0;
       const int grid = 16 * ((st->nchains + 7) / 8);
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
@@ -3233,13 +3299,18 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
     rc |= dev_alloc_copy(d, &A.glbuf, (const double *)nullptr, C * st->M);
     rc |= dev_alloc_copy(d, &A.gcbuf, (const double *)nullptr, C * sr_gm_cbuf(st->M));
   }
+  if (d->mcd) {
+    rc |= dev_alloc_copy(d, &A.cdv, (const double *)st->cdv, C * 2 * st->M);
+    rc |= dev_alloc_copy(d, &A.cdx, (const double *)nullptr, C * 2 * st->M);
+    rc |= dev_alloc_copy(d, &A.rec_cdv, (const double *)nullptr, C * d->rec_cap * 2 * st->M);
+  }
   if (d->sp) {
     rc |= dev_alloc_copy(d, &A.xflag, (const int *)nullptr, C * 2);
     rc |= dev_alloc_copy(d, &A.xbuf, (const int *)nullptr, C * sr_sp_xb(st->M));
     rc |= dev_alloc_copy(d, &A.xerr, (const int *)nullptr, 1);
   }
   if (rc) { srk_destroy(d); return -5; }
-  sr_kfn k = sr_pick_kernel(TB, st->N, st->M, d->gm != 0, d->pr != 0, st->nh, d->sp != 0);
+  sr_kfn k = sr_pick_kernel(TB, st->N, st->M, d->gm != 0, d->pr != 0, st->nh, d->sp != 0, d->mcd != 0);
   if (hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d->lds) != hipSuccess) {
     srk_destroy(d);
     return -5;
@@ -3270,7 +3341,7 @@ extern "C" int srk_run(srk_dev *d, int calls, int spc, int save, int rec_base)
   HIPCHK(hipSetDevice(d->device));
   KArgs A = d->args;
   A.calls = calls; A.spc = spc; A.save = save; A.rec_base = rec_base;
-  sr_kfn k = sr_pick_kernel(d->TB, d->N, d->M, d->gm != 0, d->pr != 0, d->nh, d->sp != 0);
+  sr_kfn k = sr_pick_kernel(d->TB, d->N, d->M, d->gm != 0, d->pr != 0, d->nh, d->sp != 0, d->mcd != 0);
   if (d->sp) HIPCHK(hipMemsetAsync(A.xflag, 0, (size_t)d->nchains * 2 * sizeof(int), d->stream));   /* exchange sequence restarts */
   if (d->have_events) HIPCHK(hipEventRecord(d->ev0, d->stream));
   if (d->jit) {   /* the run-time specialised kernel (same arguments; LDS columns: one workgroup per chain) */
@@ -3423,7 +3494,7 @@ extern "C" int srk_fetch_chain_records(srk_dev *d, int chain, int first, int cou
  * rec_cap >= 2 * cpl.  consume(ctx, first_call, count, ab_pi [nchains][count][2M+N], cdl
  * [nchains][count][3]) returns nonzero to stop. */
 extern "C" int srk_run_pipelined(srk_dev *d, int total_calls, int cpl, int spc,
-                                 int (*consume)(void *, int, int, const int16_t *, const double *), void *ctx)
+                                 int (*consume)(void *, int, int, const int16_t *, const double *, const double *), void *ctx)
 {
   if (total_calls <= 0) return 0;
   if (cpl <= 0 || 2 * cpl > d->rec_cap) return -1;
@@ -3431,13 +3502,16 @@ extern "C" int srk_run_pipelined(srk_dev *d, int total_calls, int cpl, int spc,
   const size_t W = 2 * (size_t)d->M + d->N, C = d->nchains;
   int16_t *hab[2] = {nullptr, nullptr};
   double *hcd[2] = {nullptr, nullptr};
+  double *hcv[2] = {nullptr, nullptr};   /* manycd: per-taxon c, d rows */
+  const size_t R2 = 2 * (size_t)d->M;
   hipEvent_t ev[2] = {nullptr, nullptr};
   int cnt[2] = {0, 0}, first[2] = {0, 0};
   int rc = 0;
   for (int h = 0; h < 2 && !rc; ++h) {
     if (hipHostMalloc((void **)&hab[h], C * cpl * W * sizeof(int16_t), hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void **)&hcd[h], C * cpl * 3 * sizeof(double), hipHostMallocDefault) != hipSuccess ||
-        hipEventCreateWithFlags(&ev[h], hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&ev[h], hipEventDisableTiming) != hipSuccess ||
+        (d->mcd && hipHostMalloc((void **)&hcv[h], C * cpl * R2 * sizeof(double), hipHostMallocDefault) != hipSuccess))
       rc = -5;
   }
   int done = 0, j = 0;
@@ -3452,12 +3526,15 @@ extern "C" int srk_run_pipelined(srk_dev *d, int total_calls, int cpl, int spc,
         hipMemcpy2DAsync(hcd[h], k * 3 * sizeof(double), d->args.rec_cdl + (size_t)h * cpl * 3,
                          d->rec_cap * 3 * sizeof(double), k * 3 * sizeof(double), C, hipMemcpyDeviceToHost,
                          d->stream) != hipSuccess ||
+        (d->mcd && hipMemcpy2DAsync(hcv[h], k * R2 * sizeof(double), d->args.rec_cdv + (size_t)h * cpl * R2,
+                                    d->rec_cap * R2 * sizeof(double), k * R2 * sizeof(double), C, hipMemcpyDeviceToHost,
+                                    d->stream) != hipSuccess) ||
         hipEventRecord(ev[h], d->stream) != hipSuccess) { rc = -5; break; }
     cnt[h] = k; first[h] = done;
     if (j > 0) {   /* the previous launch's records, while this launch runs */
       const int p = h ^ 1;
       if (hipEventSynchronize(ev[p]) != hipSuccess) { rc = -5; break; }
-      if (consume(ctx, first[p], cnt[p], hab[p], hcd[p])) { rc = -1; break; }
+      if (consume(ctx, first[p], cnt[p], hab[p], hcd[p], hcv[p])) { rc = -1; break; }
     }
     done += k;
     ++j;
@@ -3465,13 +3542,14 @@ extern "C" int srk_run_pipelined(srk_dev *d, int total_calls, int cpl, int spc,
   if (!rc && j > 0) {
     const int p = (j - 1) & 1;
     if (hipEventSynchronize(ev[p]) != hipSuccess) rc = -5;
-    else if (consume(ctx, first[p], cnt[p], hab[p], hcd[p])) rc = -1;
+    else if (consume(ctx, first[p], cnt[p], hab[p], hcd[p], hcv[p])) rc = -1;
   }
   (void)hipStreamSynchronize(d->stream);
   if (!rc) rc = sp_check(d);
   for (int h = 0; h < 2; ++h) {
     if (hab[h]) (void)hipHostFree(hab[h]);
     if (hcd[h]) (void)hipHostFree(hcd[h]);
+    if (hcv[h]) (void)hipHostFree(hcv[h]);
     if (ev[h]) (void)hipEventDestroy(ev[h]);
   }
   return rc;
@@ -3505,6 +3583,20 @@ extern "C" int srk_download_state(srk_dev *d, sr_state_host *st)
   if (st->mt) HIPCHK(hipMemcpy(st->mt, A.mt, C * SR_RING * SR_MT_N * 4, hipMemcpyDeviceToHost));
   if (st->rng) HIPCHK(hipMemcpy(st->rng, A.rng, C * 2 * 8, hipMemcpyDeviceToHost));
   if (st->acc) HIPCHK(hipMemcpy(st->acc, A.acc, C * SR_NACC * 8, hipMemcpyDeviceToHost));
+  if (st->cdv && d->mcd) HIPCHK(hipMemcpy(st->cdv, A.cdv, C * 2 * d->M * 8, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+/* manycd: every chain's per-taxon c, d of record rows [first, first + count): cdv [nchains][count][2M] */
+extern "C" int srk_fetch_cdv(srk_dev *d, int first, int count, double *cdv)
+{
+  if (!d->mcd || first < 0 || count < 0 || first + count > d->rec_cap) return -1;
+  HIPCHK(hipSetDevice(d->device));
+  HIPCHK(hipStreamSynchronize(d->stream));
+  if (count == 0) return 0;
+  const size_t row = 2 * (size_t)d->M;
+  HIPCHK(hipMemcpy2D(cdv, count * row * 8, d->args.rec_cdv + (size_t)first * row, d->rec_cap * row * 8, count * row * 8,
+                     d->nchains, hipMemcpyDeviceToHost));
   return 0;
 }
 

@@ -226,6 +226,7 @@ typedef struct {
   int32_t *pi, *rpi, *a, *b, *t0, *f0, *t1, *f1;
   int t0a, f0a, t1a, f1a;
   double c, d, loglik;
+  const double *cv;         /* manycd: per-taxon c[M], d[M] (mcmc.h:38-39 vectors), else NULL: c, d shared */
   int diag;                 /* SR_F_DIAG: the reference's stderr diagnostics */
 } hmodel;
 
@@ -265,8 +266,10 @@ static void h_count01(hmodel *x)                      /* mcmc_count01, mcmc.c:65
 static double h_logl(const hmodel *x)                 /* mcmc_logl, mcmc.c:625-648 */
 {
   double loglik = 0.;
-  for (int m = 0; m < x->M; m++)
-    loglik += x->t0[m] * h_log(1. - h_exp(x->c)) + x->f0[m] * x->d + x->t1[m] * h_log(1. - h_exp(x->d)) + x->f1[m] * x->c;
+  for (int m = 0; m < x->M; m++) {
+    const double c = x->cv ? x->cv[m] : x->c, d = x->cv ? x->cv[x->M + m] : x->d;   /* mcmc.c:641-642 */
+    loglik += x->t0[m] * h_log(1. - h_exp(c)) + x->f0[m] * d + x->t1[m] * h_log(1. - h_exp(d)) + x->f1[m] * c;
+  }
   return loglik;
 }
 
@@ -338,14 +341,15 @@ struct sr_session {
 static void state_free(sr_state_host *st)
 {
   free(st->P); free(st->rpi); free(st->hp); free(st->ab); free(st->cnt);
-  free(st->cdl); free(st->mt); free(st->rng); free(st->acc);
+  free(st->cdl); free(st->mt); free(st->rng); free(st->acc); free(st->cdv);
   memset(st, 0, sizeof(*st));
 }
 
-static int state_alloc(sr_state_host *st, int N, int M, int nh, int C)
+static int state_alloc(sr_state_host *st, int N, int M, int nh, int C, int manycd)
 {
   memset(st, 0, sizeof(*st));
-  st->N = N; st->M = M; st->NW = (N + 31) / 32; st->nh = nh; st->nchains = C;
+  st->N = N; st->M = M; st->NW = (N + 31) / 32; st->nh = nh; st->nchains = C; st->manycd = manycd != 0;
+  if (st->manycd && !(st->cdv = (double *)calloc((size_t)C * 2 * M, 8))) return SR_ENOMEM;
   st->P = (uint32_t *)calloc((size_t)C * st->NW * M, 4);
   st->rpi = (int32_t *)calloc((size_t)C * N, 4);
   st->hp = (int32_t *)calloc((size_t)C * SR_NHMAX, 4);
@@ -400,6 +404,8 @@ static int init_chain(const sr_dataset *ds, uint64_t seed, sr_state_host *st, in
   st->cdl[(size_t)c * 4 + 0] = x.c;
   st->cdl[(size_t)c * 4 + 1] = x.d;
   st->cdl[(size_t)c * 4 + 2] = x.loglik;
+  if (st->manycd)   /* every taxon starts at log .01 / log .3 (mcmc.c:417-421): the same loglik */
+    for (int m = 0; m < M; m++) { st->cdv[(size_t)c * 2 * M + m] = x.c; st->cdv[(size_t)c * 2 * M + M + m] = x.d; }
   memcpy(st->mt + ((size_t)c * SR_RING + (r.bidx % SR_RING)) * SR_MT_N, r.blk, sizeof(r.blk));
   st->rng[(size_t)c * 2 + 0] = r.pos;
   st->rng[(size_t)c * 2 + 1] = r.bidx + 1;
@@ -430,7 +436,7 @@ static int session_new(const sr_dataset *ds, const sr_chain_spec *specs, int32_t
   sr_run_opts o;
   if (opts) o = *opts; else sr_default_opts(&o);
   if (o.sweeps_per_call <= 0) return SR_EINVAL;
-  if (o.manycd != 0) return SR_EUNSUPPORTED;
+  o.manycd = o.manycd != 0;   /* mcmc_readmodel stores the flag; any nonzero value means per-taxon c, d */
   /* nh <= 64 hard sites (a 64-bit mask per taxon), N <= 4095 (12-bit positions in the packed proposal
      records); records are int16 (M <= 32767).  The LDS layout must also fit 160 KB (srk_create). */
   if (ds->nh > SR_NHMAX || ds->N > 4095 || ds->M > 32767) return SR_EUNSUPPORTED;
@@ -447,7 +453,7 @@ static int session_new(const sr_dataset *ds, const sr_chain_spec *specs, int32_t
   s->nchains = n_chains;
   s->opts = o;
   sr_state_host st;
-  int rc = state_alloc(&st, ds->N, ds->M, ds->nh, n_chains);
+  int rc = state_alloc(&st, ds->N, ds->M, ds->nh, n_chains, o.manycd);
   if (rc) { sr_session_destroy(s); return rc; }
   const int philox = (o.flags & SR_F_RNG_PHILOX) != 0;
   if (restore) rc = restore(restore_ctx, &st);
@@ -575,6 +581,15 @@ SR_API int sr_session_fetch_chain_records(sr_session *s, int32_t chain, int32_t 
   return srk_fetch_chain_records(s->dev, chain, first, count, ab_pi, cdl) ? SR_EDEVICE : SR_OK;
 }
 
+SR_API int sr_session_fetch_cd_vectors(sr_session *s, int32_t first, int32_t count, double *cdv)
+{
+  if (!s || !cdv || first < 0 || count < 0 || first + count > s->nrec) return SR_EINVAL;
+  if (!s->opts.manycd) return SR_EINVAL;
+  return srk_fetch_cdv(s->dev, first, count, cdv) ? SR_EDEVICE : SR_OK;
+}
+
+SR_API int32_t sr_session_manycd(const sr_session *s) { return s ? s->opts.manycd : 0; }
+
 /* compute_exp_data + print_exp_data (mcmc.c:53-67) over the buffered records [first, first + count)
  * of every chain: sums of -loglik, e^c, e^d in sample order (C library exp, as the reference),
  * divided by the reference's hard-coded 1000.  consistent is left 0 (no check is run). */
@@ -606,7 +621,7 @@ SR_API int sr_session_reset_records(sr_session *s)
 
 static int download(sr_session *s, sr_state_host *st)
 {
-  int rc = state_alloc(st, s->ds.N, s->ds.M, s->ds.nh, s->nchains);
+  int rc = state_alloc(st, s->ds.N, s->ds.M, s->ds.nh, s->nchains, s->opts.manycd);
   if (rc) return rc;
   if (srk_download_state(s->dev, st)) { state_free(st); return SR_EDEVICE; }
   return SR_OK;
@@ -627,28 +642,31 @@ static uint64_t dataset_hash(const sr_dataset *ds)
 
 typedef struct { size_t bytes; void *p; } ck_part;
 #define SR_CK_VERSION 3   /* 2: SR_NACC counters per chain; 3: SR_NHMAX = 64 hard positions per chain */
+#define SR_CK_VERSION_MANYCD 4   /* version 3 + the per-taxon c, d of every chain (manycd sessions) */
+#define SR_CK_PARTS 10
 
 static int ck_parts(sr_state_host *st, ck_part *pt)
 {
   const size_t C = (size_t)st->nchains;
-  ck_part q[9] = {
+  ck_part q[SR_CK_PARTS] = {
     {C * st->NW * st->M * 4, st->P}, {C * st->N * 4, st->rpi}, {C * SR_NHMAX * 4, st->hp},
     {C * 2 * st->M * 4, st->ab}, {C * 4 * st->M * 4, st->cnt}, {C * 4 * 8, st->cdl},
-    {C * SR_RING * SR_MT_N * 4, st->mt}, {C * 2 * 8, st->rng}, {C * SR_NACC * 8, st->acc}};
+    {C * SR_RING * SR_MT_N * 4, st->mt}, {C * 2 * 8, st->rng}, {C * SR_NACC * 8, st->acc},
+    {C * 2 * st->M * 8, st->cdv}};
   memcpy(pt, q, sizeof q);
-  return 9;
+  return st->manycd ? 10 : 9;
 }
 
 static int ck_write(const char *path, const sr_dataset *ds, const sr_chain_spec *specs, int32_t n, sr_state_host *st)
 {
   FILE *f = fopen(path, "wb");
   if (!f) return SR_EIO;
-  const uint32_t ver = SR_CK_VERSION;
+  const uint32_t ver = st->manycd ? SR_CK_VERSION_MANYCD : SR_CK_VERSION;
   const int32_t dims[4] = {ds->N, ds->M, ds->nh, n};
   const uint64_t h = dataset_hash(ds);
   int ok = fwrite("SRCK", 1, 4, f) == 4 && fwrite(&ver, 4, 1, f) == 1 && fwrite(dims, 4, 4, f) == 4 &&
            fwrite(&h, 8, 1, f) == 1 && fwrite(specs, sizeof(sr_chain_spec), n, f) == (size_t)n;
-  ck_part pt[9];
+  ck_part pt[SR_CK_PARTS];
   const int np = ck_parts(st, pt);
   for (int k = 0; k < np && ok; k++) ok = fwrite(pt[k].p, 1, pt[k].bytes, f) == pt[k].bytes;
   if (fclose(f) != 0) ok = 0;
@@ -672,7 +690,7 @@ SR_API int sr_host_initial_checkpoint(const sr_dataset *ds, const sr_chain_spec 
 {
   if (!ds || !specs || n_chains <= 0 || !path || ds->nh > SR_NHMAX) return SR_EINVAL;
   sr_state_host st;
-  int rc = state_alloc(&st, ds->N, ds->M, ds->nh, n_chains);
+  int rc = state_alloc(&st, ds->N, ds->M, ds->nh, n_chains, 0);
   if (rc) return rc;
   for (int c = 0; c < n_chains && rc == SR_OK; c++) rc = init_chain(ds, specs[c].seed, &st, c, 0);
   if (rc == SR_OK) rc = ck_write(path, ds, specs, n_chains, &st);
@@ -708,7 +726,7 @@ static int ck_validate(const sr_dataset *ds, const sr_state_host *st)
 static int ck_restore(void *ctx, sr_state_host *st)
 {
   ck_reader *r = (ck_reader *)ctx;
-  ck_part pt[9];
+  ck_part pt[SR_CK_PARTS];
   const int np = ck_parts(st, pt);
   for (int k = 0; k < np; k++)
     if (fread(pt[k].p, 1, pt[k].bytes, r->f) != pt[k].bytes) return SR_EPARSE;
@@ -727,7 +745,8 @@ SR_API int sr_session_restore(const sr_dataset *ds, const char *path, const sr_r
   uint64_t h = 0;
   int rc = SR_OK;
   sr_chain_spec *specs = NULL;
-  if (fread(magic, 1, 4, f) != 4 || memcmp(magic, "SRCK", 4) != 0 || fread(&ver, 4, 1, f) != 1 || ver != SR_CK_VERSION ||
+  if (fread(magic, 1, 4, f) != 4 || memcmp(magic, "SRCK", 4) != 0 || fread(&ver, 4, 1, f) != 1 ||
+      (ver != SR_CK_VERSION && ver != SR_CK_VERSION_MANYCD) ||
       fread(dims, 4, 4, f) != 4 || fread(&h, 8, 1, f) != 1 || dims[3] <= 0)
     rc = SR_EPARSE;
   else if (dims[0] != ds->N || dims[1] != ds->M || dims[2] != ds->nh || h != dataset_hash(ds))
@@ -736,9 +755,13 @@ SR_API int sr_session_restore(const sr_dataset *ds, const char *path, const sr_r
     rc = SR_ENOMEM;
   else if (fread(specs, sizeof(sr_chain_spec), dims[3], f) != (size_t)dims[3])
     rc = SR_EPARSE;
-  if (rc == SR_OK) {
+  if (rc == SR_OK) {   /* the checkpoint's kind (manycd or not) decides; a caller's opts naming the other is an error */
+    sr_run_opts o;
+    if (opts) o = *opts; else sr_default_opts(&o);
+    if (opts && (o.manycd != 0) != (ver == SR_CK_VERSION_MANYCD)) rc = SR_EINVAL;
+    o.manycd = ver == SR_CK_VERSION_MANYCD;
     ck_reader r = {f, ds};
-    rc = session_new(ds, specs, dims[3], opts, ck_restore, &r, out);
+    if (rc == SR_OK) rc = session_new(ds, specs, dims[3], &o, ck_restore, &r, out);
   }
   free(specs);
   fclose(f);
@@ -882,6 +905,7 @@ static int check_chain(const sr_dataset *ds, const sr_state_host *st, int c)
   if (nh != ds->nh) flag = 1;
   x.c = st->cdl[(size_t)c * 4 + 0];
   x.d = st->cdl[(size_t)c * 4 + 1];
+  x.cv = st->manycd ? st->cdv + (size_t)c * 2 * M : NULL;
   h_count01(&x);
   const int32_t *cnt = st->cnt + (size_t)c * 4 * M;
   for (int m = 0; m < M; m++)
@@ -909,14 +933,15 @@ typedef struct {
 } dir_ctx;
 
 /* one mcmc_save_chain line (mcmc.c:69-92) into *buf; c and d are shared by all taxa
- * (manycd=0), so their "%.14f " text is formatted once and replicated.  Returns the length. */
+ * (manycd=0), so their "%.14f " text is formatted once and replicated; cdv (manycd=1): each
+ * taxon's own c[M], d[M].  Returns the length. */
 static char *put_int(char *p, int v);
-static long format_line(char **buf, size_t *cap, int N, int M, const int16_t *ab_pi, const double *cdl)
+static long format_line(char **buf, size_t *cap, int N, int M, const int16_t *ab_pi, const double *cdl, const double *cdv)
 {
   char cbuf[64], dbuf[64];
   const int cl = snprintf(cbuf, sizeof cbuf, "%.14f ", exp(cdl[0]));
   const int dl = snprintf(dbuf, sizeof dbuf, "%.14f ", exp(cdl[1]));
-  const size_t need = (size_t)(2 * M + N) * 12 + (size_t)M * (cl + dl) + 128;
+  const size_t need = (size_t)(2 * M + N) * 12 + (size_t)M * (cdv ? 2 * 40 : (cl + dl)) + 128;
   if (need > *cap) {
     char *nl = (char *)realloc(*buf, need);
     if (!nl) return -1;
@@ -929,9 +954,15 @@ static long format_line(char **buf, size_t *cap, int N, int M, const int16_t *ab
   *p++ = ',';
   for (int i = 0; i < N; i++) { p = put_int(p, ab_pi[2 * M + i]); *p++ = ' '; }
   *p++ = ',';
-  for (int i = 0; i < M; i++) { memcpy(p, cbuf, cl); p += cl; }
-  *p++ = ',';
-  for (int i = 0; i < M; i++) { memcpy(p, dbuf, dl); p += dl; }
+  if (cdv) {
+    for (int i = 0; i < M; i++) p += sprintf(p, "%.14f ", exp(cdv[i]));
+    *p++ = ',';
+    for (int i = 0; i < M; i++) p += sprintf(p, "%.14f ", exp(cdv[M + i]));
+  } else {
+    for (int i = 0; i < M; i++) { memcpy(p, cbuf, cl); p += cl; }
+    *p++ = ',';
+    for (int i = 0; i < M; i++) { memcpy(p, dbuf, dl); p += dl; }
+  }
   p += sprintf(p, ",%.14f\n", cdl[2]);
   return (long)(p - *buf);
 }
@@ -952,6 +983,7 @@ typedef struct {
   int first, count;
   const int16_t *ab;
   const double *cd;
+  const double *cdv;   /* manycd: [n][count][2M] per-taxon c, d, else NULL */
   int err;
 } run_ctx;
 
@@ -976,17 +1008,18 @@ static void *writer_main(void *va)
     chain_sums(r, c);
     for (int t = 0; t < r->count; t++) {
       const long len = format_line(&w->line, &w->cap, r->N, r->M, r->ab + ((size_t)c * r->count + t) * W,
-                                   r->cd + ((size_t)c * r->count + t) * 3);
+                                   r->cd + ((size_t)c * r->count + t) * 3,
+                                   r->cdv ? r->cdv + ((size_t)c * r->count + t) * 2 * r->M : NULL);
       if (len < 0 || fwrite(w->line, 1, (size_t)len, r->dir->f[c]) != (size_t)len) { r->err = 1; return NULL; }
     }
   }
   return NULL;
 }
 
-static int consume_batch(void *vctx, int first, int count, const int16_t *ab, const double *cd)
+static int consume_batch(void *vctx, int first, int count, const int16_t *ab, const double *cd, const double *cdv)
 {
   run_ctx *r = (run_ctx *)vctx;
-  r->first = first; r->count = count; r->ab = ab; r->cd = cd;
+  r->first = first; r->count = count; r->ab = ab; r->cd = cd; r->cdv = cdv;
   const int N = r->N, M = r->M, W = 2 * M + N;
   if (r->dir) {
     writer_arg wa[SR_MAX_WRITERS];
@@ -1009,7 +1042,8 @@ static int consume_batch(void *vctx, int first, int count, const int16_t *ab, co
       const int16_t *src = ab + ((size_t)c * count + t) * W;
       const double *cdl = cd + ((size_t)c * count + t) * 3;
       for (int q = 0; q < W; q++) r->ra[q] = src[q];
-      sr_record rec = {N, M, r->ra, r->ra + M, r->ra + 2 * M, cdl[0], cdl[1], cdl[2]};
+      const double *cv = cdv ? cdv + ((size_t)c * count + t) * 2 * M : NULL;
+      sr_record rec = {N, M, r->ra, r->ra + M, r->ra + 2 * M, cdl[0], cdl[1], cdl[2], cv, cv ? cv + M : NULL};
       if (r->sink(r->ctx, c, first + t, &rec)) return 1;
     }
   }
@@ -1059,15 +1093,17 @@ static int run_common(const sr_dataset *ds, const sr_chain_spec *specs, int32_t 
     const size_t W2 = (size_t)W;
     int16_t *ab = (int16_t *)malloc(W2 * n * sizeof(int16_t));
     double *cd = (double *)malloc((size_t)3 * n * sizeof(double));
-    rc = (ab && cd) ? SR_OK : SR_ENOMEM;
+    double *cv = o.manycd ? (double *)malloc((size_t)2 * M * n * sizeof(double)) : NULL;
+    rc = (ab && cd && (cv || !o.manycd)) ? SR_OK : SR_ENOMEM;
     for (int t = 0; t < o.sample_calls && rc == SR_OK; t++) {
       sr_session_reset_records(s);
       if ((rc = sr_session_run(s, 1, 1)) && rc != SR_EINCONSISTENT) break;
       rc = SR_OK;   /* a flagged chain (dbg_bad) keeps sampling */
       if ((rc = sr_session_fetch_records(s, 0, 1, ab, cd))) break;
-      if (consume_batch(&r, t, 1, ab, cd)) rc = dir ? SR_EIO : SR_EINVAL;
+      if (cv && (rc = sr_session_fetch_cd_vectors(s, 0, 1, cv))) break;
+      if (consume_batch(&r, t, 1, ab, cd, cv)) rc = dir ? SR_EIO : SR_EINVAL;
     }
-    free(ab); free(cd); free(r.ra);
+    free(ab); free(cd); free(cv); free(r.ra);
     if (rc) { free(r.sums); goto fail; }
   } else {
   rc = srk_run_pipelined(s->dev, o.sample_calls, cpl, o.sweeps_per_call, consume_batch, &r);
@@ -1175,10 +1211,10 @@ static int run_multi(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n
   for (int k = 0; k < nd && final_state && (rc == SR_OK || rc == SR_EINCONSISTENT); k++)
     if (!sa[k].st.ab) rc = SR_EDEVICE;
   if (final_state && (rc == SR_OK || rc == SR_EINCONSISTENT)) {
-    int r2 = state_alloc(final_state, ds->N, ds->M, ds->nh, n);
+    int r2 = state_alloc(final_state, ds->N, ds->M, ds->nh, n, o.manycd != 0);
     if (r2) rc = r2;
     else {
-      ck_part dst[9], src[9];
+      ck_part dst[SR_CK_PARTS], src[SR_CK_PARTS];
       const int np = ck_parts(final_state, dst);
       for (int k = 0; k < nd; k++) {
         ck_parts(&sa[k].st, src);
@@ -1276,8 +1312,10 @@ SR_API int sr_run_to_dirs_multi(const sr_dataset *ds, const sr_chain_spec *specs
     fprintf(f4, "%.14f,%.14f,%.14f", sum[c].exp_loglik, sum[c].exp_c, sum[c].exp_d);
     const int32_t *a = st.ab + (size_t)c * 2 * M, *b = a + M;
     const double cc = exp(st.cdl[(size_t)c * 4 + 0]), dd = exp(st.cdl[(size_t)c * 4 + 1]);
+    const double *cv = st.manycd ? st.cdv + (size_t)c * 2 * M : NULL;   /* manycd: each taxon's own */
     fprintf(f1, "a,b,c,d\n");                                   /* mcmc_save, mcmc.c:261-293 */
-    for (int i = 0; i < M; i++) fprintf(f1, "%d,%d,%.14f,%.14f\n", a[i], b[i], cc, dd);
+    for (int i = 0; i < M; i++)
+      fprintf(f1, "%d,%d,%.14f,%.14f\n", a[i], b[i], cv ? exp(cv[i]) : cc, cv ? exp(cv[M + i]) : dd);
     int *pi = (int *)malloc(N * sizeof(int));
     for (int p = 0; p < N; p++) pi[st.rpi[(size_t)c * N + p]] = p;
     fprintf(f2, "sites\n");
@@ -1330,7 +1368,7 @@ SR_API int sr_host_init_chain(const sr_dataset *ds, uint64_t seed, int32_t *a, i
                               double *cdl3, uint64_t *rng_pos)
 {
   sr_state_host st;
-  int rc = state_alloc(&st, ds->N, ds->M, ds->nh, 1);
+  int rc = state_alloc(&st, ds->N, ds->M, ds->nh, 1, 0);
   if (rc) return rc;
   rc = init_chain(ds, seed, &st, 0, 0);
   if (!rc) {

@@ -31,6 +31,8 @@ typedef struct {
   double *cdl;
   uint32_t *mt;
   uint64_t *rng, *acc;
+  int manycd;         /* 1: per-taxon c, d (mcmc.h:40 manycd) */
+  double *cdv;        /* manycd: [nchains][2M] c[M], d[M] (NULL otherwise) */
 } sr_state_host;
 
 typedef struct srk_dev srk_dev;
@@ -66,7 +68,7 @@ int srk_create(const sr_state_host *st, int device, int block_threads, int rec_c
 /* the kernel a session of this shape would run, without a GPU: *lds_cols 1 for LDS columns, *shape the
  * specialised kernel's shape (valid when the function returns 1); 0 no specialised kernel (HBM columns,
  * pair kernel), negative: unsupported */
-int srk_plan(int N, int M, int nh, int block_threads, int gm_force, sr_spec_shape *shape);
+int srk_plan(int N, int M, int nh, int block_threads, int gm_force, int manycd, sr_spec_shape *shape);
 int srk_set_stream(srk_dev *d, void *stream);
 /* calls*spc sweeps for all chains; save -> records appended at slot rec_base.. */
 int srk_run(srk_dev *d, int calls, int spc, int save, int rec_base);
@@ -81,8 +83,11 @@ int srk_fetch_records(srk_dev *d, int first, int count, int16_t *ab_pi, double *
 int srk_exp_data(srk_dev *d, int first, int count, double *sums);
 int srk_fetch_chain_records(srk_dev *d, int chain, int first, int count, int16_t *ab_pi, double *cdl);
 int srk_download_state(srk_dev *d, sr_state_host *st);
+/* consume's last argument: manycd sessions' per-taxon c, d rows [nchains][count][2M], else NULL */
 int srk_run_pipelined(srk_dev *d, int total_calls, int cpl, int spc,
-                      int (*consume)(void *, int, int, const int16_t *, const double *), void *ctx);
+                      int (*consume)(void *, int, int, const int16_t *, const double *, const double *), void *ctx);
+/* manycd: per-taxon c, d of record rows [first, first + count), [nchains][count][2M] */
+int srk_fetch_cdv(srk_dev *d, int first, int count, double *cdv);
 /* the session's record buffer in HBM: [nchains][rec_cap][2M+N] int16 */
 int srk_records_device(srk_dev *d, const int16_t **rec, int *rec_cap, int *device, void **stream);
 

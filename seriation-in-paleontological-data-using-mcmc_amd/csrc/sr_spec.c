@@ -93,6 +93,11 @@ int main(int argc, char **argv)
 #ifndef SR_ARCH
 #define SR_ARCH "gfx950"
 #endif
+/* extra device definitions of an experimental library build (tools/build_variant.sh): its specialised
+   kernels are compiled with them too (they are part of the key) */
+#ifndef SR_SPEC_EXTRA
+#define SR_SPEC_EXTRA ""
+#endif
 
 /* resolved once per process: the library's directory, its snapshot and whether it is intact */
 static struct {
@@ -205,8 +210,8 @@ static int profiler_preloaded(void)
 
 static void defs_of(const sr_spec_shape *s, char *defs, size_t len)
 {
-  snprintf(defs, len, "-DSR_JIT -DSR_JIT_TB=%d -DSR_JIT_NWM=%d -DSR_FN=%d -DSR_FM=%d -DSR_FH=%d%s", s->TB, s->NWM, s->N,
-           s->M, s->NH, s->force ? " -DSR_FORCE_EXACT" : "");
+  snprintf(defs, len, "-DSR_JIT -DSR_JIT_TB=%d -DSR_JIT_NWM=%d -DSR_FN=%d -DSR_FM=%d -DSR_FH=%d%s%s%s", s->TB, s->NWM,
+           s->N, s->M, s->NH, s->force ? " -DSR_FORCE_EXACT" : "", SR_SPEC_EXTRA[0] ? " " : "", SR_SPEC_EXTRA);
 }
 
 static void cache_dir(char *dir, size_t len)
@@ -220,7 +225,7 @@ int sr_spec_path(const sr_spec_shape *s, char *path, size_t len)
 {
   pthread_once(&g_once, spec_init);
   if (g_spec.state) return g_spec.state;
-  char defs[256], dir[4200];
+  char defs[1024], dir[4200];
   defs_of(s, defs, sizeof defs);
   uint64_t h = g_spec.src_hash;
   h = fnv(h, defs, strlen(defs) + 1);
@@ -249,7 +254,7 @@ int sr_spec_object(const sr_spec_shape *s, char *path, size_t len)
   if (profiler_preloaded()) return SR_SPEC_EPROF;
   const char *cc = hipcc_path();
   if (access(cc, X_OK) != 0) return SR_SPEC_ENOCC;
-  char dir[4200], tmp[4500], log[4500], inc[4300], src[4300], arch[64], defs[256], fl[512];
+  char dir[4200], tmp[4500], log[4500], inc[4300], src[4300], arch[64], defs[1024], fl[1280];
   snprintf(dir, sizeof dir, "%s", path);
   *strrchr(dir, '/') = 0;
   mkdirs(dir);

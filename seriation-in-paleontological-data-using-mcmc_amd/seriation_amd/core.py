@@ -74,14 +74,14 @@ class Dataset:
 
 def make_opts(burnin_calls=1000, sample_calls=1000, sweeps_per_call=10, device=0, block_threads=0,
               calls_per_launch=0, check=True, columns="auto", debug_check=False, debug_print=False, rng="mt",
-              generic=False):
+              generic=False, manycd=0):
     """columns: "auto" (LDS when the layout fits, else HBM), "lds" or "hbm" (SR_F_*_COLUMNS).
     debug_check: mcmc_consistent after every mcmc_sample call (the reference's MCMCDEBUG,
     mcmc.c:249-255; SR_F_DEBUG_CHECK), debug_print: its acceptance-rate lines on stderr.
     rng: "mt" (the reference's GSL MT19937 stream, bit-exact) or "philox" (opt-in SR_F_RNG_PHILOX:
     counter-based Philox4x32-10 per chain for the sampling phase; statistically equivalent only).
     generic: the generic sweep kernel instead of the default shape-specialised one (SR_F_GENERIC_KERNEL;
-    identical results)."""
+    identical results).  manycd: 1 = per-taxon c[m], d[m] (mcmc_readmodel's manycd, mcmc.c:777-786, 807-816)."""
     o = L.sr_run_opts()
     L.lib().sr_default_opts(ctypes.byref(o))
     o.burnin_calls = burnin_calls
@@ -90,6 +90,7 @@ def make_opts(burnin_calls=1000, sample_calls=1000, sweeps_per_call=10, device=0
     o.device = device
     o.block_threads = block_threads
     o.calls_per_launch = calls_per_launch
+    o.manycd = 1 if manycd else 0
     o.flags = (0 if check else L.SR_F_NO_CHECK) | {"auto": 0, "lds": L.SR_F_LDS_COLUMNS,
                                                    "hbm": L.SR_F_HBM_COLUMNS}[columns]
     if debug_check:
@@ -127,13 +128,13 @@ class Session:
     ``calls`` mcmc_sample calls (mcmc.c:214-258) for every chain."""
 
     def __init__(self, dataset, seeds, device=0, sweeps_per_call=10, calls_per_launch=0, block_threads=0,
-                 chain_ids=None, columns="auto", debug_check=False, rng="mt", generic=False):
+                 chain_ids=None, columns="auto", debug_check=False, rng="mt", generic=False, manycd=0):
         self.ds = dataset
         self.n = len(seeds)
         self.specs = make_specs(seeds, chain_ids)
         self.opts = make_opts(sweeps_per_call=sweeps_per_call, device=device, block_threads=block_threads,
                               calls_per_launch=calls_per_launch, columns=columns, debug_check=debug_check, rng=rng,
-                              generic=generic)
+                              generic=generic, manycd=manycd)
         h = ctypes.c_void_p()
         _check(L.lib().sr_session_create(ctypes.byref(dataset.c), self.specs, self.n, ctypes.byref(self.opts),
                                          ctypes.byref(h)), "sr_session_create")
@@ -145,12 +146,13 @@ class Session:
 
     @classmethod
     def restore(cls, dataset, path, device=0, sweeps_per_call=10, calls_per_launch=0, block_threads=0,
-                columns="auto", rng="mt"):
-        """sr_session_restore: a session continuing the chains of a checkpoint over `dataset`."""
+                columns="auto", rng="mt", manycd=0):
+        """sr_session_restore: a session continuing the chains of a checkpoint over `dataset` (manycd must
+        name the checkpoint's kind)."""
         self = cls.__new__(cls)
         self.ds = dataset
         self.opts = make_opts(sweeps_per_call=sweeps_per_call, device=device, block_threads=block_threads,
-                              calls_per_launch=calls_per_launch, columns=columns, rng=rng)
+                              calls_per_launch=calls_per_launch, columns=columns, rng=rng, manycd=manycd)
         h = ctypes.c_void_p()
         _check(L.lib().sr_session_restore(ctypes.byref(dataset.c), os.fsencode(path), ctypes.byref(self.opts),
                                           ctypes.byref(h)), "sr_session_restore")
@@ -211,6 +213,19 @@ class Session:
             _check(L.lib().sr_session_fetch_records(self.h, 0, k, ab.ctypes.data_as(ctypes.POINTER(ctypes.c_int16)),
                                                     cdl.ctypes.data_as(ctypes.POINTER(ctypes.c_double))), "fetch")
         return ab, cdl
+
+    @property
+    def manycd(self):
+        return bool(L.lib().sr_session_manycd(self.h))
+
+    def fetch_cd_vectors(self):
+        """manycd sessions: every taxon's (c, d) of the k buffered calls, float64 [n, k, 2M] (c[M] then d[M])."""
+        k = L.lib().sr_session_records(self.h)
+        cv = np.zeros((self.n, k, 2 * self.ds.M), np.float64)
+        if k:
+            _check(L.lib().sr_session_fetch_cd_vectors(self.h, 0, k, cv.ctypes.data_as(ctypes.POINTER(ctypes.c_double))),
+                   "fetch_cd_vectors")
+        return cv
 
     def fetch_cdl(self):
         """(c, d, loglik) float64 [n, k, 3] of the k buffered calls, without the a/b/pi rows."""
@@ -306,20 +321,23 @@ def _devices(devices):
 
 def run_chains(dataset, seeds, burnin_calls=1000, sample_calls=1000, sweeps_per_call=10, device=0,
                chain_ids=None, keep_records=False, calls_per_launch=0, block_threads=0, columns="auto",
-               devices=None, debug_check=False, rng="mt", generic=False):
+               devices=None, debug_check=False, rng="mt", generic=False, manycd=0):
     """sr_run_chains: returns (summaries list of dicts, records or None).
-    records = (ab_pi int32 [n, ts, 2M+N], cdl [n, ts, 3]) when keep_records.
+    records = (ab_pi int32 [n, ts, 2M+N], cdl [n, ts, 3]) when keep_records, plus cdv [n, ts, 2M] (every
+    taxon's c then d) for manycd=1.
     devices: a list of HIP ordinals (may repeat) -> sr_run_chains_multi, chains sharded over them."""
     n = len(seeds)
     specs = make_specs(seeds, chain_ids)
     opts = make_opts(burnin_calls, sample_calls, sweeps_per_call, device, block_threads=block_threads,
                      calls_per_launch=calls_per_launch, columns=columns, debug_check=debug_check, rng=rng,
-                     generic=generic)
+                     generic=generic, manycd=manycd)
     out = (L.sr_chain_summary * n)()
     N, M = dataset.N, dataset.M
     recs = None
     if keep_records:
         recs = (np.zeros((n, sample_calls, 2 * M + N), np.int32), np.zeros((n, sample_calls, 3)))
+        if manycd:
+            recs = recs + (np.zeros((n, sample_calls, 2 * M)),)
 
     def sink(ctx, ci, si, rp):
         r = rp.contents
@@ -328,6 +346,9 @@ def run_chains(dataset, seeds, burnin_calls=1000, sample_calls=1000, sweeps_per_
         ab[M:2 * M] = np.ctypeslib.as_array(r.b, shape=(M,))
         ab[2 * M:] = np.ctypeslib.as_array(r.pi, shape=(N,))
         recs[1][ci, si] = (r.c, r.d, r.loglik)
+        if manycd:
+            recs[2][ci, si, :M] = np.ctypeslib.as_array(r.cv, shape=(M,))
+            recs[2][ci, si, M:] = np.ctypeslib.as_array(r.dv, shape=(M,))
         return 0
 
     cb = L.SINK_FN(sink) if keep_records else ctypes.cast(None, L.SINK_FN)
@@ -344,13 +365,13 @@ def run_chains(dataset, seeds, burnin_calls=1000, sample_calls=1000, sweeps_per_
 
 
 def run_to_dirs(dataset, seeds, root=".", chain_ids=None, burnin_calls=1000, sample_calls=1000, device=0,
-                sweeps_per_call=10, devices=None, rng="mt"):
+                sweeps_per_call=10, devices=None, rng="mt", manycd=0):
     """sr_run_to_dirs: writes Chains/chain_NN/*.csv under root like the reference main().
     sweeps_per_call is the thinning (the reference's mcmc_sample runs 10, mcmc.c:225).
     devices: HIP ordinals (may repeat) -> sr_run_to_dirs_multi."""
     n = len(seeds)
     specs = make_specs(seeds, chain_ids)
-    opts = make_opts(burnin_calls, sample_calls, sweeps_per_call, device, rng=rng)
+    opts = make_opts(burnin_calls, sample_calls, sweeps_per_call, device, rng=rng, manycd=manycd)
     out = (L.sr_chain_summary * n)()
     if devices:
         darr, nd = _devices(devices)

@@ -36,6 +36,7 @@ int srk_create(const sr_state_host *st, int device, int block_threads, int rec_c
                const uint32_t *pkey, int spec, srk_dev **out)
 {
   (void)block_threads; (void)gm_force; (void)pkey; (void)spec;
+  if (st->manycd) return -6;   /* (the fake device keeps no per-taxon c, d) */
   if (device < 0 || device >= 2) return -5;
   srk_dev *d = (srk_dev *)calloc(1, sizeof(*d));
   if (!d) return -5;
@@ -140,7 +141,7 @@ int srk_download_state(srk_dev *d, sr_state_host *st)
   return 0;
 }
 
-int srk_run_pipelined(srk_dev *d, int total, int cpl, int spc, int (*consume)(void *, int, int, const int16_t *, const double *),
+int srk_run_pipelined(srk_dev *d, int total, int cpl, int spc, int (*consume)(void *, int, int, const int16_t *, const double *, const double *),
                       void *ctx)
 {
   if (cpl <= 0 || 2 * cpl > d->rec_cap) return -1;
@@ -152,7 +153,7 @@ int srk_run_pipelined(srk_dev *d, int total, int cpl, int spc, int (*consume)(vo
     const int k = total - done < cpl ? total - done : cpl;
     rc = srk_run(d, k, spc, 1, 0);
     if (!rc) rc = srk_fetch_records(d, 0, k, ab, cd);
-    if (!rc && consume(ctx, done, k, ab, cd)) rc = -1;
+    if (!rc && consume(ctx, done, k, ab, cd, NULL)) rc = -1;
     done += k;
   }
   free(ab); free(cd);
@@ -187,3 +188,5 @@ void srk_destroy(srk_dev *d)
   free(d->rec); free(d->rcd);
   free(d);
 }
+/* manycd sessions are refused by the fake device (srk_create), so this is never reached */
+int srk_fetch_cdv(srk_dev *d, int f, int c, double *v) { (void)d; (void)f; (void)c; (void)v; return -1; }

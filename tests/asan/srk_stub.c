@@ -29,7 +29,7 @@ int srk_fetch_chain_records(srk_dev *d, int ch, int f, int c, int16_t *a, double
   (void)d; (void)ch; (void)f; (void)c; (void)a; (void)b;
   return -5;
 }
-int srk_run_pipelined(srk_dev *d, int total, int cpl, int spc, int (*consume)(void *, int, int, const int16_t *, const double *),
+int srk_run_pipelined(srk_dev *d, int total, int cpl, int spc, int (*consume)(void *, int, int, const int16_t *, const double *, const double *),
                       void *ctx)
 {
   (void)d; (void)total; (void)cpl; (void)spc; (void)consume; (void)ctx;
@@ -54,3 +54,4 @@ int srp_posterior_host(int device, int kind, const int16_t *ab, int n_sel, int c
   return -5;
 }
 void srk_destroy(srk_dev *d) { (void)d; }
+int srk_fetch_cdv(srk_dev *d, int f, int c, double *v) { (void)d; (void)f; (void)c; (void)v; return -5; }

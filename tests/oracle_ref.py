@@ -41,6 +41,11 @@ def load(path):
                                    ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                    P(ctypes.c_int32), P(ctypes.c_double), P(ctypes.c_int32), P(ctypes.c_double),
                                    P(ctypes.c_double), P(ctypes.c_longlong), P(ctypes.c_ulonglong)]
+    L.oracle_run_chain_v.restype = ctypes.c_int
+    L.oracle_run_chain_v.argtypes = [ctypes.c_char_p, ctypes.c_long, ctypes.c_int, ctypes.c_ulong, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     P(ctypes.c_int32), P(ctypes.c_double), P(ctypes.c_int32), P(ctypes.c_double),
+                                     P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_longlong), P(ctypes.c_ulonglong)]
     L.oracle_rng_stream.restype = None
     L.oracle_rng_stream.argtypes = [ctypes.c_ulong, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_long,
                                     P(ctypes.c_double), P(ctypes.c_ulonglong)]
@@ -74,8 +79,9 @@ def parse(text, maxs=2000):
     return 0, X.reshape(N.value, M.value), h
 
 
-def run_chain(text, seed, tb, ts, sweeps=10, check=0, maxs=2000, want_init=False, rng="mt"):
-    """Returns dict(rc, init (a,b,pi), init_cdl, rec_int [ts, 2M+N], rec_dbl [ts, 3], exp, acc, words).
+def run_chain(text, seed, tb, ts, sweeps=10, check=0, maxs=2000, want_init=False, rng="mt", manycd=0):
+    """Returns dict(rc, init (a,b,pi), init_cdl, rec_int [ts, 2M+N], rec_dbl [ts, 3], exp, acc, words) and, for
+    manycd=1 (per-taxon c, d: mcmc.c:777-786, 807-816), rec_cdv [ts, 2M] (every taxon's c then d per sample).
     rng="philox": the sampling phase on the Philox stream (the product's SR_F_RNG_PHILOX)."""
     if isinstance(text, str):
         text = text.encode()
@@ -91,12 +97,16 @@ def run_chain(text, seed, tb, ts, sweeps=10, check=0, maxs=2000, want_init=False
     ex = np.zeros(3)
     acc = np.zeros(7, np.int64)
     words = ctypes.c_ulonglong()
-    rc = lib().oracle_run_chain(text, len(text), maxs, seed, 0, tb, ts, sweeps, check,
-                                _p(init, ctypes.c_int32), _p(initd, ctypes.c_double),
-                                _p(ri, ctypes.c_int32), _p(rd, ctypes.c_double), _p(ex, ctypes.c_double),
-                                _p(acc, ctypes.c_longlong), ctypes.byref(words))
-    return dict(rc=rc, N=N, M=M, init=init, init_cdl=initd, rec_int=ri[:ts * W].reshape(ts, W),
-                rec_dbl=rd[:ts * 3].reshape(ts, 3), exp=ex, acc=acc, words=words.value)
+    cv = np.zeros(max(ts, 1) * 2 * M) if manycd else None
+    rc = lib().oracle_run_chain_v(text, len(text), maxs, seed, 1 if manycd else 0, tb, ts, sweeps, check,
+                                  _p(init, ctypes.c_int32), _p(initd, ctypes.c_double),
+                                  _p(ri, ctypes.c_int32), _p(rd, ctypes.c_double), _p(cv, ctypes.c_double),
+                                  _p(ex, ctypes.c_double), _p(acc, ctypes.c_longlong), ctypes.byref(words))
+    out = dict(rc=rc, N=N, M=M, init=init, init_cdl=initd, rec_int=ri[:ts * W].reshape(ts, W),
+               rec_dbl=rd[:ts * 3].reshape(ts, 3), exp=ex, acc=acc, words=words.value)
+    if manycd:
+        out["rec_cdv"] = cv[:ts * 2 * M].reshape(ts, 2 * M)
+    return out
 
 
 def rng_stream(seed, kind, count, a=0.0, b=0.0):

@@ -138,19 +138,38 @@ def test_product_cli_stderr_lines_on_fake_device(tmp_path):
     assert ref_lines(pa.stderr) == ref_lines(pb.stderr) and len(ref_lines(pb.stderr)) == 7
 
 
-def test_manycd_refused(tmp_path):
-    """`mcmc manycd Tburnin T` with manycd = 1 (per-taxon c, d: mcmc.c:118, 777-786, 807-816) is refused
-    with SR_EUNSUPPORTED's message and exit 1 before any device call; the reference's own driver never
-    sets it (script.py:44 passes the chain index alone).  The library refuses it the same way."""
-    p = run_cli(PRODUCT_CLI, str(tmp_path), "g5s5.txt", ["1", "2", "2"], 5, "chain_00")
-    assert p.returncode == 1
-    assert L.lib().sr_strerror(L.SR_EUNSUPPORTED).decode() in p.stderr.decode()
+def test_oracle_cli_manycd_format(tmp_path):
+    """`mcmc 1 Tburnin T` (manycd = 1, mcmc.c:118): every taxon carries its own c, d -- chain_data.csv's c and
+    d fields (mcmc.c:86-90) and taxa.csv's columns differ between taxa, the oracle's records say the same."""
+    oracle_ref.lib()
+    p = run_cli(ORACLE_CLI, str(tmp_path), "g10s10.txt", ["1", "2", "3"], 7, "chain_00")
+    assert p.returncode == 0, p.stderr
+    files = read_dir(str(tmp_path), "chain_00")
+    M = 139
+    f = files["chain_data.csv"].decode().splitlines()[-1].split(",")
+    assert len(set(f[3].split())) > 1 and len(set(f[4].split())) > 1
+    o = oracle_ref.run_chain(open(os.path.join(DS, "g10s10.txt"), "rb").read(), 7, 2, 3, manycd=1)
+    import math
+    assert f[3].split() == ["%.14f" % math.exp(v) for v in o["rec_cdv"][-1][:M]]
+    assert f[4].split() == ["%.14f" % math.exp(v) for v in o["rec_cdv"][-1][M:]]
+
+
+def test_manycd_block_size_and_no_specialised_kernel():
+    """manycd sessions run the generic 1024-thread kernels: any other block size is SR_EUNSUPPORTED before a
+    device call, and no shape-specialised kernel exists for them (sr_specialize reports 0)."""
     import ctypes
     import seriation_amd as sa
     ds = sa.Dataset.load(os.path.join(DS, "g5s5.txt"))
-    o = L.sr_run_opts()
-    L.lib().sr_default_opts(ctypes.byref(o))
-    o.manycd = 1
+    o = sa.core.make_opts(manycd=1, block_threads=512)
     h = ctypes.c_void_p()
     assert L.lib().sr_session_create(ctypes.byref(ds.c), sa.core.make_specs([1]), 1, ctypes.byref(o), ctypes.byref(h)) == \
         L.SR_EUNSUPPORTED
+    o = sa.core.make_opts(manycd=1)
+    assert L.lib().sr_specialize(ctypes.byref(ds.c), ctypes.byref(o)) == 0
+
+
+@pytest.mark.gpu
+def test_product_cli_manycd_byte_identical(tmp_path):
+    """manycd = 1 through the drop-in CLI: the five files byte-identical to the oracle CLI's (per-taxon c, d in
+    chain_data.csv and taxa.csv)."""
+    _compare(tmp_path, "g10s10.txt", ["1", "5", "12"], 11, "chain_00")

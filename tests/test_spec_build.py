@@ -18,7 +18,7 @@ PKG = os.path.join(ROOT, "seriation-in-paleontological-data-using-mcmc_amd")
 LIBDIR = os.path.join(PKG, "build")
 SYNTH = os.path.join(ROOT, "tests", "golden", "datasets", "synth_256x512.txt")
 HIPCC = "/opt/rocm/bin/hipcc"
-BENCH_KERNEL = b"_Z15sr_sweep_kernelILi512ELi9ELb0ELb0ELb0EEv5KArgs"
+BENCH_KERNEL = b"_Z15sr_sweep_kernelILi512ELi9ELb0ELb0ELb0ELb0EEv5KArgs"
 
 needs_hipcc = pytest.mark.skipif(not os.access(HIPCC, os.X_OK), reason="no hipcc")
 

@@ -3079,7 +3079,7 @@ struct srk_kplan { int TB, pr, gm, mcd; size_t lds; };
 
 static int plan_kernel(int N, int M, int nh, int block_threads, int gm_force, int mcd, srk_kplan *kp)
 {
-  if (nh > SR_NHMAX || N > 32767 || M > 32767) return -6;
+  if (nh > SR_NHMAX || N > 4095 || M > SR_MMAX) return -6;
   const int NW = (N + 31) / 32;
   int TB = block_threads;
   if (mcd) {   /* manycd: 1024 threads (one or more taxa per thread) */

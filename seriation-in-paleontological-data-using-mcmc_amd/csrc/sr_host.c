@@ -438,8 +438,9 @@ static int session_new(const sr_dataset *ds, const sr_chain_spec *specs, int32_t
   if (o.sweeps_per_call <= 0) return SR_EINVAL;
   o.manycd = o.manycd != 0;   /* mcmc_readmodel stores the flag; any nonzero value means per-taxon c, d */
   /* nh <= 64 hard sites (a 64-bit mask per taxon), N <= 4095 (12-bit positions in the packed proposal
-     records); records are int16 (M <= 32767).  The LDS layout must also fit 160 KB (srk_create). */
-  if (ds->nh > SR_NHMAX || ds->N > 4095 || ds->M > 32767) return SR_EUNSUPPORTED;
+     records, int16 a, b, pi records), M <= SR_MMAX taxa (several per thread beyond the block; the records hold
+     positions only).  The LDS layout must also fit 160 KB (srk_create), else HBM columns. */
+  if (ds->nh > SR_NHMAX || ds->N > 4095 || ds->M > SR_MMAX) return SR_EUNSUPPORTED;
   sr_session *s = (sr_session *)calloc(1, sizeof(*s));
   if (!s) return SR_ENOMEM;
   s->ds.N = ds->N; s->ds.M = ds->M; s->ds.nh = ds->nh;

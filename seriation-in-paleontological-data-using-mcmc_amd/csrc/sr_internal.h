@@ -9,6 +9,7 @@
 
 #define SR_NHMAX 64      /* hard sites per dataset the kernel supports (a 64-bit mask per taxon; one per lane) */
 #define SR_RING 8        /* MT19937 blocks resident per chain */
+#define SR_MMAX (1 << 20)   /* taxa per dataset (int32 indices; per-chain columns and records grow with M) */
 
 /* Per-chain state in HBM, struct-of-arrays over chains.  Layout (per chain c):
  *   P   [NW][M] u32  position-ordered occurrence columns: bit (p&31) of P[p>>5][m]

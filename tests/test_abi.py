@@ -168,7 +168,8 @@ def test_hard_site_limit_boundary():
     """The kernel holds at most SR_NHMAX = 64 hard sites (a 64-bit mask per taxon, one hard site per
     lane): 65 are refused with SR_EUNSUPPORTED before any device call (40 and 64 run bit-exact in
     tests/test_gpu_edge.py 'nh40' / 'nh64').  Sites are limited to N <= 4095 (12-bit positions in the
-    packed proposal records): 4096 are refused the same way.  The reference has neither limit."""
+    packed proposal records): 4096 are refused the same way.  The reference has neither limit.  Taxa are
+    not limited by the records (they hold positions): M = 40000 is accepted."""
     def text(nh, N=90, M=6):
         rows = ["%d %d" % (N, M)]
         for i in range(N):
@@ -187,8 +188,9 @@ def test_hard_site_limit_boundary():
     with pytest.raises(sa.SrError) as e:
         sa.Session(big, [1])
     assert e.value.code == L.SR_EUNSUPPORTED
-    if not _gpu_present():
-        for ok in (sa.Dataset.parse(text(64)), sa.Dataset.parse(text(3, N=4095, M=2), maxs=0)):
+    if not _gpu_present():   # (taxa beyond int16: M = 40000 runs, tests/test_gpu_edge.py::test_taxa_beyond_int16)
+        for ok in (sa.Dataset.parse(text(64)), sa.Dataset.parse(text(3, N=4095, M=2), maxs=0),
+                   sa.Dataset.parse(text(3, N=8, M=40000), maxs=0)):
             with pytest.raises(sa.SrError) as e:
                 sa.Session(ok, [1])
             assert e.value.code == L.SR_EDEVICE   # accepted by the limit check, then no device

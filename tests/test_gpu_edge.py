@@ -214,3 +214,19 @@ def test_pair_kernel_parity(monkeypatch, name, N, M, nh):
         np.testing.assert_array_equal(ri[k], o["rec_int"], err_msg="%s seed %d" % (name, s))
         assert np.array_equal(rd[k].view(np.uint64), o["rec_dbl"].view(np.uint64)), (name, s)
         assert summ[k]["consistent"] == 0
+
+
+def test_taxa_beyond_int16():
+    """M = 40 000 taxa (beyond int16; the records hold positions only): HBM columns, one workgroup of 1024
+    threads with ~40 taxa per thread, one chain x (1 + 2) calls equal to the oracle bit for bit."""
+    N, M = 40, 40000
+    text = make_text(N, M, 3, seed=4040000)
+    ds = sa.Dataset.parse(text, maxs=0)
+    with sa.Session(ds, [2]) as s:
+        assert s.variant == "hbm" and s.block_threads == 1024
+    summ, (ri, rd) = sa.run_chains(ds, [2], burnin_calls=1, sample_calls=2, keep_records=True)
+    o = oracle_ref.run_chain(text, 2, 1, 2, maxs=0)
+    assert o["rc"] == 0
+    np.testing.assert_array_equal(ri[0], o["rec_int"])
+    assert np.array_equal(rd[0].view(np.uint64), o["rec_dbl"].view(np.uint64))
+    assert summ[0]["consistent"] == 0

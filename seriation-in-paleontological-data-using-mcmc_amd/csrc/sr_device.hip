@@ -72,7 +72,8 @@ struct KArgs {
   unsigned long long *dbg;   /* SR_STAMPS builds: [chain][16] cycles per phase */
   uint16_t *gpre;            /* gm variant scratch, per chain: column prefix tables */
   uint32_t *pkey;            /* [chain][2] Philox keys (SR_F_RNG_PHILOX), else null: MT19937 */
-  double *gck, *glbuf, *gcbuf;   /* gm variant scratch: Gibbs checkpoints, logl terms, exact-delta terms */
+  float *gck;                    /* gm variant scratch: Gibbs checkpoints (f32: half the bytes of the scratch stream) */
+  double *glbuf, *gcbuf;         /* gm variant scratch: logl terms, exact-delta terms */
   int *xflag, *xbuf, *xerr;      /* split chains (SP kernels): [chain][2] progress flags, exchange slots, timeout flag */
   double *cdv, *cdx;   /* manycd (MCD kernels): [chain][2M] per-taxon c, d (state); [chain][2M] their cc, dd (scratch) */
   double *rec_cdv;     /* manycd: [chain][rec_cap][2M] per-taxon c, d of every saved sample */
@@ -748,7 +749,8 @@ __device__ __forceinline__ double exp2_split(double q)
 template <bool B8>
 __device__ __forceinline__ int draw_fast(const uint32_t *Pm, const uint16_t *prem, int M, int N, int NW, bool rev, int o, int L,
                                          int POo, double u, const CD &K, const sr_mtab &tb, double vA, double vB, double rA, double rB,
-                                         const double *T4, const double *T8, double *ck, int ckstride, uint64_t *fbk, int &dt0, int &df0,
+                                         const double *T4, const double *T8, typename std::conditional<B8, float, double>::type *ck,
+                                         int ckstride, uint64_t *fbk, int &dt0, int &df0,
                                          int &dt1, int &df1 GSTAMP_ARGS)
 {
   /* POo: ones among walk entries [0, o), from the caller's column prefix table */
@@ -878,7 +880,7 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, const uint16_t *pre
               y = y * t4.y;
             }
           }
-          ck[k * ckstride] = S;
+          ck[k * ckstride] = S;   /* (B8: rounded to f32; pass 2 covers it by ABS) */
         }
       }
     }
@@ -890,12 +892,17 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, const uint16_t *pre
      sum by at most ~9 2^-53 S (the subtraction and the word's fma roundings in pass 1): the extra
      absolute slack 2^-46 in u covers it; the unscaled sums' own rounding (and, with the byte tables in
      pass 1, the relative difference of the two table forms, <= 2 x 16 ulp) is inside REL's + 32.
+     B8 (HBM columns): the checkpoints are stored as f32 (half the scratch stream that spills L2): each is
+     within 2^-24 S of its f64 value, so the word search may land one word off (then the word's first or
+     last entry fails its certification and the exact walk runs) and a reconstructed partial sum moves by
+     at most 3 2^-24 S (Sp0, Sj and y = (Sj - Sp0) / sum): the absolute slack grows by 2^-21, which a
+     uniform u hits with probability ~2^-20 per draw.
      Ones before the word from the column prefix table. */
   int res = -1, POp = 0;
   if (S > 0.0 && S < 0x1p1000 && !uf) {
     const double inv = 1.0 / S;
     const double REL = (double)(N + 33) * 0x1p-50;
-    const double ABS = (double)(N + 1) * 0x1p-39 + 0x1p-46;
+    const double ABS = (double)(N + 1) * 0x1p-39 + 0x1p-46 + (B8 ? 0x1p-21 : 0.0);
     int j = klo;   /* first window word whose checkpoint reaches u (checkpoints ascend) */
     for (int k0 = klo; k0 < khi; k0 += SR_WCH) {
       double cv[SR_WCH];
@@ -1877,7 +1884,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   int16_t *hcnt = (int16_t *)(smem + L.ht) + wave * (2 * N + 2);    /* this wave's hard-site tables */
   int16_t *nhall = hcnt + N + 1;
   const int CKS = SP ? 2 * TB : sr_ckstride(M, TB);   /* SP: slots [half TB + tid] */
-  double *ckb = GM ? A.gck + (size_t)chain * (SP ? sr_sp_ck(N, TB) : sr_gm_ck(N, M, TB)) : (double *)(smem + L.ck);
+  using CKT = typename std::conditional<GM, float, double>::type;   /* Gibbs checkpoints: f32 in HBM scratch, f64 in LDS */
+  CKT *ckb = GM ? (CKT *)(void *)(A.gck + (size_t)chain * (SP ? sr_sp_ck(N, TB) : sr_gm_ck(N, M, TB))) : (CKT *)(void *)(smem + L.ck);
   const int ckslot = SP ? half * TB + tid : tid;   /* this thread's Gibbs checkpoint slots */
   int *ccnt = (int *)(smem + L.ccnt);
   int32_t *sab = GM ? A.ab + (size_t)chain * 2 * M : (int32_t *)(smem + L.sab);     /* a[M], b[M] */
@@ -3295,7 +3303,7 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
   if (pkey) rc |= dev_alloc_copy(d, &A.pkey, pkey, C * 2);
   if (d->gm) {
     rc |= dev_alloc_copy(d, &A.gpre, (const uint16_t *)nullptr, C * sr_gm_pre(st->M, st->NW));
-    rc |= dev_alloc_copy(d, &A.gck, (const double *)nullptr, C * (d->sp ? sr_sp_ck(st->N, TB) : sr_gm_ck(st->N, st->M, TB)));
+    rc |= dev_alloc_copy(d, &A.gck, (const float *)nullptr, C * (d->sp ? sr_sp_ck(st->N, TB) : sr_gm_ck(st->N, st->M, TB)));
     rc |= dev_alloc_copy(d, &A.glbuf, (const double *)nullptr, C * st->M);
     rc |= dev_alloc_copy(d, &A.gcbuf, (const double *)nullptr, C * sr_gm_cbuf(st->M));
   }

@@ -358,6 +358,11 @@ def main():
             "sites": ds.N, "taxa": ds.M, "chains": total_chains, "chains_per_gpu": C,
             "sweeps_per_step": sweeps_per_step, "block_threads": sess.block_threads, "columns": sess.variant,
             "kernel": sess.kernel,   # "split": two workgroups per chain (HBM columns)
+            # split chains need both halves resident: hipLaunchCooperativeKernel (the product path), or an ordinary
+            # launch of the same grid under SR_COOP=0 (the profiling runs: rocprofv3's tracer aborts at exit after
+            # cooperative launches)
+            "launch": ("ordinary (SR_COOP=0)" if os.environ.get("SR_COOP") == "0" else "cooperative")
+                      if sess.kernel == "split" else "ordinary",
             "kernel_build": "specialized" if sess.specialized else "generic",   # the default is specialized
             "rng": "GSL MT19937 (the reference's stream)" if args.rng == "mt" else "Philox4x32-10 (opt-in)",
             "parallelism": "chains sharded over %d GPU(s), %s all-gather at end" % (

@@ -79,6 +79,24 @@ struct KArgs {
   double *rec_cdv;     /* manycd: [chain][rec_cap][2M] per-taxon c, d of every saved sample */
 };
 
+/* The launch arguments re-read from the kernarg segment (constant for the launch; the kernel's only
+ * argument is KArgs, at offset 0): the record and state pointers used after the sweeps come from here, so
+ * they are not held live (in spilled SGPRs) across the sweep loop.  SR_KARG_RELOAD=0: the by-value copy. */
+#ifndef SR_KARG_RELOAD
+#define SR_KARG_RELOAD 0
+#endif
+__device__ __forceinline__ const KArgs &kargs_late(const KArgs &A)
+{
+#if SR_KARG_RELOAD
+  (void)A;
+  const KArgs *p = (const KArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+  __asm__ volatile("" : "+s"(p));   /* an opaque pointer: the loads stay here, after the loop */
+  return *p;
+#else
+  return A;
+#endif
+}
+
 /* ---------------------------------------------------------------- LDS carve */
 struct Lay {
   size_t tab, cbuf, lbuf, mt, P, rpi0, rpi1, ht, ck, ccnt, sab, scnt, hpw, hbw, t4, t8, pre, part, tot, xs, ptab, misc, total;
@@ -2929,9 +2947,10 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 
     /* ---------------- saved sample (mcmc_save_chain, mcmc.c:69-92) */
     if (A.save) {
-      const int slot = A.rec_base + call;
+      const KArgs &B = kargs_late(A);
+      const int slot = B.rec_base + call;
       const int W = 2 * M + N;
-      int16_t *rec = A.rec_abpi + ((size_t)chain * A.rec_cap + slot) * W;
+      int16_t *rec = B.rec_abpi + ((size_t)chain * B.rec_cap + slot) * W;
       if constexpr (SP) {   /* own taxa; the permutation and c, d, loglik from half 0 */
         for (int m = olo + tid; m < ohi; m += TB) { rec[m] = (int16_t)sab[m]; rec[M + m] = (int16_t)sab[M + m]; }
       } else {
@@ -2941,11 +2960,11 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       if (!SP || half == 0)
         for (int n = tid; n < N; n += TB) rec[2 * M + rc[n]] = (int16_t)n;
       if (tid == 0 && (!SP || half == 0)) {
-        double *rd = A.rec_cdl + ((size_t)chain * A.rec_cap + slot) * 3;
+        double *rd = B.rec_cdl + ((size_t)chain * B.rec_cap + slot) * 3;
         rd[0] = c; rd[1] = d; rd[2] = loglik;
       }
       if constexpr (MCD) {   /* every taxon's c, d (mcmc.c:86-90) */
-        double *rv = A.rec_cdv + ((size_t)chain * A.rec_cap + slot) * 2 * M;
+        double *rv = B.rec_cdv + ((size_t)chain * B.rec_cap + slot) * 2 * M;
         for (int m = tid; m < 2 * M; m += TB) rv[m] = cv[m];
       }
     }
@@ -2964,28 +2983,29 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 }
 #endif
   __syncthreads();
-  uint32_t *oP = A.P + (size_t)chain * NW * M;
+  const KArgs &B = kargs_late(A);
+  uint32_t *oP = B.P + (size_t)chain * NW * M;
   if (!GM) for (int i = tid; i < NW * M; i += TB) oP[i] = P[i];
   const int32_t *rc = rcur ? rpiB : rpiA;
-  int32_t *orpi = A.rpi + (size_t)chain * N;
-  uint32_t *omt = A.mt + (size_t)chain * SR_RING * SR_MT_N;
+  int32_t *orpi = B.rpi + (size_t)chain * N;
+  uint32_t *omt = B.mt + (size_t)chain * SR_RING * SR_MT_N;
   if (!SP || half == 0) {   /* SP: block-uniform state, identical in both halves */
     for (int i = tid; i < N; i += TB) orpi[i] = rc[i];
     for (int i = tid; i < SR_RING * SR_MT_N; i += TB) omt[i] = ring[i];
   }
-  int32_t *oab = A.ab + (size_t)chain * 2 * M;
+  int32_t *oab = B.ab + (size_t)chain * 2 * M;
   if (!GM) for (int i = tid; i < 2 * M; i += TB) oab[i] = sab[i];
-  int32_t *ocnt = A.cnt + (size_t)chain * 4 * M;
+  int32_t *ocnt = B.cnt + (size_t)chain * 4 * M;
   if (!GM) for (int i = tid; i < 4 * M; i += TB) ocnt[i] = scnt[i];
   if (tid == 0) {
-    uint64_t *acc = A.acc + (size_t)chain * SR_NACC;
+    uint64_t *acc = B.acc + (size_t)chain * SR_NACC;
     if (!SP || half == 0) {
-      for (int k = 0; k < nh; ++k) A.hp[(size_t)chain * SR_NHMAX + k] = hp[k];
-      A.cdl[(size_t)chain * 4 + 0] = c;
-      A.cdl[(size_t)chain * 4 + 1] = d;
-      A.cdl[(size_t)chain * 4 + 2] = loglik;
-      A.rng[(size_t)chain * 2 + 0] = (uint64_t)R.blk * SR_MT_N + R.off;
-      A.rng[(size_t)chain * 2 + 1] = R.gen;
+      for (int k = 0; k < nh; ++k) B.hp[(size_t)chain * SR_NHMAX + k] = hp[k];
+      B.cdl[(size_t)chain * 4 + 0] = c;
+      B.cdl[(size_t)chain * 4 + 1] = d;
+      B.cdl[(size_t)chain * 4 + 2] = loglik;
+      B.rng[(size_t)chain * 2 + 0] = (uint64_t)R.blk * SR_MT_N + R.off;
+      B.rng[(size_t)chain * 2 + 1] = R.gen;
       for (int k = 0; k < 7; ++k)
         if (k != 2) acc[k] += misc[MS_ACC + k];
       acc[7] += misc[MS_NEXACT];

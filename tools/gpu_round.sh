@@ -12,8 +12,11 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${1:-round}
 mkdir -p "$OUT"
 B="bench.py"
-P="bench.py --no-cpu-baseline --steps 5 --warmup 3"
-C5="bench.py --no-cpu-baseline --sites 1024 --taxa 2048 --calls-per-step 2 --steps 10 --warmup 3 --block-threads 1024"
+P="bench.py --no-cpu-baseline --parity-chains 0 --steps 5 --warmup 3"
+C5="bench.py --no-cpu-baseline --parity-chains 0 --sites 1024 --taxa 2048 --calls-per-step 2 --steps 10 --warmup 3 --block-threads 1024"
+# the config-5 bench line re-checks its first 4 saved calls of 2 selected chains against the oracle (the CPU
+# oracle takes ~25 ms per 1024 x 2048 sweep); the profiled runs skip the parity leg
+C5B="${C5/--parity-chains 0/--parity-chains 2 --parity-calls 4}"
 SQA="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA"
 SQB="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH"
 if [ "$2" != "skip-tests" ]; then
@@ -26,7 +29,7 @@ timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o w -- python3 $P > "$OUT/pmc_write.log" 2>&1 &&
 timeout -s KILL 180 rocprofv3 --pmc $SQA --output-format csv -d "$OUT/pmc_sq" -o s -- python3 $P > "$OUT/pmc_sq.log" 2>&1 &&
 timeout -s KILL 180 rocprofv3 --pmc $SQB --output-format csv -d "$OUT/pmc_sq_b" -o s -- python3 $P > "$OUT/pmc_sq_b.log" 2>&1 &&
-timeout -k 10 200 python $C5 > "$OUT/c5_bench.json" 2> "$OUT/c5_bench.err" && export SR_COOP=0 &&   # (rocprofv3 + cooperative launch: see tools/gpu_c5_round.sh)
+timeout -k 10 200 python $C5B > "$OUT/c5_bench.json" 2> "$OUT/c5_bench.err" && export SR_COOP=0 &&   # (rocprofv3 + cooperative launch: see tools/gpu_c5_round.sh)
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c5_prof" -o c5 -- python3 $C5 > "$OUT/c5_prof.log" 2>&1 &&
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/c5_fetch" -o f -- python3 $C5 > "$OUT/c5_fetch.log" 2>&1 &&
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/c5_write" -o w -- python3 $C5 > "$OUT/c5_write.log" 2>&1 &&

@@ -141,7 +141,7 @@ __host__ __device__ static constexpr inline Lay sr_layout(int N, int M, int NW, 
   L.ccnt = o;  o = sr_al16(o + (size_t)2 * KT * 4);
   L.sab = o;   o = sr_al16(o + g * 2 * M * 4);
   L.scnt = o;  o = sr_al16(o + g * 4 * M * 4);
-  L.hpw = o;   o = sr_al16(o + (size_t)NWV * SR_NHMAX * 4);           /* per wave: hard positions */
+  L.hpw = o;   o = sr_al16(o + (size_t)NWV * SR_NHCAP(nh) * 4);       /* per wave: hard positions */
   L.hbw = o;   o = sr_al16(o + (size_t)NWV * NW * 4);                 /* per wave: hard bitmap */
   L.t4 = o;    o = sr_al16(o + NT * 160 * 8);                         /* per wave: 4-entry step tables (T4STRIDE) */
   L.t8 = o;    o = sr_al16(o + (rw ? NT : (gm ? 1 : 0)) * T8STRIDE * 8);   /* per wave (gm: one shared copy): 8-entry step tables */
@@ -1694,7 +1694,7 @@ __device__ __forceinline__ void build_hard_tables(const int *hp, int nh, int N, 
   /* hard bitmap (hbw: this wave's NW words, NW <= 64), then ranks by ballot over positions */
   for (int w = lane; w < NW; w += 64) hbw[w] = 0u;
   wsync();
-  if (lane < nh) { const int h = hp[lane]; atomicOr(&hbw[h >> 5], 1u << (h & 31)); }
+  for (int k = lane; k < nh; k += 64) { const int h = hp[k]; atomicOr(&hbw[h >> 5], 1u << (h & 31)); }
   wsync();
   int base = 0;
   for (int x0 = 0; x0 <= N; x0 += 64) {
@@ -1719,7 +1719,7 @@ template <typename HM = uint64_t>
 __device__ __forceinline__ HM hard_bits_col(const uint32_t *Pm, int M, int hl, int nh)
 {
   HM hbm = 0;
-  if (nh > 0) {
+  if (nh > 0 && nh <= SR_NHMAX) {   /* (more hard sites: the bitmap path of taxon_dt) */
 #pragma unroll
     for (int k = 0; k < 16; ++k) {   /* independent loads, one round trip */
       const int h = __builtin_amdgcn_readlane(hl, min(k, nh - 1));
@@ -1734,9 +1734,12 @@ __device__ __forceinline__ HM hard_bits_col(const uint32_t *Pm, int M, int hl, i
   return hbm;
 }
 
+/* hbx: the wave's hard bitmap when there are more than SR_NHMAX hard sites (the column's ones at hard
+ * positions then come from the bitmap, word by word), else nullptr (the mask hbm) */
 template <typename HM>
 __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, const uint32_t *Pm, const uint16_t *prem,
-                                         int M, HM hbm, const int16_t *hcnt, const int16_t *nhall, int &dt0, int &dt1)
+                                         int M, HM hbm, const int16_t *hcnt, const int16_t *nhall, int &dt0, int &dt1,
+                                         const uint32_t *hbx = nullptr)
 {
   const int i = q.i, j = q.j;
   dt0 = 0; dt1 = 0;
@@ -1782,6 +1785,11 @@ __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, 
       if (hi < lo) { cnt = 0; return 0; }
       const int kl = hcnt[lo], kh = hcnt[hi + 1];
       cnt = kh - kl;
+      if (hbx) {   /* many hard sites: ones of the column at the hard positions of [lo, hi], word by word */
+        int o = 0;
+        for (int w = lo >> 5; w <= (hi >> 5); ++w) o += __popc(Pm[w * M] & hbx[w] & range_mask(w, lo, hi));
+        return o;
+      }
       constexpr int HB = 8 * (int)sizeof(HM);
       const HM km = ((kh >= HB) ? ~(HM)0 : (((HM)1 << kh) - (HM)1)) & ~((kl >= HB) ? ~(HM)0 : (((HM)1 << kl) - (HM)1));
       return (int)__popcll((uint64_t)(hbm & km));
@@ -1822,7 +1830,8 @@ __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, 
 template <bool PR, bool GM, bool SP, typename XSync>
 __device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const int32_t *sab, const uint32_t *P, const uint16_t *pre,
                                               int M, int KT, int olo, int ohi,
-                                              int hl, int nh, const int16_t *hcnt, const int16_t *nhall, double *cb, int *cc, double *xs,
+                                              int hl, int nh, const int16_t *hcnt, const int16_t *nhall, const uint32_t *hbx,
+                                              double *cb, int *cc, double *xs,
                                               int lane, int wave, int TB, XSync &&xsync, const double *kv = nullptr,
                                               const double *kx = nullptr)
 {
@@ -1833,7 +1842,7 @@ __device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const i
     int dt0 = 0, dt1 = 0;
     if (m < M && ev)
       taxon_dt(kind, q, sab[m], sab[M + m], P + m, pre + m, M, kind == PK_PI3 ? hard_bits_col<uint64_t>(P + m, M, hl, nh) : 0ull,
-               hcnt, nhall, dt0, dt1);
+               hcnt, nhall, dt0, dt1, hbx);
     CD Km = K;
     if (kv && m < M) { Km.c = kv[m]; Km.d = kv[M + m]; Km.cc = kx[m]; Km.dd = kx[M + m]; }
     const double tv = (m < M && ev) ? qval(dt0, -dt0, dt1, -dt1, Km) : 0.0;
@@ -1908,8 +1917,10 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   int *ccnt = (int *)(smem + L.ccnt);
   int32_t *sab = GM ? A.ab + (size_t)chain * 2 * M : (int32_t *)(smem + L.sab);     /* a[M], b[M] */
   int32_t *scnt = GM ? A.cnt + (size_t)chain * 4 * M : (int32_t *)(smem + L.scnt);  /* t0[M], f0[M], t1[M], f1[M] */
-  int *hp = (int *)(smem + L.hpw) + wave * SR_NHMAX;   /* this wave's copy of the hard positions */
+  const int NHC = SR_NHCAP(nh);   /* hard positions per chain in the state (64, or nh in whole waves) */
+  int *hp = (int *)(smem + L.hpw) + wave * NHC;   /* this wave's copy of the hard positions */
   uint32_t *hbw = (uint32_t *)(smem + L.hbw) + wave * NW;   /* this wave's hard bitmap */
+  const uint32_t *hbx = nh > SR_NHMAX ? hbw : nullptr;   /* many hard sites: hard ones from the bitmap */
   double *T4w = (double *)(smem + L.t4) + (PR ? 0 : wave) * T4STRIDE;   /* this wave's (PR: the block's) 4-step tables */
   constexpr bool SH8 = PR || GM;   /* one shared copy of the 8-step tables (built by waves 0-3, then a barrier) */
   double *T8w = (double *)(smem + L.t8) + (SH8 ? 0 : wave) * T8STRIDE;   /* this wave's (SH8: the block's) 8-step tables */
@@ -1967,7 +1978,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   }
   if (tid == 0) for (int q = MS_CAB; q < 64; ++q) misc[q] = 0;
 
-  if (lane < SR_NHMAX) hp[lane] = (lane < nh) ? A.hp[(size_t)chain * SR_NHMAX + lane] : -1;
+  for (int k = lane; k < NHC; k += 64) hp[k] = (k < nh) ? A.hp[(size_t)chain * NHC + k] : -1;
   wsync();
   double c = A.cdl[(size_t)chain * 4 + 0];
   double d = A.cdl[(size_t)chain * 4 + 1];
@@ -2558,7 +2569,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 q.Kn = hf ? qb.Kn : qa.Kn; q.r0 = hf ? qb.r0 : qa.r0;
                 int d0 = 0, d1 = 0;
                 if ((hf ? vb : va) && tx < M)
-                  taxon_dt(prop_kind(pa), q, a1, b1, P + tx, pre + tx, M, hb1, hcnt, nhall, d0, d1);
+                  taxon_dt(prop_kind(pa), q, a1, b1, P + tx, pre + tx, M, hb1, hcnt, nhall, d0, d1, hbx);
                 int Xa0, Xa1, Ya, Xb0, Xb1, Yb;
                 if (prop_kind(pa) == PK_PI1) {   /* dt in {-1, 0, 1}, dt0 dt1 = 0: ballot counts per parity */
                   const uint64_t p0m = __ballot(d0 > 0), n0m = __ballot(d0 < 0);
@@ -2593,7 +2604,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               if (sI >= p0 && sI < pend && !vetoed(sI)) {
                 const Prop q = load_prop(sI);
                 int dt0 = 0, dt1 = 0;
-                if (mt < ohi) taxon_dt(prop_kind(sI), q, a1, b1, P + mt, pre + mt, M, hb1, hcnt, nhall, dt0, dt1);
+                if (mt < ohi) taxon_dt(prop_kind(sI), q, a1, b1, P + mt, pre + mt, M, hb1, hcnt, nhall, dt0, dt1, hbx);
                 d0s[sI] = dt0; d1s[sI] = dt1;
               }
             }
@@ -2652,7 +2663,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 if (sI >= p0 && sI < pend && !vetoed(sI)) {
                   const Prop q = load_prop(sI);
                   int dt0 = 0, dt1 = 0;
-                  if (mv) taxon_dt(prop_kind(sI), q, a, b, P + m, pre + m, M, hb, hcnt, nhall, dt0, dt1);
+                  if (mv) taxon_dt(prop_kind(sI), q, a, b, P + m, pre + m, M, hb, hcnt, nhall, dt0, dt1, hbx);
                   x0s[sI] += dt0; x1s[sI] += dt1; ys[sI] += abs(dt0) + abs(dt1);
                 }
               }
@@ -2767,11 +2778,11 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             }
             if (!decided || (accept && want_logl && !have_exact)) {   /* the exact sequential delta */
               if constexpr (SP)
-                dl = sr_exact_delta<PR, GM, SP>(kind, q, K, sab, P, pre, M, KTC, olo, ohi, hl, nh, hcnt, nhall,
+                dl = sr_exact_delta<PR, GM, SP>(kind, q, K, sab, P, pre, M, KTC, olo, ohi, hl, nh, hcnt, nhall, hbx,
                                                 cbuf + xpar * KTC * sr_chunk(PR), xb + 272 + xpar * KTC, xs, lane, wave,
                                                 TB, xsync);
               else   /* (no exchange: the one-workgroup kernels never see the split machinery) */
-                dl = sr_exact_delta<PR, GM, SP>(kind, q, K, sab, P, pre, M, KTC, 0, M, hl, nh, hcnt, nhall,
+                dl = sr_exact_delta<PR, GM, SP>(kind, q, K, sab, P, pre, M, KTC, 0, M, hl, nh, hcnt, nhall, hbx,
                                                 cbuf + xpar * KTC * sr_chunk(PR), ccnt + xpar * KTC, xs, lane, wave, TB,
                                                 [] {}, cv, cx);
               xpar ^= 1;
@@ -2812,7 +2823,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             uint32_t *Pm = P + m;
             const int a = sab[m], b = sab[M + m];
             int dt0, dt1;
-            taxon_dt(kind, q, a, b, Pm, pre + m, M, kind == PK_PI3 ? hard_bits_col<HM>(Pm, M, hl, nh) : (HM)0, hcnt, nhall, dt0, dt1);
+            taxon_dt(kind, q, a, b, Pm, pre + m, M, kind == PK_PI3 ? hard_bits_col<HM>(Pm, M, hl, nh) : (HM)0, hcnt, nhall, dt0, dt1,
+                     hbx);
             scnt[m] += dt0; scnt[M + m] -= dt0; scnt[2 * M + m] += dt1; scnt[3 * M + m] -= dt1;
             if (kind == PK_PI1) {                                  /* mcmc.c:1266-1297 */
               /* the shifted words read 8 at a time before they are rewritten (one memory round trip
@@ -2907,22 +2919,24 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 else { if (n > j && n <= i) src = n - 1; else if (n == j) src = i; }
                 rn[n] = ro[src];
               }
-              {
-                const int h = (lane < nh) ? hp[lane] : -1;
+              for (int k0 = 0; k0 < nh; k0 += 64) {   /* one hard site per lane (several waves of them: > 64) */
+                const int k = k0 + lane;
+                const int h = (k < nh) ? hp[k] : -1;
                 int hn = h;
                 if (h == i) hn = j;
                 else if (i < j && h > i && h <= j) hn = h - 1;
                 else if (i > j && h >= j && h < i) hn = h + 1;
-                hmoved = __ballot(lane < nh && hn != h) != 0;
-                if (lane < nh) hp[lane] = hn;
+                hmoved = hmoved || __ballot(k < nh && hn != h) != 0;
+                if (k < nh) hp[k] = hn;
               }
             } else if (kind != PK_PI3) {
               for (int n = tid; n < N; n += TB) rn[n] = ro[(n >= i && n <= j) ? (i + j - n) : n];
-              {
-                const int h = (lane < nh) ? hp[lane] : -1;
-                const bool mv = lane < nh && h >= i && h <= j && i + j - h != h;
-                hmoved = __ballot(mv) != 0;
-                if (mv) hp[lane] = i + j - h;
+              for (int k0 = 0; k0 < nh; k0 += 64) {
+                const int k = k0 + lane;
+                const int h = (k < nh) ? hp[k] : -1;
+                const bool mv = k < nh && h >= i && h <= j && i + j - h != h;
+                hmoved = hmoved || __ballot(mv) != 0;
+                if (mv) hp[k] = i + j - h;
               }
             } else {
               for (int n = tid; n < N; n += TB)
@@ -3000,7 +3014,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   if (tid == 0) {
     uint64_t *acc = B.acc + (size_t)chain * SR_NACC;
     if (!SP || half == 0) {
-      for (int k = 0; k < nh; ++k) B.hp[(size_t)chain * SR_NHMAX + k] = hp[k];
+      for (int k = 0; k < nh; ++k) B.hp[(size_t)chain * NHC + k] = hp[k];
       B.cdl[(size_t)chain * 4 + 0] = c;
       B.cdl[(size_t)chain * 4 + 1] = d;
       B.cdl[(size_t)chain * 4 + 2] = loglik;
@@ -3107,7 +3121,7 @@ struct srk_kplan { int TB, pr, gm, mcd; size_t lds; };
 
 static int plan_kernel(int N, int M, int nh, int block_threads, int gm_force, int mcd, srk_kplan *kp)
 {
-  if (nh > SR_NHMAX || N > 4095 || M > SR_MMAX) return -6;
+  if (nh > N || N > 4095 || M > SR_MMAX) return -6;
   const int NW = (N + 31) / 32;
   int TB = block_threads;
   if (mcd) {   /* manycd: 1024 threads (one or more taxa per thread) */
@@ -3310,7 +3324,7 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
   int rc = 0;
   rc |= dev_alloc_copy(d, &A.P, st->P, C * st->NW * st->M);
   rc |= dev_alloc_copy(d, &A.rpi, st->rpi, C * st->N);
-  rc |= dev_alloc_copy(d, &A.hp, st->hp, C * SR_NHMAX);
+  rc |= dev_alloc_copy(d, &A.hp, st->hp, C * SR_NHCAP(st->nh));
   rc |= dev_alloc_copy(d, &A.ab, st->ab, C * 2 * st->M);
   rc |= dev_alloc_copy(d, &A.cnt, st->cnt, C * 4 * st->M);
   rc |= dev_alloc_copy(d, &A.cdl, st->cdl, C * 4);
@@ -3604,7 +3618,7 @@ extern "C" int srk_download_state(srk_dev *d, sr_state_host *st)
   const KArgs &A = d->args;
   if (st->P) HIPCHK(hipMemcpy(st->P, A.P, C * d->NW * d->M * 4, hipMemcpyDeviceToHost));
   if (st->rpi) HIPCHK(hipMemcpy(st->rpi, A.rpi, C * d->N * 4, hipMemcpyDeviceToHost));
-  if (st->hp) HIPCHK(hipMemcpy(st->hp, A.hp, C * SR_NHMAX * 4, hipMemcpyDeviceToHost));
+  if (st->hp) HIPCHK(hipMemcpy(st->hp, A.hp, C * SR_NHCAP(d->nh) * 4, hipMemcpyDeviceToHost));
   if (st->ab) HIPCHK(hipMemcpy(st->ab, A.ab, C * 2 * d->M * 4, hipMemcpyDeviceToHost));
   if (st->cnt) HIPCHK(hipMemcpy(st->cnt, A.cnt, C * 4 * d->M * 4, hipMemcpyDeviceToHost));
   if (st->cdl) HIPCHK(hipMemcpy(st->cdl, A.cdl, C * 4 * 8, hipMemcpyDeviceToHost));

@@ -352,7 +352,7 @@ static int state_alloc(sr_state_host *st, int N, int M, int nh, int C, int manyc
   if (st->manycd && !(st->cdv = (double *)calloc((size_t)C * 2 * M, 8))) return SR_ENOMEM;
   st->P = (uint32_t *)calloc((size_t)C * st->NW * M, 4);
   st->rpi = (int32_t *)calloc((size_t)C * N, 4);
-  st->hp = (int32_t *)calloc((size_t)C * SR_NHMAX, 4);
+  st->hp = (int32_t *)calloc((size_t)C * SR_NHCAP(nh), 4);
   st->ab = (int32_t *)calloc((size_t)C * 2 * M, 4);
   st->cnt = (int32_t *)calloc((size_t)C * 4 * M, 4);
   st->cdl = (double *)calloc((size_t)C * 4, 8);
@@ -394,7 +394,7 @@ static int init_chain(const sr_dataset *ds, uint64_t seed, sr_state_host *st, in
   memcpy(st->rpi + (size_t)c * N, x.rpi, N * 4);
   int k = 0;
   for (int s = 0; s < N; s++)
-    if (ds->hard[s]) st->hp[(size_t)c * SR_NHMAX + k++] = x.pi[s];
+    if (ds->hard[s]) st->hp[(size_t)c * SR_NHCAP(ds->nh) + k++] = x.pi[s];
   memcpy(st->ab + (size_t)c * 2 * M, x.a, M * 4);
   memcpy(st->ab + (size_t)c * 2 * M + M, x.b, M * 4);
   memcpy(st->cnt + (size_t)c * 4 * M, x.t0, M * 4);
@@ -440,7 +440,7 @@ static int session_new(const sr_dataset *ds, const sr_chain_spec *specs, int32_t
   /* nh <= 64 hard sites (a 64-bit mask per taxon), N <= 4095 (12-bit positions in the packed proposal
      records, int16 a, b, pi records), M <= SR_MMAX taxa (several per thread beyond the block; the records hold
      positions only).  The LDS layout must also fit 160 KB (srk_create), else HBM columns. */
-  if (ds->nh > SR_NHMAX || ds->N > 4095 || ds->M > SR_MMAX) return SR_EUNSUPPORTED;
+  if (ds->N > 4095 || ds->M > SR_MMAX) return SR_EUNSUPPORTED;
   sr_session *s = (sr_session *)calloc(1, sizeof(*s));
   if (!s) return SR_ENOMEM;
   s->ds.N = ds->N; s->ds.M = ds->M; s->ds.nh = ds->nh;
@@ -650,7 +650,7 @@ static int ck_parts(sr_state_host *st, ck_part *pt)
 {
   const size_t C = (size_t)st->nchains;
   ck_part q[SR_CK_PARTS] = {
-    {C * st->NW * st->M * 4, st->P}, {C * st->N * 4, st->rpi}, {C * SR_NHMAX * 4, st->hp},
+    {C * st->NW * st->M * 4, st->P}, {C * st->N * 4, st->rpi}, {C * SR_NHCAP(st->nh) * 4, st->hp},
     {C * 2 * st->M * 4, st->ab}, {C * 4 * st->M * 4, st->cnt}, {C * 4 * 8, st->cdl},
     {C * SR_RING * SR_MT_N * 4, st->mt}, {C * 2 * 8, st->rng}, {C * SR_NACC * 8, st->acc},
     {C * 2 * st->M * 8, st->cdv}};
@@ -689,7 +689,7 @@ SR_API int sr_session_checkpoint(sr_session *s, const char *path)
    the host without a device (restore validation tests) */
 SR_API int sr_host_initial_checkpoint(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n_chains, const char *path)
 {
-  if (!ds || !specs || n_chains <= 0 || !path || ds->nh > SR_NHMAX) return SR_EINVAL;
+  if (!ds || !specs || n_chains <= 0 || !path) return SR_EINVAL;
   sr_state_host st;
   int rc = state_alloc(&st, ds->N, ds->M, ds->nh, n_chains, 0);
   if (rc) return rc;
@@ -712,7 +712,7 @@ static int ck_validate(const sr_dataset *ds, const sr_state_host *st)
   const int N = ds->N, nh = ds->nh;
   for (int c = 0; c < st->nchains; c++) {
     if (check_chain(ds, st, c)) return SR_EPARSE;
-    const int32_t *hp = st->hp + (size_t)c * SR_NHMAX, *rpi = st->rpi + (size_t)c * N;
+    const int32_t *hp = st->hp + (size_t)c * SR_NHCAP(nh), *rpi = st->rpi + (size_t)c * N;
     for (int k = 0; k < nh; k++)
       if (hp[k] < 0 || hp[k] >= N || (k > 0 && hp[k] <= hp[k - 1]) || !ds->hard[rpi[hp[k]]]) return SR_EPARSE;
     const uint64_t pos = st->rng[(size_t)c * 2 + 0], gen = st->rng[(size_t)c * 2 + 1];

@@ -7,7 +7,10 @@
 #include <stdint.h>
 #include <stddef.h>
 
-#define SR_NHMAX 64      /* hard sites per dataset the kernel supports (a 64-bit mask per taxon; one per lane) */
+#define SR_NHMAX 64      /* hard sites of the mask paths (a 64-bit mask per taxon, one hard site per lane); more
+                            hard sites take the bitmap paths (any number up to N) */
+/* hard positions stored per chain: 64, or nh rounded up to whole waves */
+#define SR_NHCAP(nh) ((nh) <= SR_NHMAX ? SR_NHMAX : (((nh) + 63) & ~63))
 #define SR_RING 8        /* MT19937 blocks resident per chain */
 #define SR_MMAX (1 << 20)   /* taxa per dataset (int32 indices; per-chain columns and records grow with M) */
 

@@ -44,7 +44,7 @@ int srk_create(const sr_state_host *st, int device, int block_threads, int rec_c
   d->st = *st;
   d->st.P = (uint32_t *)dup(st->P, C * st->NW * st->M * 4);
   d->st.rpi = (int32_t *)dup(st->rpi, C * st->N * 4);
-  d->st.hp = (int32_t *)dup(st->hp, C * SR_NHMAX * 4);
+  d->st.hp = (int32_t *)dup(st->hp, C * SR_NHCAP(st->nh) * 4);
   d->st.ab = (int32_t *)dup(st->ab, C * 2 * st->M * 4);
   d->st.cnt = (int32_t *)dup(st->cnt, C * 4 * st->M * 4);
   d->st.cdl = (double *)dup(st->cdl, C * 4 * 8);
@@ -131,7 +131,7 @@ int srk_download_state(srk_dev *d, sr_state_host *st)
   const size_t C = (size_t)d->st.nchains;
   if (st->P) memcpy(st->P, d->st.P, C * d->st.NW * d->st.M * 4);
   if (st->rpi) memcpy(st->rpi, d->st.rpi, C * d->st.N * 4);
-  if (st->hp) memcpy(st->hp, d->st.hp, C * SR_NHMAX * 4);
+  if (st->hp) memcpy(st->hp, d->st.hp, C * SR_NHCAP(st->nh) * 4);
   if (st->ab) memcpy(st->ab, d->st.ab, C * 2 * d->st.M * 4);
   if (st->cnt) memcpy(st->cnt, d->st.cnt, C * 4 * d->st.M * 4);
   if (st->cdl) memcpy(st->cdl, d->st.cdl, C * 4 * 8);

@@ -165,11 +165,11 @@ def test_restore_validates_chain_state(tmp_path):
 
 
 def test_hard_site_limit_boundary():
-    """The kernel holds at most SR_NHMAX = 64 hard sites (a 64-bit mask per taxon, one hard site per
-    lane): 65 are refused with SR_EUNSUPPORTED before any device call (40 and 64 run bit-exact in
-    tests/test_gpu_edge.py 'nh40' / 'nh64').  Sites are limited to N <= 4095 (12-bit positions in the
-    packed proposal records): 4096 are refused the same way.  The reference has neither limit.  Taxa are
-    not limited by the records (they hold positions): M = 40000 is accepted."""
+    """Up to SR_NHMAX = 64 hard sites take the mask paths (a 64-bit mask per taxon, one hard site per lane),
+    more take the bitmap paths: 65 are accepted (40, 64, 65, 200 and N - 1 = 129 run bit-exact in
+    tests/test_gpu_edge.py).  Sites are limited to N <= 4095 (12-bit positions in the packed proposal
+    records): 4096 are refused with SR_EUNSUPPORTED before any device call.  Taxa are not limited by the
+    records (they hold positions): M = 40000 is accepted."""
     def text(nh, N=90, M=6):
         rows = ["%d %d" % (N, M)]
         for i in range(N):
@@ -177,19 +177,12 @@ def test_hard_site_limit_boundary():
         return ("\n".join(rows) + "\n").encode()
     ds65 = sa.Dataset.parse(text(65))
     assert ds65.nh == 65
-    with pytest.raises(sa.SrError) as e:
-        sa.Session(ds65, [1])
-    assert e.value.code == L.SR_EUNSUPPORTED
-    out = (L.sr_chain_summary * 1)()
-    devs = (ctypes.c_int32 * 1)(0)
-    assert sa.lib().sr_run_chains_multi(ctypes.byref(ds65.c), sa.core.make_specs([1]), 1, None, devs, 1,
-                                        ctypes.cast(None, L.SINK_FN), None, out) == L.SR_EUNSUPPORTED
     big = sa.Dataset.parse(text(3, N=4096, M=2), maxs=0)
     with pytest.raises(sa.SrError) as e:
         sa.Session(big, [1])
     assert e.value.code == L.SR_EUNSUPPORTED
     if not _gpu_present():   # (taxa beyond int16: M = 40000 runs, tests/test_gpu_edge.py::test_taxa_beyond_int16)
-        for ok in (sa.Dataset.parse(text(64)), sa.Dataset.parse(text(3, N=4095, M=2), maxs=0),
+        for ok in (sa.Dataset.parse(text(64)), ds65, sa.Dataset.parse(text(3, N=4095, M=2), maxs=0),
                    sa.Dataset.parse(text(3, N=8, M=40000), maxs=0)):
             with pytest.raises(sa.SrError) as e:
                 sa.Session(ok, [1])
@@ -206,3 +199,35 @@ def test_multi_device_arguments_rejected():
     assert lib.sr_run_chains_multi(ctypes.byref(ds.c), sa.core.make_specs([1, 2]), 2, None, devs, 3, none, None, out) == L.SR_EINVAL
     assert lib.sr_run_chains_multi(ctypes.byref(ds.c), sa.core.make_specs([1, 2]), 2, None, None, 1, none, None, out) == L.SR_EINVAL
     assert lib.sr_run_to_dirs_multi(ctypes.byref(ds.c), sa.core.make_specs([1, 2]), 2, None, devs, 0, b"/tmp", out) == L.SR_EINVAL
+
+
+def test_checkpoint_many_hard_sites(tmp_path):
+    """More than 64 hard sites: the state keeps nh hard positions per chain rounded up to whole waves (128 for
+    nh = 100); such a checkpoint validates (SR_EDEVICE without a GPU), a damaged hard position beyond the
+    first 64 is refused."""
+    import numpy as np
+    N, M, nh, C = 150, 8, 100, 2
+    rows = ["%d %d" % (N, M)] + [" ".join("1" if (i * 7 + m) % 5 == 0 else "0" for m in range(M)) + (" *" if i % 3 else "")
+                                 for i in range(N)]
+    ds = sa.Dataset.parse(("\n".join(rows) + "\n").encode())
+    assert ds.nh == nh
+    specs = sa.core.make_specs([3, 4])
+    good = tmp_path / "nh100.srck"
+    assert L.lib().sr_host_initial_checkpoint(ctypes.byref(ds.c), specs, C, os.fsencode(str(good))) == 0
+    opts = L.sr_run_opts()
+    L.lib().sr_default_opts(ctypes.byref(opts))
+    h = ctypes.c_void_p()
+    rc = L.lib().sr_session_restore(ctypes.byref(ds.c), os.fsencode(str(good)), ctypes.byref(opts), ctypes.byref(h))
+    if rc == 0:
+        L.lib().sr_session_destroy(h)
+    assert rc in (0, L.SR_EDEVICE)
+    NW = (N + 31) // 32
+    off = 32 + C * ctypes.sizeof(L.sr_chain_spec) + C * NW * M * 4 + C * N * 4
+    raw = bytearray(good.read_bytes())
+    assert len(raw) == off + C * 128 * 4 + C * 2 * M * 4 + C * 4 * M * 4 + C * 4 * 8 + C * 8 * 624 * 4 + C * 2 * 8 + C * 10 * 8
+    hp = np.frombuffer(bytes(raw), "<i4", C * 128, off).reshape(C, 128)
+    assert (np.diff(hp[0, :nh]) > 0).all() and (hp[:, nh:] == 0).all()
+    raw[off + 4 * 80: off + 4 * 81] = np.array([N + 9], "<i4").tobytes()
+    bad = tmp_path / "bad.srck"
+    bad.write_bytes(bytes(raw))
+    assert L.lib().sr_session_restore(ctypes.byref(ds.c), os.fsencode(str(bad)), ctypes.byref(opts), ctypes.byref(h)) == -2

@@ -42,6 +42,11 @@ CASES = [
     ("nh32", 90, 64, 32, 0),
     ("nh40", 120, 70, 40, 0),
     ("nh64", 150, 64, 64, 0),
+    # more than 64 hard sites: the bitmap paths (hard ones of a column from the wave's hard bitmap, hard
+    # positions in several waves of lanes)
+    ("nh65", 160, 70, 65, 0),
+    ("nh200", 300, 90, 200, 0),
+    ("nh-n-1-big", 130, 40, 129, 0),
     ("n2500", 2500, 24, 10, 0),
     # nh = N - 1 / N - 2: mcmc_randomize's hard-position scan reads q[nh] past the end there
     # (mcmc.c:530, UB); host and oracle both stop at nh (the intended reading)
@@ -72,8 +77,8 @@ def test_edge_parity(name, N, M, nh, tb):
 
 # The HBM-column variant (columns, prefix tables, a/b, counts in HBM; chosen automatically when
 # the LDS layout exceeds 160 KB) forced on small cases: same bits as the oracle.
-HBM_CASES = [c for c in CASES if c[0] in ("tiny", "many-hard", "nh64", "n2500", "walk17", "lds-walk", "tb256-2-per-thread",
-                                          "3-per-thread")]
+HBM_CASES = [c for c in CASES if c[0] in ("tiny", "many-hard", "nh64", "nh200", "n2500", "walk17", "lds-walk",
+                                          "tb256-2-per-thread", "3-per-thread")]
 
 
 @pytest.mark.parametrize("name,N,M,nh,tb", HBM_CASES, ids=["hbm-" + c[0] for c in HBM_CASES])

@@ -72,7 +72,7 @@ struct KArgs {
   unsigned long long *dbg;   /* SR_STAMPS builds: [chain][16] cycles per phase */
   uint16_t *gpre;            /* gm variant scratch, per chain: column prefix tables */
   uint32_t *pkey;            /* [chain][2] Philox keys (SR_F_RNG_PHILOX), else null: MT19937 */
-  float *gck;                    /* gm variant scratch: Gibbs checkpoints (f32: half the bytes of the scratch stream) */
+  void *gck;                     /* gm variant scratch: Gibbs checkpoints (SR_CK32: f32, half the bytes of the scratch stream) */
   double *glbuf, *gcbuf;         /* gm variant scratch: logl terms, exact-delta terms */
   int *xflag, *xbuf, *xerr;      /* split chains (SP kernels): [chain][2] progress flags, exchange slots, timeout flag */
   double *cdv, *cdx;   /* manycd (MCD kernels): [chain][2M] per-taxon c, d (state); [chain][2M] their cc, dd (scratch) */
@@ -82,6 +82,10 @@ struct KArgs {
 /* The launch arguments re-read from the kernarg segment (constant for the launch; the kernel's only
  * argument is KArgs, at offset 0): the record and state pointers used after the sweeps come from here, so
  * they are not held live (in spilled SGPRs) across the sweep loop.  SR_KARG_RELOAD=0: the by-value copy. */
+/* HBM-column kernels: Gibbs checkpoints stored as f32 (1) or f64 (0) in their HBM scratch (draw_fast) */
+#ifndef SR_CK32
+#define SR_CK32 1
+#endif
 #ifndef SR_KARG_RELOAD
 #define SR_KARG_RELOAD 0
 #endif
@@ -767,7 +771,8 @@ __device__ __forceinline__ double exp2_split(double q)
 template <bool B8>
 __device__ __forceinline__ int draw_fast(const uint32_t *Pm, const uint16_t *prem, int M, int N, int NW, bool rev, int o, int L,
                                          int POo, double u, const CD &K, const sr_mtab &tb, double vA, double vB, double rA, double rB,
-                                         const double *T4, const double *T8, typename std::conditional<B8, float, double>::type *ck,
+                                         const double *T4, const double *T8,
+                                         typename std::conditional<B8 && SR_CK32, float, double>::type *ck,
                                          int ckstride, uint64_t *fbk, int &dt0, int &df0,
                                          int &dt1, int &df1 GSTAMP_ARGS)
 {
@@ -920,7 +925,7 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, const uint16_t *pre
   if (S > 0.0 && S < 0x1p1000 && !uf) {
     const double inv = 1.0 / S;
     const double REL = (double)(N + 33) * 0x1p-50;
-    const double ABS = (double)(N + 1) * 0x1p-39 + 0x1p-46 + (B8 ? 0x1p-21 : 0.0);
+    const double ABS = (double)(N + 1) * 0x1p-39 + 0x1p-46 + ((B8 && SR_CK32) ? 0x1p-21 : 0.0);
     int j = klo;   /* first window word whose checkpoint reaches u (checkpoints ascend) */
     for (int k0 = klo; k0 < khi; k0 += SR_WCH) {
       double cv[SR_WCH];
@@ -1911,8 +1916,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   int16_t *hcnt = (int16_t *)(smem + L.ht) + wave * (2 * N + 2);    /* this wave's hard-site tables */
   int16_t *nhall = hcnt + N + 1;
   const int CKS = SP ? 2 * TB : sr_ckstride(M, TB);   /* SP: slots [half TB + tid] */
-  using CKT = typename std::conditional<GM, float, double>::type;   /* Gibbs checkpoints: f32 in HBM scratch, f64 in LDS */
-  CKT *ckb = GM ? (CKT *)(void *)(A.gck + (size_t)chain * (SP ? sr_sp_ck(N, TB) : sr_gm_ck(N, M, TB))) : (CKT *)(void *)(smem + L.ck);
+  using CKT = typename std::conditional<GM && SR_CK32, float, double>::type;   /* Gibbs checkpoints: f32 in HBM scratch, f64 in LDS */
+  CKT *ckb = GM ? (CKT *)A.gck + (size_t)chain * (SP ? sr_sp_ck(N, TB) : sr_gm_ck(N, M, TB)) : (CKT *)(void *)(smem + L.ck);
   const int ckslot = SP ? half * TB + tid : tid;   /* this thread's Gibbs checkpoint slots */
   int *ccnt = (int *)(smem + L.ccnt);
   int32_t *sab = GM ? A.ab + (size_t)chain * 2 * M : (int32_t *)(smem + L.sab);     /* a[M], b[M] */
@@ -3337,7 +3342,10 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
   if (pkey) rc |= dev_alloc_copy(d, &A.pkey, pkey, C * 2);
   if (d->gm) {
     rc |= dev_alloc_copy(d, &A.gpre, (const uint16_t *)nullptr, C * sr_gm_pre(st->M, st->NW));
-    rc |= dev_alloc_copy(d, &A.gck, (const float *)nullptr, C * (d->sp ? sr_sp_ck(st->N, TB) : sr_gm_ck(st->N, st->M, TB)));
+    using CKT = typename std::conditional<SR_CK32 != 0, float, double>::type;
+    CKT *gck = nullptr;
+    rc |= dev_alloc_copy(d, &gck, (const CKT *)nullptr, C * (d->sp ? sr_sp_ck(st->N, TB) : sr_gm_ck(st->N, st->M, TB)));
+    A.gck = gck;
     rc |= dev_alloc_copy(d, &A.glbuf, (const double *)nullptr, C * st->M);
     rc |= dev_alloc_copy(d, &A.gcbuf, (const double *)nullptr, C * sr_gm_cbuf(st->M));
   }

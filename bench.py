@@ -307,17 +307,6 @@ def main():
     assert len(gathered) == C * world and np.isfinite(gathered).all() and selected
     assert sel_ab.shape[0] == len(selected) and (sel_ab[:, :, 2 * ds.M:] >= 0).all()
 
-    # parity leg (after the timed region, rank 0): the CPU oracle reruns some selected chains and every saved
-    # record of the timed region must match bit for bit (tests/bench_parity.py; the checker, not measured)
-    parity = None
-    if rank == 0 and args.parity_chains > 0 and not args.no_save and args.rng == "mt":
-        import bench_parity
-        with open(args.dataset, "rb") as fh:
-            text = fh.read()
-        k = min(args.parity_chains, len(selected))
-        parity = bench_parity.check_selected(text, selected[:k], [c + 1 for c in selected[:k]], args.warmup * cps,
-                                             sel_ab[:k], sel_cdl[:k], calls=args.parity_calls or None)
-
     total_chains = C * world
     sweeps_per_step = cps * 10
     iters = total_chains * sweeps_per_step * args.steps
@@ -395,13 +384,23 @@ def main():
                                                        np.ascontiguousarray(sel_cdl).tobytes()).hexdigest(),
                       "note": "script.py:70-152 over every timed step's saved samples of the selected chains (the "
                               "reference divides by 1000: exact means at --steps 20 x 50 calls = 1000 samples)"},
-        "parity": parity,
     }
+    sess.close()
+    if dist:   # (the ranks leave together; rank 0's CPU parity leg below runs after the process group is gone)
+        dist.destroy_process_group()
+    # parity leg (after the timed region, rank 0): the CPU oracle reruns some selected chains and every saved
+    # record of the timed region must match bit for bit (tests/bench_parity.py; the checker, not measured)
+    parity = None
+    if rank == 0 and args.parity_chains > 0 and not args.no_save and args.rng == "mt":
+        import bench_parity
+        with open(args.dataset, "rb") as fh:
+            text = fh.read()
+        k = min(args.parity_chains, len(selected))
+        parity = bench_parity.check_selected(text, selected[:k], [c + 1 for c in selected[:k]], args.warmup * cps,
+                                             sel_ab[:k], sel_cdl[:k], calls=args.parity_calls or None)
+    out["parity"] = parity
     if rank == 0:
         print(json.dumps(out), flush=True)
-    sess.close()
-    if dist:
-        dist.destroy_process_group()
     if parity is not None and not parity["match"]:
         raise SystemExit("bench.py: the timed records differ from the CPU oracle: %s" % parity["mismatch"])
 

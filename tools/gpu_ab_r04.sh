@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-4 same-box A/Bs: config 3 (256 x 512, the bench) default vs the kernarg-reload variant; config 5
-# (1024 x 2048, split chains) default (f32 Gibbs checkpoints) vs the f64-checkpoint source.  Variants are
+# (1024 x 2048, split chains) default (f32 Gibbs checkpoints per word) vs f64 checkpoints (ck64) and f32
+# checkpoints per word pair (ckg2).  Variants are
 # built here by tools/build_variant.sh (self-contained: own snapshot and spec defines).
 #   tools/gpu_ab_r04.sh OUT
 set -o pipefail
@@ -8,7 +9,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 OUT=${1:-r04ab}
 NOPARITY=1 bash tools/gpu_ab.sh ${OUT}_karg karg &&
-NOPARITY=1 BENCH_ARGS="--sites 1024 --taxa 2048 --calls-per-step 2 --block-threads 1024" bash tools/gpu_ab.sh ${OUT}_ck64 ck64
+NOPARITY=1 BENCH_ARGS="--sites 1024 --taxa 2048 --calls-per-step 2 --block-threads 1024" bash tools/gpu_ab.sh ${OUT}_c5 ck64 ckg2
 rc=$?
 echo "exit $rc"
 exit $rc

@@ -175,6 +175,7 @@ const char *sr_spec_reason(int code)
     case SR_SPEC_ECC: return "the compile failed";
     case SR_SPEC_EPROF: return "a profiler tool library is preloaded and the code object is not cached";
     case SR_SPEC_ELOAD: return "the code object did not load or does not match this library";
+    case SR_SPEC_ECACHE: return "the cache directory cannot be created or written ($SR_JIT_CACHE / build/jit)";
     default: return "unknown";
   }
 }
@@ -256,8 +257,10 @@ int sr_spec_object(const sr_spec_shape *s, char *path, size_t len)
   if (access(cc, X_OK) != 0) return SR_SPEC_ENOCC;
   char dir[4200], tmp[4500], log[4500], inc[4300], src[4300], arch[64], defs[1024], fl[1280];
   snprintf(dir, sizeof dir, "%s", path);
-  *strrchr(dir, '/') = 0;
+  char *sl = strrchr(dir, '/');
+  if (sl) *sl = 0;
   mkdirs(dir);
+  if (access(dir, W_OK) != 0) return SR_SPEC_ECACHE;
   /* a per-compile temporary name: shard threads and processes may compile the same shape together;
      rename() publishes the finished object atomically */
   static int seq;

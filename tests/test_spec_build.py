@@ -137,3 +137,11 @@ def test_hbm_sessions_have_no_specialised_kernel(tmp_path):
     from test_gpu_edge import make_text
     ds = sa.Dataset.parse(make_text(64, 1100, 6, seed=64 * 1000 + 1100), maxs=0)
     assert sa.specialize(ds, columns="hbm") is False
+
+
+def test_unwritable_cache_is_reported(tmp_path):
+    """A cache directory that cannot be created (under a regular file): SR_EIO and a line naming the cache."""
+    blocker = tmp_path / "file"
+    blocker.write_text("x")
+    out, err = child({"SR_JIT_CACHE": str(blocker / "cache")})
+    assert out["rc"] == -7 and "cache directory" in err

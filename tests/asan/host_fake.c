@@ -3,7 +3,7 @@
  * device (srk_fake.c: sweeps leave the state unchanged; SR_FAKE_DAMAGE="chain:call" corrupts a count)
  * under ASan + UBSan.  Checks that a chain failing mcmc_consistent after some call is reported in
  * its summary and by SR_EINCONSISTENT -- single device, two shards, the session API -- and that no
- * path crashes on it.   usage: host_fake DATASET TMPDIR   (exit 0 = every check held) */
+ * path crashes on it; and manycd = 1 through the same paths (records, writers, checkpoint v4).   usage: host_fake DATASET TMPDIR   (exit 0 = every check held) */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -97,6 +97,41 @@ int main(int argc, char **argv)
   memset(out, 0, sizeof out);
   CHECK(sr_run_chains(&ds, specs, 4, &o, NULL, NULL, out) == SR_EINCONSISTENT);
   for (int c = 0; c < 4; c++) CHECK((out[c].consistent != 0) == (c == 3));
+
+  /* 7. manycd = 1 through the writers, the debug check, a checkpoint (v4) and its restore: every taxon's
+        c, d travels with the records (the fake device keeps them unchanged: log .01 / log .3) */
+  unsetenv("SR_FAKE_DAMAGE");
+  o.flags = SR_F_DEBUG_CHECK;
+  o.manycd = 1;
+  o.calls_per_launch = 2;
+  memset(out, 0, sizeof out);
+  char root[4096];
+  snprintf(root, sizeof root, "%s/manycd", argv[2]);
+  mkdir(root, 0777);
+  CHECK(sr_run_to_dirs_multi(&ds, specs, 4, &o, devs, 2, root, out) == SR_OK);
+  for (int c = 0; c < 4; c++) CHECK(out[c].consistent == 0);
+  snprintf(path, sizeof path, "%s/Chains/chain_02/chain_data.csv", root);
+  size_t clen = 0;
+  char *cd = slurp(path, &clen);
+  CHECK(cd && strstr(cd, "0.01000000000000 ") && strstr(cd, "0.30000000000000 "));
+  free(cd);
+  o.flags = 0;
+  CHECK(sr_run_chains(&ds, specs, 4, &o, NULL, NULL, out) == SR_OK);
+  o.calls_per_launch = 8;
+  CHECK(sr_session_create(&ds, specs, 4, &o, &s) == SR_OK && sr_session_manycd(s) == 1);
+  CHECK(sr_session_run(s, 2, 1) == SR_OK);
+  double *cv = (double *)malloc(sizeof(double) * 4 * 2 * 2 * ds.M);
+  CHECK(cv && sr_session_fetch_cd_vectors(s, 0, 2, cv) == SR_OK);
+  CHECK(cv[0] < -4.6 && cv[0] > -4.61 && cv[ds.M] < -1.2 && cv[ds.M] > -1.21);   /* log .01, log .3 */
+  free(cv);
+  snprintf(path, sizeof path, "%s/m.ck", argv[2]);
+  CHECK(sr_session_checkpoint(s, path) == SR_OK);
+  sr_session_destroy(s);
+  s = NULL;
+  CHECK(sr_session_restore(&ds, path, &o, &s) == SR_OK && sr_session_manycd(s) == 1);
+  sr_session_destroy(s);
+  o.manycd = 0;
+  CHECK(sr_session_restore(&ds, path, &o, &s) == SR_EINVAL);   /* a manycd checkpoint, opts say 0 */
 
   sr_free_dataset(&ds);
   printf("host_fake: ok\n");

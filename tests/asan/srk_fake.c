@@ -4,7 +4,8 @@
  *
  * It does NOT sample: a "sweep" leaves the uploaded chain state unchanged (so every chain stays
  * exactly as consistent as mcmc_randomize left it), records are the current state, and two
- * "devices" are reported.  Fault injection: SR_FAKE_DAMAGE="chain:call" adds 1 to chain's t0 of
+ * "devices" are reported; manycd sessions keep their per-taxon c, d (unchanged, recorded per call).
+ * Fault injection: SR_FAKE_DAMAGE="chain:call" adds 1 to chain's t0 of
  * taxon 0 when that chain's session has completed `call` mcmc_sample calls (a count that no longer
  * matches count01: mcmc_consistent must flag it).  Never linked by the product. */
 #include <stdio.h>
@@ -18,6 +19,7 @@ struct srk_dev {
   int rec_cap;
   int16_t *rec;
   double *rcd;
+  double *rcv;   /* manycd: [chain][rec_cap][2M] */
   long calls;
   int dmg_chain;
   long dmg_call;
@@ -36,7 +38,6 @@ int srk_create(const sr_state_host *st, int device, int block_threads, int rec_c
                const uint32_t *pkey, int spec, srk_dev **out)
 {
   (void)block_threads; (void)gm_force; (void)pkey; (void)spec;
-  if (st->manycd) return -6;   /* (the fake device keeps no per-taxon c, d) */
   if (device < 0 || device >= 2) return -5;
   srk_dev *d = (srk_dev *)calloc(1, sizeof(*d));
   if (!d) return -5;
@@ -51,9 +52,11 @@ int srk_create(const sr_state_host *st, int device, int block_threads, int rec_c
   d->st.mt = (uint32_t *)dup(st->mt, C * SR_RING * 624 * 4);
   d->st.rng = (uint64_t *)dup(st->rng, C * 2 * 8);
   d->st.acc = (uint64_t *)dup(st->acc, C * SR_NACC * 8);
+  d->st.cdv = st->manycd ? (double *)dup(st->cdv, C * 2 * st->M * 8) : NULL;
   d->rec_cap = rec_cap_calls > 0 ? rec_cap_calls : 1;
   d->rec = (int16_t *)calloc(C * d->rec_cap * (2 * (size_t)st->M + st->N), 2);
   d->rcd = (double *)calloc(C * d->rec_cap * 3, 8);
+  d->rcv = st->manycd ? (double *)calloc(C * d->rec_cap * 2 * st->M, 8) : NULL;
   d->dmg_chain = -1;
   const char *e = getenv("SR_FAKE_DAMAGE");
   if (e) sscanf(e, "%d:%ld", &d->dmg_chain, &d->dmg_call);
@@ -70,6 +73,8 @@ static void put_record(srk_dev *d, int c, int slot)
   for (int k = 0; k < 2 * M; k++) r[k] = (int16_t)d->st.ab[(size_t)c * 2 * M + k];
   for (int p = 0; p < N; p++) r[2 * M + d->st.rpi[(size_t)c * N + p]] = (int16_t)p;
   memcpy(d->rcd + ((size_t)c * d->rec_cap + slot) * 3, d->st.cdl + (size_t)c * 4, 3 * 8);
+  if (d->rcv)
+    memcpy(d->rcv + ((size_t)c * d->rec_cap + slot) * 2 * M, d->st.cdv + (size_t)c * 2 * M, (size_t)2 * M * 8);
 }
 
 int srk_run(srk_dev *d, int calls, int spc, int save, int rec_base)
@@ -138,6 +143,7 @@ int srk_download_state(srk_dev *d, sr_state_host *st)
   if (st->mt) memcpy(st->mt, d->st.mt, C * SR_RING * 624 * 4);
   if (st->rng) memcpy(st->rng, d->st.rng, C * 2 * 8);
   if (st->acc) memcpy(st->acc, d->st.acc, C * SR_NACC * 8);
+  if (st->cdv && d->st.cdv) memcpy(st->cdv, d->st.cdv, C * 2 * d->st.M * 8);
   return 0;
 }
 
@@ -148,15 +154,17 @@ int srk_run_pipelined(srk_dev *d, int total, int cpl, int spc, int (*consume)(vo
   const size_t W = 2 * (size_t)d->st.M + d->st.N, C = (size_t)d->st.nchains;
   int16_t *ab = (int16_t *)malloc(C * cpl * W * 2);
   double *cd = (double *)malloc(C * cpl * 24);
-  int rc = (ab && cd) ? 0 : -5;
+  double *cv = d->rcv ? (double *)malloc(C * cpl * 2 * d->st.M * 8) : NULL;
+  int rc = (ab && cd && (cv || !d->rcv)) ? 0 : -5;
   for (int done = 0; !rc && done < total;) {
     const int k = total - done < cpl ? total - done : cpl;
     rc = srk_run(d, k, spc, 1, 0);
     if (!rc) rc = srk_fetch_records(d, 0, k, ab, cd);
-    if (!rc && consume(ctx, done, k, ab, cd, NULL)) rc = -1;
+    if (!rc && cv) rc = srk_fetch_cdv(d, 0, k, cv);
+    if (!rc && consume(ctx, done, k, ab, cd, cv)) rc = -1;
     done += k;
   }
-  free(ab); free(cd);
+  free(ab); free(cd); free(cv);
   return rc;
 }
 
@@ -184,9 +192,15 @@ void srk_destroy(srk_dev *d)
 {
   if (!d) return;
   free(d->st.P); free(d->st.rpi); free(d->st.hp); free(d->st.ab); free(d->st.cnt);
-  free(d->st.cdl); free(d->st.mt); free(d->st.rng); free(d->st.acc);
-  free(d->rec); free(d->rcd);
+  free(d->st.cdl); free(d->st.mt); free(d->st.rng); free(d->st.acc); free(d->st.cdv);
+  free(d->rec); free(d->rcd); free(d->rcv);
   free(d);
 }
-/* manycd sessions are refused by the fake device (srk_create), so this is never reached */
-int srk_fetch_cdv(srk_dev *d, int f, int c, double *v) { (void)d; (void)f; (void)c; (void)v; return -1; }
+int srk_fetch_cdv(srk_dev *d, int first, int count, double *cdv)
+{
+  if (!d->rcv || first < 0 || count < 0 || first + count > d->rec_cap) return -1;
+  const size_t R2 = 2 * (size_t)d->st.M;
+  for (int c = 0; c < d->st.nchains; c++)
+    memcpy(cdv + (size_t)c * count * R2, d->rcv + ((size_t)c * d->rec_cap + first) * R2, (size_t)count * R2 * 8);
+  return 0;
+}

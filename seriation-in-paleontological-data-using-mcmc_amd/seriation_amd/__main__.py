@@ -6,7 +6,7 @@ whole job at once and writes the same ``Chains/chain_NN`` tree:
 
     python -m seriation_amd DATASET [--chains 100] [--burnin 1000] [--samples 1000] [--thin 10]
                                     [--seed-base S] [--devices 0,1] [--root .] [--select K]
-                                    [--no-save] [--debug-check] [--rng mt|philox]
+                                    [--no-save] [--debug-check] [--rng mt|philox] [--manycd]
 
   --thin        sweeps per saved sample (the reference's mcmc_sample runs 10, mcmc.c:225)
   --seed-base   chain k gets seed S + k; omitted -> unique 1-byte urandom seeds like
@@ -18,6 +18,7 @@ whole job at once and writes the same ``Chains/chain_NN`` tree:
                 Philox4x32-10 stream for sampling (statistically equivalent, not bit-equal)
   --debug-check mcmc_consistent on every chain after every mcmc_sample call (the reference's
                 MCMCDEBUG build, mcmc.c:249-255); with --no-save
+  --manycd      per-taxon c, d (mcmc_readmodel's manycd = 1, mcmc.c:777-786, 807-816)
 
 Prints the wall time (seconds, 2 decimals) as script.py:67 does.  Exit status 1 when a chain
 fails its closing consistency check (mcmc.c:199-204).
@@ -44,6 +45,7 @@ def main(argv=None):
     ap.add_argument("--no-save", action="store_true")
     ap.add_argument("--debug-check", action="store_true")
     ap.add_argument("--rng", default="mt", choices=("mt", "philox"))
+    ap.add_argument("--manycd", action="store_true")
     a = ap.parse_args(argv)
     if a.chains < 1 or a.burnin < 0 or a.samples < 0 or a.thin < 1:
         ap.error("--chains and --thin must be >= 1, --burnin and --samples >= 0")
@@ -62,7 +64,7 @@ def main(argv=None):
         t0 = time.perf_counter()
         summ, _ = core.run_chains(ds, seeds, burnin_calls=a.burnin, sample_calls=a.samples,
                                   sweeps_per_call=a.thin, devices=devices[:len(seeds)], debug_check=a.debug_check,
-                                  rng=a.rng)
+                                  rng=a.rng, manycd=int(a.manycd))
         wall = time.perf_counter() - t0
         for s in summ:
             print(json.dumps(s))
@@ -70,7 +72,7 @@ def main(argv=None):
     else:
         summ = launcher.run_all_chains(a.dataset, n_chains=a.chains, seeds=seeds, devices=devices,
                                        burnin_calls=a.burnin, sample_calls=a.samples, root=a.root,
-                                       sweeps_per_call=a.thin, rng=a.rng)
+                                       sweeps_per_call=a.thin, rng=a.rng, manycd=int(a.manycd))
         if a.select:
             print("selected:", " ".join(str(k) for k in launcher.choose_chains(a.select, a.root)))
     return 1 if any(s.get("consistent", 0) for s in summ) else 0

@@ -42,13 +42,14 @@ def run_chain(chain_index, old_seeds, dataset, burnin_calls=1000, sample_calls=1
 
 
 def run_all_chains(dataset, n_chains=100, seeds=None, devices=None, burnin_calls=1000, sample_calls=1000,
-                   root=".", verbose=True, sweeps_per_call=10, rng="mt"):
+                   root=".", verbose=True, sweeps_per_call=10, rng="mt", manycd=0):
     """script.py:48-67: run all chains and print the wall time (seconds, 2 decimals).
 
     seeds: None -> unique 1-byte urandom seeds exactly like the reference (only 256 exist, so
     n_chains <= 256); otherwise an explicit list (deterministic runs).
     devices: list of GPU ordinals to shard over (default: [0]); the sharding is done by the C
-    library (sr_run_to_dirs_multi: one host thread and session per device)."""
+    library (sr_run_to_dirs_multi: one host thread and session per device).
+    manycd: 1 = per-taxon c, d (mcmc_readmodel's flag, mcmc.c:777-786, 807-816)."""
     if seeds is None:
         old = []
         seeds = [_unique_seed(old) for _ in range(n_chains)]
@@ -59,7 +60,8 @@ def run_all_chains(dataset, n_chains=100, seeds=None, devices=None, burnin_calls
     start = time.perf_counter()
     devices = devices[:len(seeds)]
     summ = core.run_to_dirs(ds, seeds, root=root, chain_ids=list(range(len(seeds))), burnin_calls=burnin_calls,
-                            sample_calls=sample_calls, sweeps_per_call=sweeps_per_call, devices=devices, rng=rng)
+                            sample_calls=sample_calls, sweeps_per_call=sweeps_per_call, devices=devices, rng=rng,
+                            manycd=manycd)
     finish = time.perf_counter()
     if verbose:
         print(round(finish - start, 2))

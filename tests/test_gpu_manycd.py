@@ -93,3 +93,30 @@ def test_manycd_debug_check_every_call():
     np.testing.assert_array_equal(ri[0], o["rec_int"])
     assert np.array_equal(rv[0].view(np.uint64), o["rec_cdv"].view(np.uint64))
     assert summ[0]["consistent"] == 0
+
+
+def test_manycd_batched_cli_matches_oracle(tmp_path):
+    """python -m seriation_amd --manycd: the Chains tree of 3 chains, chain_data.csv lines with every taxon's
+    own c and d, each equal to the oracle's records formatted as mcmc_save_chain does (mcmc.c:69-92)."""
+    import math
+    import subprocess
+    import sys
+    pkg = os.path.join(os.path.dirname(HERE), "seriation-in-paleontological-data-using-mcmc_amd")
+    ds_path = os.path.join(DS, "g5s5.txt")
+    r = subprocess.run([sys.executable, "-m", "seriation_amd", ds_path, "--chains", "3", "--burnin", "2", "--samples", "3",
+                        "--seed-base", "21", "--root", str(tmp_path), "--manycd"], cwd=pkg, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    text = _text("g5s5.txt")
+    ds = sa.Dataset.parse(text)
+    M = ds.M
+    for k in range(3):
+        o = oracle_ref.run_chain(text, 21 + k, 2, 3, manycd=1)
+        with open(os.path.join(str(tmp_path), "Chains", "chain_%02d" % k, "chain_data.csv")) as fh:
+            lines = fh.read().splitlines()
+        assert len(lines) == 3
+        for t, ln in enumerate(lines):
+            f = ln.split(",")
+            assert f[3].split() == ["%.14f" % math.exp(v) for v in o["rec_cdv"][t][:M]]
+            assert f[4].split() == ["%.14f" % math.exp(v) for v in o["rec_cdv"][t][M:]]
+            assert f[5] == "%.14f" % o["rec_dbl"][t][2]

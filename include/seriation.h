@@ -159,6 +159,9 @@ int sr_session_summaries(sr_session *s, int32_t first, int32_t count, sr_chain_s
 /* Current state of one chain (any pointer may be NULL); counts = t0,f0,t1,f1 (4*M). */
 int sr_session_state(sr_session *s, int32_t chain, int32_t *a, int32_t *b, int32_t *pi,
                      double *c_d_loglik, int32_t *counts);
+/* manycd sessions: one chain's current per-taxon c[M], d[M] (log values; either may be NULL); SR_EINVAL for
+   manycd = 0 sessions (their c, d are sr_session_state's). */
+int sr_session_state_cd(sr_session *s, int32_t chain, double *c, double *d);
 /* Acceptance counters cc, cd, cab, cpi1, cpi20, cpi21, cpi3 (mcmc.c:220). */
 int sr_session_accept_counts(sr_session *s, int32_t chain, int64_t *acc7);
 /* How often the fast paths fell back to the reference's own computation (no counterpart in

@@ -786,6 +786,19 @@ SR_API int sr_session_state(sr_session *s, int32_t chain, int32_t *a, int32_t *b
   return SR_OK;
 }
 
+SR_API int sr_session_state_cd(sr_session *s, int32_t chain, double *c, double *d)
+{
+  if (!s || chain < 0 || chain >= s->nchains || !s->opts.manycd) return SR_EINVAL;
+  sr_state_host st;
+  int rc = download(s, &st);
+  if (rc) return rc;
+  const int M = s->ds.M;
+  if (c) memcpy(c, st.cdv + (size_t)chain * 2 * M, (size_t)M * 8);
+  if (d) memcpy(d, st.cdv + (size_t)chain * 2 * M + M, (size_t)M * 8);
+  state_free(&st);
+  return SR_OK;
+}
+
 SR_API int sr_session_accept_counts(sr_session *s, int32_t chain, int64_t *acc7)
 {
   if (!s || chain < 0 || chain >= s->nchains || !acc7) return SR_EINVAL;

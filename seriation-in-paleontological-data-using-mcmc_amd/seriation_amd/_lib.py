@@ -83,7 +83,7 @@ PUBLIC_SYMBOLS = [
     "sr_run_chains", "sr_run_to_dirs", "sr_run_chains_multi", "sr_run_to_dirs_multi", "sr_session_create", "sr_session_set_stream",
     "sr_session_run", "sr_session_sync", "sr_session_records", "sr_session_record_capacity",
     "sr_session_fetch_records", "sr_session_reset_records", "sr_session_fetch_chain_records", "sr_session_summaries",
-    "sr_session_fetch_cd_vectors", "sr_session_manycd",
+    "sr_session_fetch_cd_vectors", "sr_session_manycd", "sr_session_state_cd",
     "sr_session_state",
     "sr_session_accept_counts", "sr_session_fallback_counts", "sr_session_debug_flagged", "sr_session_last_kernel_ms", "sr_session_block_threads", "sr_session_variant", "sr_session_specialized",
     "sr_session_checkpoint", "sr_session_restore",
@@ -129,6 +129,7 @@ def _lib():
         "sr_session_summaries": (c_int, [c_void_p, c_i32, c_i32, P(sr_chain_summary)]),
         "sr_session_fetch_cd_vectors": (c_int, [c_void_p, c_i32, c_i32, P(c_double)]),
         "sr_session_manycd": (c_i32, [c_void_p]),
+        "sr_session_state_cd": (c_int, [c_void_p, c_i32, P(c_double), P(c_double)]),
         "sr_session_state": (c_int, [c_void_p, c_i32, P(c_i32), P(c_i32), P(c_i32), P(c_double), P(c_i32)]),
         "sr_session_accept_counts": (c_int, [c_void_p, c_i32, P(ctypes.c_int64)]),
         "sr_session_fallback_counts": (c_int, [c_void_p, c_i32, P(ctypes.c_int64)]),

@@ -280,7 +280,13 @@ class Session:
                                         b.ctypes.data_as(P(ctypes.c_int32)), pi.ctypes.data_as(P(ctypes.c_int32)),
                                         cdl.ctypes.data_as(P(ctypes.c_double)), cnt.ctypes.data_as(P(ctypes.c_int32))),
                "state")
-        return {"a": a, "b": b, "pi": pi, "c": cdl[0], "d": cdl[1], "loglik": cdl[2], "counts": cnt.reshape(4, M)}
+        out = {"a": a, "b": b, "pi": pi, "c": cdl[0], "d": cdl[1], "loglik": cdl[2], "counts": cnt.reshape(4, M)}
+        if self.manycd:   # every taxon's own c, d
+            cv, dv = np.zeros(M), np.zeros(M)
+            _check(L.lib().sr_session_state_cd(self.h, chain, cv.ctypes.data_as(P(ctypes.c_double)),
+                                               dv.ctypes.data_as(P(ctypes.c_double))), "state_cd")
+            out["cv"], out["dv"] = cv, dv
+        return out
 
     def accept_counts(self, chain):
         acc = np.zeros(7, np.int64)

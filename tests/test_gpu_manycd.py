@@ -75,6 +75,10 @@ def test_manycd_session_records_and_checkpoint(tmp_path):
     rv2 = r.fetch_cd_vectors()
     r.close()
     np.testing.assert_array_equal(ri2, ri[:, 3:])
+    with sa.Session.restore(ds, ck, calls_per_launch=6, manycd=1) as r3:   # the state API: every taxon's c, d
+        st = r3.state(1)
+        assert np.array_equal(st["cv"].view(np.uint64), rv[1, 2, :ds.M].view(np.uint64))
+        assert np.array_equal(st["dv"].view(np.uint64), rv[1, 2, ds.M:].view(np.uint64))
     assert np.array_equal(rv2.view(np.uint64), rv[:, 3:].view(np.uint64))
     for k, sd in enumerate(seeds):
         o = oracle_ref.run_chain(text, sd, 0, 6, manycd=1)

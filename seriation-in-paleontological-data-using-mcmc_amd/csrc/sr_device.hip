@@ -3270,6 +3270,7 @@ static int srk_spec_load(srk_dev *d)
            hipMemcpyDtoH(abi, ga, sizeof abi) != hipSuccess) what = "no ABI record";
   else if (memcmp(abi, want, sizeof abi) != 0) what = "ABI record differs";
   if (what) {
+    (void)hipGetLastError();   /* the failed module call's error must not surface at the first generic launch */
     snprintf(log, sizeof log, "%s (%s)", path, what);
     sr_spec_note(SR_SPEC_ELOAD, log);
     if (d->mod) (void)hipModuleUnload(d->mod);

@@ -82,9 +82,13 @@ struct KArgs {
 /* The launch arguments re-read from the kernarg segment (constant for the launch; the kernel's only
  * argument is KArgs, at offset 0): the record and state pointers used after the sweeps come from here, so
  * they are not held live (in spilled SGPRs) across the sweep loop.  SR_KARG_RELOAD=0: the by-value copy. */
-/* HBM-column kernels: Gibbs checkpoints stored as f32 (1) or f64 (0) in their HBM scratch (draw_fast) */
+/* HBM-column kernels: Gibbs checkpoints stored as f32 (1) or f64 (0) in their HBM scratch (draw_fast).
+   f32 halves the scratch stream but is rejected (r04c/r04d, same box): the certification's absolute slack
+   must then grow to 2^-21 S, and an entry with less mass than twice the slack can never be certified, so
+   u landing in the window's many small-mass entries sends ~1.3e-4 of the draws to the exact walk (0.52
+   per chain-sweep against 0.0025 in f64): config 5 ran 2.3x slower (10.45 vs 4.56 ms per launch). */
 #ifndef SR_CK32
-#define SR_CK32 1
+#define SR_CK32 0
 #endif
 /* HBM-column kernels: window words per stored Gibbs checkpoint (1, or 2: half the checkpoint stream again;
    pass 2 then splits the chosen pair from the words' own sums) */
@@ -921,11 +925,11 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, const uint16_t *pre
      sum by at most ~9 2^-53 S (the subtraction and the word's fma roundings in pass 1): the extra
      absolute slack 2^-46 in u covers it; the unscaled sums' own rounding (and, with the byte tables in
      pass 1, the relative difference of the two table forms, <= 2 x 16 ulp) is inside REL's + 32.
-     B8 (HBM columns): the checkpoints are stored as f32 (half the scratch stream that spills L2): each is
-     within 2^-24 S of its f64 value, so the word search may land one word off (then the word's first or
-     last entry fails its certification and the exact walk runs) and a reconstructed partial sum moves by
-     at most 3 2^-24 S (Sp0, Sj and y = (Sj - Sp0) / sum): the absolute slack grows by 2^-21, which a
-     uniform u hits with probability ~2^-20 per draw.
+     B8 with SR_CK32 (HBM columns, not the default): the checkpoints are stored as f32: each is within
+     2^-24 S of its f64 value, so the word search may land one word off (then the word's first or last
+     entry fails its certification and the exact walk runs) and a reconstructed partial sum moves by at
+     most 3 2^-24 S (Sp0, Sj and y = (Sj - Sp0) / sum): the absolute slack grows by 2^-21 -- and every
+     entry with less mass than that slack fails certification, which measured 200x more exact walks.
      Ones before the word from the column prefix table. */
   int res = -1, POp = 0;
   if (S > 0.0 && S < 0x1p1000 && !uf) {

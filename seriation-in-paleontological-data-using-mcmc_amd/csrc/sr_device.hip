@@ -93,7 +93,7 @@ struct KArgs {
 /* HBM-column kernels: window words per stored Gibbs checkpoint (1, or 2: half the checkpoint stream again;
    pass 2 then splits the chosen pair from the words' own sums) */
 #ifndef SR_CKG
-#define SR_CKG 1
+#define SR_CKG 2
 #endif
 #ifndef SR_KARG_RELOAD
 #define SR_KARG_RELOAD 0
@@ -912,8 +912,8 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, const uint16_t *pre
               y = y * t4.y;
             }
           }
-          if (!B8 || SR_CKG == 1 || ((k - klo) & 1) == 1)
-            ck[(B8 && SR_CKG == 2 ? (k - klo) >> 1 : k) * ckstride] = S;   /* (B8: rounded to f32; pass 2 covers it by ABS) */
+          if (!B8 || SR_CKG == 1 || (k - klo) % SR_CKG == SR_CKG - 1)
+            ck[(B8 && SR_CKG > 1 ? (k - klo) / SR_CKG : k) * ckstride] = S;   /* (B8: one per SR_CKG window words) */
         }
       }
     }
@@ -938,51 +938,66 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, const uint16_t *pre
     const double ABS = (double)(N + 1) * 0x1p-39 + 0x1p-46 + ((B8 && SR_CK32) ? 0x1p-21 : 0.0);
     int j = klo;   /* first window word whose checkpoint reaches u (checkpoints ascend) */
     double Sp0, yj;   /* the partial sum before word j, y at its start */
-    if (B8 && SR_CKG == 2) {
-      /* checkpoints after every second window word: the pair holding u, then the word from the pair's own
-         unscaled sums (the byte tables as in pass 1); y at the pair start from its checkpoint difference */
-      const int npair = (khi - klo + 2) >> 1;
+    if (B8 && SR_CKG > 1) {
+      /* checkpoints after every SR_CKG-th window word: the group holding u, then the word from the group's
+         own unscaled sums (the byte tables as in pass 1, its words read in one round trip); y at the group
+         start from its checkpoint difference.  The group's partial sums Sa + yg A_t (A_t the unscaled sum
+         of its first t words) re-associate pass 1's chain: within REL's + 32 and the 2^-46 of ABS. */
+      const int ngrp = (khi - klo + SR_CKG) / SR_CKG;
       int g = 0;
-      for (int k0 = 0; k0 < npair - 1; k0 += SR_WCH) {
+      for (int k0 = 0; k0 < ngrp - 1; k0 += SR_WCH) {
         double cv[SR_WCH];
 #pragma unroll
-        for (int t = 0; t < SR_WCH; ++t) cv[t] = (k0 + t < npair - 1) ? (double)ck[(k0 + t) * ckstride] : 0.0;
+        for (int t = 0; t < SR_WCH; ++t) cv[t] = (k0 + t < ngrp - 1) ? (double)ck[(k0 + t) * ckstride] : 0.0;
 #pragma unroll
-        for (int t = 0; t < SR_WCH; ++t) g += (k0 + t < npair - 1 && cv[t] * inv < u) ? 1 : 0;
+        for (int t = 0; t < SR_WCH; ++t) g += (k0 + t < ngrp - 1 && cv[t] * inv < u) ? 1 : 0;
       }
       const double Sa = (g == 0) ? 0.0 : (double)ck[(g - 1) * ckstride];
-      const double Sb = (g == npair - 1) ? S : (double)ck[g * ckstride];
-      const int k1 = klo + 2 * g, k2 = k1 + 1;
-      const bool two = k2 <= khi;
-      /* unscaled sum and product of window word k (y = 1 at its start), as pass 1 adds it */
-      auto wsum = [&](int k, double &P) -> double {
-        const uint32_t ww = walk_word(Pm, M, N, NW, rev, k);
-        const int nb = min(32, L + 1 - 32 * k), nfk = nb >> 3, c8 = nb & 7;
-        double2 t8[4];
+      const double Sb = (g == ngrp - 1) ? S : (double)ck[g * ckstride];
+      const int k1 = klo + SR_CKG * g;
+      uint32_t gw[SR_CKG];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint32_t e = (q < nfk) ? ((ww >> (8 * q)) & 255u) : 256u;
-          t8[q] = *reinterpret_cast<const double2 *>(T8 + 2 * e);
+      for (int t = 0; t < SR_CKG; ++t) gw[t] = (k1 + t <= khi) ? walk_word(Pm, M, N, NW, rev, k1 + t) : 0u;
+      double A[SR_CKG], Yt[SR_CKG];   /* unscaled sum of the group's words before word t, product before t */
+      double acc = 0.0, yy = 1.0;
+#pragma unroll
+      for (int t = 0; t < SR_CKG; ++t) {
+        A[t] = acc;
+        Yt[t] = yy;
+        if (k1 + t <= khi) {
+          const uint32_t ww = gw[t];
+          const int nb = min(32, L + 1 - 32 * (k1 + t)), nfk = nb >> 3, c8 = nb & 7;
+          double2 t8[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t e = (q < nfk) ? ((ww >> (8 * q)) & 255u) : 256u;
+            t8[q] = *reinterpret_cast<const double2 *>(T8 + 2 * e);
+          }
+          const double w23 = __builtin_fma(t8[2].y, t8[3].x, t8[2].x);
+          const double w13 = __builtin_fma(t8[1].y, w23, t8[1].x);
+          double W = __builtin_fma(t8[0].y, w13, t8[0].x);
+          const double P = (t8[0].y * t8[1].y) * (t8[2].y * t8[3].y);
+          if (c8 > 0) {
+            const uint32_t eb = (ww >> (8 * nfk)) & 255u;
+            const double2 tlo = t4sp(T4, min(c8, 4), eb & 15u);
+            W = __builtin_fma(P, tlo.x, W);
+            W = __builtin_fma(P * tlo.y, t4s(T4, max(c8 - 4, 0), eb >> 4), W);
+          }
+          acc = __builtin_fma(yy, W, acc);
+          yy = yy * P;
         }
-        const double w23 = __builtin_fma(t8[2].y, t8[3].x, t8[2].x);
-        const double w13 = __builtin_fma(t8[1].y, w23, t8[1].x);
-        double W = __builtin_fma(t8[0].y, w13, t8[0].x);
-        P = (t8[0].y * t8[1].y) * (t8[2].y * t8[3].y);
-        if (c8 > 0) {
-          const uint32_t eb = (ww >> (8 * nfk)) & 255u;
-          const double2 tlo = t4sp(T4, min(c8, 4), eb & 15u);
-          W = __builtin_fma(P, tlo.x, W);
-          W = __builtin_fma(P * tlo.y, t4s(T4, max(c8 - 4, 0), eb >> 4), W);
-        }
-        return W;
-      };
-      double P1 = 1.0, P2 = 1.0;
-      const double U1 = wsum(k1, P1);
-      const double U2 = two ? wsum(k2, P2) : 0.0;
-      const double yg = (g == 0) ? y0 : (Sb - Sa) / __builtin_fma(P1, U2, U1);
-      const double S1 = __builtin_fma(yg, U1, Sa);
-      if (two && S1 * inv < u) { j = k2; Sp0 = S1; yj = yg * P1; }
-      else { j = k1; Sp0 = Sa; yj = yg; }
+      }
+      const double yg = (g == 0) ? y0 : (Sb - Sa) / acc;
+      int t_sel = 0;
+#pragma unroll
+      for (int t = 1; t < SR_CKG; ++t) t_sel += (k1 + t <= khi && __builtin_fma(yg, A[t], Sa) * inv < u) ? 1 : 0;
+      double At = A[0], Yp = Yt[0];
+#pragma unroll
+      for (int t = 1; t < SR_CKG; ++t)
+        if (t == t_sel) { At = A[t]; Yp = Yt[t]; }
+      j = k1 + t_sel;
+      Sp0 = __builtin_fma(yg, At, Sa);
+      yj = yg * Yp;
     } else {
       for (int k0 = klo; k0 < khi; k0 += SR_WCH) {
         double cv[SR_WCH];
@@ -1019,7 +1034,7 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, const uint16_t *pre
         gsum[g] = acc;
         yy = yy * t.y;
       }
-      const double y = (B8 && SR_CKG == 2) ? yj : ((j == klo) ? y0 : (yj - Sp0) / acc);
+      const double y = (B8 && SR_CKG > 1) ? yj : ((j == klo) ? y0 : (yj - Sp0) / acc);
 #pragma unroll
       for (int g = 0; g < 8; ++g) {
         gsum[g] = __builtin_fma(y, gsum[g], Sp0);

@@ -93,7 +93,7 @@ struct KArgs {
 /* HBM-column kernels: window words per stored Gibbs checkpoint (1, or 2: half the checkpoint stream again;
    pass 2 then splits the chosen pair from the words' own sums) */
 #ifndef SR_CKG
-#define SR_CKG 2
+#define SR_CKG 4
 #endif
 #ifndef SR_KARG_RELOAD
 #define SR_KARG_RELOAD 0

@@ -92,6 +92,14 @@ struct KArgs {
 #endif
 /* HBM-column kernels: window words per stored Gibbs checkpoint (1, or 2: half the checkpoint stream again;
    pass 2 then splits the chosen pair from the words' own sums) */
+/* HBM-column kernels: pi2 / swap / pi3 reversals word-parallel (seg_reverse_gm) and the prefix entries
+   rewritten with the moved words (1), or the per-bit exchange loop and a prefix pass (0: A/B) */
+#ifndef SR_SEGREV
+#define SR_SEGREV 1
+#endif
+#ifndef SR_SEGCH
+#define SR_SEGCH 4   /* output words per round trip of seg_reverse_gm's second pass */
+#endif
 #ifndef SR_CKG
 #define SR_CKG 4
 #endif
@@ -1618,6 +1626,99 @@ __device__ __forceinline__ uint32_t range_mask(int w, int lo, int hi)
   return (n == 32) ? 0xffffffffu : (((1u << n) - 1u) << (lo - b0));
 }
 
+/* the bits of x at the set positions of msk, packed from bit 0 (pext), and the inverse (pdep): msk is
+   block-uniform and has few runs (a word's positions in a segment, less its hard sites) */
+__device__ __forceinline__ uint32_t bits_pack(uint32_t x, uint32_t msk)
+{
+  uint32_t r = 0u;
+  int o = 0;
+  while (msk) {
+    const int s = __builtin_ctz(msk);
+    const uint32_t t = ~(msk >> s);
+    const int l = t ? __builtin_ctz(t) : 32 - s;
+    const uint32_t lm = (l == 32) ? 0xffffffffu : ((1u << l) - 1u);
+    r |= ((x >> s) & lm) << o;
+    o += l;
+    msk &= ~(lm << s);
+  }
+  return r;
+}
+__device__ __forceinline__ uint32_t bits_unpack(uint32_t v, uint32_t msk)
+{
+  uint32_t r = 0u;
+  int o = 0;
+  while (msk) {
+    const int s = __builtin_ctz(msk);
+    const uint32_t t = ~(msk >> s);
+    const int l = t ? __builtin_ctz(t) : 32 - s;
+    const uint32_t lm = (l == 32) ? 0xffffffffu : ((1u << l) - 1u);
+    r |= ((v >> o) & lm) << s;
+    o += l;
+    msk &= ~(lm << s);
+  }
+  return r;
+}
+
+/* HBM columns: reverse a column's bits at the positions of [i, j] -- all of them (pi2 / swap, mcmc.c:
+   1446-1474) or the non-hard ones (HARD: pi3, mcmc.c:1641-1670, hard sites stay) -- word-parallel, and
+   rewrite the column prefix entries (i/32, j/32].  The per-bit exchange loop costs one dependent memory
+   round trip per bit pair on HBM columns (~170 for a mean pi2 / pi3 reversal at 1024 sites); here the
+   selected bits are packed into the thread's scratch D (Kt bits, in the Gibbs checkpoint slots, idle in
+   this phase), and each output word takes its c bits as the bit-reversed 32-bit window of D ending at
+   Kt - off (off: the selected positions before the word): D' bit k = D bit Kt - 1 - k. */
+template <bool HARD>
+__device__ void seg_reverse_gm(uint32_t *Pm, uint16_t *prem, int M, int i, int j, const uint32_t *hbw,
+                               uint32_t *sc, int scs)
+{
+  const int wlo = i >> 5, whi = j >> 5;
+  auto msk_of = [&](int w) -> uint32_t { const uint32_t r = range_mask(w, i, j); return HARD ? (r & ~hbw[w]) : r; };
+  uint64_t acc = 0;
+  int fill = 0, dn = 0;
+  for (int w0 = wlo; w0 <= whi; w0 += 8) {
+    uint32_t wv[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) wv[t] = (w0 + t <= whi) ? Pm[(w0 + t) * M] : 0u;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      if (w0 + t <= whi) {
+        const uint32_t mk = msk_of(w0 + t);
+        acc |= (uint64_t)bits_pack(wv[t], mk) << fill;
+        fill += __popc(mk);
+        if (fill >= 32) { sc[dn * scs] = (uint32_t)acc; ++dn; acc >>= 32; fill -= 32; }
+      }
+    }
+  }
+  if (fill > 0) sc[dn * scs] = (uint32_t)acc;
+  const int Kt = 32 * dn + fill, dtop = (Kt - 1) >> 5;
+  int off = 0, sacc = prem[wlo * M];
+  for (int w0 = wlo; w0 <= whi; w0 += SR_SEGCH) {
+    uint32_t wv[SR_SEGCH], d0[SR_SEGCH], d1[SR_SEGCH], mks[SR_SEGCH];
+    int offs[SR_SEGCH];
+#pragma unroll
+    for (int t = 0; t < SR_SEGCH; ++t) {
+      const bool in = w0 + t <= whi;
+      mks[t] = in ? msk_of(w0 + t) : 0u;
+      offs[t] = off;
+      off += __popc(mks[t]);
+      const int q = (Kt - offs[t] - 32) >> 5;   /* (floor: the window may start below bit 0) */
+      wv[t] = in ? Pm[(w0 + t) * M] : 0u;
+      d0[t] = (in && q >= 0) ? sc[q * scs] : 0u;
+      d1[t] = (in && q + 1 >= 0 && q + 1 <= dtop) ? sc[(q + 1) * scs] : 0u;
+    }
+#pragma unroll
+    for (int t = 0; t < SR_SEGCH; ++t) {
+      const int w = w0 + t;
+      if (w <= whi) {
+        const int sh = (Kt - offs[t] - 32) & 31;
+        const uint32_t win = (uint32_t)((((uint64_t)d1[t] << 32) | d0[t]) >> sh);
+        const uint32_t nw = (wv[t] & ~mks[t]) | bits_unpack(__brev(win), mks[t]);
+        Pm[w * M] = nw;
+        if (w < whi) { sacc += __popc(nw); prem[(w + 1) * M] = (uint16_t)sacc; }
+      }
+    }
+  }
+}
+
 /* ones of column m in [lo, mid) and [mid, hi) (one pass over the words) */
 __device__ __forceinline__ void ones_split(const uint32_t *Pm, int M, int lo, int mid, int hi, int &O1, int &O2)
 {
@@ -2897,6 +2998,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           if (tid == 0) misc[MS_ACC + (kind == PK_PI1 ? 3 : kind == PK_PI2 ? 4 : kind == PK_SWAP ? 5 : 6)]++;
           loglik += delta;
           const int16_t *nhp = nhall + q.r0;   /* pi3: the non-hard positions of [i, j] in order */
+          constexpr bool GMX = GM && SR_SEGREV;   /* HBM columns: word-parallel reversals, prefix with the words */
           for (int m = (PR && hf) ? M : olo + tx; m < ohi; m += TXS) {   /* PR: the even lane of each pair; SP: own taxa */
             uint32_t *Pm = P + m;
             const int a = sab[m], b = sab[M + m];
@@ -2911,6 +3013,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 if (ii < a && a <= jj + 1) sab[m] = a - 1;
                 if (ii < b && b <= jj + 1) sab[M + m] = b - 1;
                 const uint32_t vb = (Pm[(i >> 5) * M] >> (i & 31)) & 1u;
+                int sacc = GMX ? (int)pre[(i >> 5) * M + m] : 0;   /* (HBM columns: prefix entries (i/32, j/32] here) */
                 for (int w0 = i >> 5; w0 <= (j >> 5); w0 += 8) {
                   uint32_t wv[9];
 #pragma unroll
@@ -2925,6 +3028,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                       uint32_t nw = (old & ~m1) | (sh & m1);
                       if ((j >> 5) == w) nw = (nw & ~(1u << (j & 31))) | (vb << (j & 31));
                       Pm[w * M] = nw;
+                      if (GMX && w < (j >> 5)) { sacc += __popc(nw); pre[(w + 1) * M + m] = (uint16_t)sacc; }
                     }
                   }
                 }
@@ -2932,6 +3036,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 if (ii <= a && a <= jj) sab[m] = a + 1;
                 if (ii <= b && b <= jj) sab[M + m] = b + 1;
                 const uint32_t vb = (Pm[(i >> 5) * M] >> (i & 31)) & 1u;
+                int sacc = GMX ? (int)pre[((i >> 5) + 1) * M + m] : 0;   /* (entry i/32 + 1 does not change) */
                 for (int w0 = i >> 5; w0 >= (j >> 5); w0 -= 8) {
                   uint32_t wv[9];   /* wv[t] = word w0 - t */
 #pragma unroll
@@ -2946,6 +3051,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                       uint32_t nw = (old & ~m1) | (sh & m1);
                       if ((j >> 5) == w) nw = (nw & ~(1u << (j & 31))) | (vb << (j & 31));
                       Pm[w * M] = nw;
+                      if (GMX && w > (j >> 5)) { sacc -= __popc(nw); pre[w * M + m] = (uint16_t)sacc; }
                     }
                   }
                 }
@@ -2956,7 +3062,11 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               if (ain && !bin) sab[m] = i + j + 1 - a;
               else if (!ain && bin) sab[M + m] = i + j + 1 - b;
               else if (ain && bin) { sab[M + m] = i + j + 1 - a; sab[m] = i + j + 1 - b; }
-              if (kind != PK_PI3) {
+              if constexpr (GMX) {
+                uint32_t *sc = reinterpret_cast<uint32_t *>(ckb + ckslot);
+                if (kind != PK_PI3) seg_reverse_gm<false>(Pm, pre + m, M, i, j, hbw, sc, CKS * (int)(sizeof(CKT) / 4));
+                else seg_reverse_gm<true>(Pm, pre + m, M, i, j, hbw, sc, CKS * (int)(sizeof(CKT) / 4));
+              } else if (kind != PK_PI3) {
                 for (int n = i; n < i + j - n; ++n) {
                   const int p2 = i + j - n;
                   const uint32_t b1 = (Pm[(n >> 5) * M] >> (n & 31)) & 1u, b2 = (Pm[(p2 >> 5) * M] >> (p2 & 31)) & 1u;
@@ -2970,7 +3080,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 }
               }
             }
-            {   /* the move permutes positions [lo, hi] only: prefix entries (lo/32, hi/32] change */
+            if (!GMX) {   /* the move permutes positions [lo, hi] only: prefix entries (lo/32, hi/32] change
+                            (HBM columns: rewritten with the words above) */
               const int lo = min(i, j), hi = max(i, j), rlo = (lo >> 5) + 1, rhi = hi >> 5;
               uint16_t *prem = pre + m;
               int sacc = prem[(rlo - 1) * M];

@@ -92,10 +92,15 @@ struct KArgs {
 #endif
 /* HBM-column kernels: window words per stored Gibbs checkpoint (1, or 2: half the checkpoint stream again;
    pass 2 then splits the chosen pair from the words' own sums) */
-/* HBM-column kernels: pi2 / swap / pi3 reversals word-parallel (seg_reverse_gm) and the prefix entries
-   rewritten with the moved words (1), or the per-bit exchange loop and a prefix pass (0: A/B) */
+/* HBM-column kernels: pi2 / swap / pi3 reversals word-parallel (seg_reverse_gm, 1) or by the per-bit
+   exchange loop (0, the default: the word-parallel form is bit-exact but measured 0.9 % slower on config 5,
+   r04h -- 0.25 accepted reversals per sweep, and its registers add 45 VGPR spills to the split kernel);
+   SR_PFUSE: pi1's column prefix entries rewritten with the shifted words instead of a second pass */
 #ifndef SR_SEGREV
-#define SR_SEGREV 1
+#define SR_SEGREV 0
+#endif
+#ifndef SR_PFUSE
+#define SR_PFUSE 0
 #endif
 #ifndef SR_SEGCH
 #define SR_SEGCH 4   /* output words per round trip of seg_reverse_gm's second pass */
@@ -2998,7 +3003,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           if (tid == 0) misc[MS_ACC + (kind == PK_PI1 ? 3 : kind == PK_PI2 ? 4 : kind == PK_SWAP ? 5 : 6)]++;
           loglik += delta;
           const int16_t *nhp = nhall + q.r0;   /* pi3: the non-hard positions of [i, j] in order */
-          constexpr bool GMX = GM && SR_SEGREV;   /* HBM columns: word-parallel reversals, prefix with the words */
+          constexpr bool GMX = GM && SR_PFUSE;    /* HBM columns: pi1's prefix entries with the shifted words */
+          constexpr bool GMR = GM && SR_SEGREV;   /* HBM columns: word-parallel reversals (prefix with the words) */
           for (int m = (PR && hf) ? M : olo + tx; m < ohi; m += TXS) {   /* PR: the even lane of each pair; SP: own taxa */
             uint32_t *Pm = P + m;
             const int a = sab[m], b = sab[M + m];
@@ -3062,7 +3068,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               if (ain && !bin) sab[m] = i + j + 1 - a;
               else if (!ain && bin) sab[M + m] = i + j + 1 - b;
               else if (ain && bin) { sab[M + m] = i + j + 1 - a; sab[m] = i + j + 1 - b; }
-              if constexpr (GMX) {
+              if constexpr (GMR) {
                 uint32_t *sc = reinterpret_cast<uint32_t *>(ckb + ckslot);
                 if (kind != PK_PI3) seg_reverse_gm<false>(Pm, pre + m, M, i, j, hbw, sc, CKS * (int)(sizeof(CKT) / 4));
                 else seg_reverse_gm<true>(Pm, pre + m, M, i, j, hbw, sc, CKS * (int)(sizeof(CKT) / 4));
@@ -3080,7 +3086,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 }
               }
             }
-            if (!GMX) {   /* the move permutes positions [lo, hi] only: prefix entries (lo/32, hi/32] change
+            if (kind == PK_PI1 ? !GMX : !GMR) {   /* the move permutes positions [lo, hi] only: prefix entries (lo/32, hi/32] change
                             (HBM columns: rewritten with the words above) */
               const int lo = min(i, j), hi = max(i, j), rlo = (lo >> 5) + 1, rhi = hi >> 5;
               uint16_t *prem = pre + m;

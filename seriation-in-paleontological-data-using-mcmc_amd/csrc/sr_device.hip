@@ -99,6 +99,12 @@ struct KArgs {
 #ifndef SR_SEGREV
 #define SR_SEGREV 0
 #endif
+/* split chains: the own taxon's limits and counts also kept in registers across the launch (SR_APREG 1;
+   HBM stays the state every other reader sees) -- a load round trip fewer at the start of the Gibbs step,
+   of every proposal batch and of every accepted move's update */
+#ifndef SR_APREG
+#define SR_APREG 0
+#endif
 #ifndef SR_PFUSE
 #define SR_PFUSE 0
 #endif
@@ -2206,6 +2212,12 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   const UDivM mdH = make_udivm((uint32_t)N - nhard > 0 ? (uint32_t)N - nhard : 1u);
   const UDivM mdH1 = make_udivm((uint32_t)N - nhard > 1 ? (uint32_t)N - nhard - 1 : 1u);
   STAMP_DECL
+  constexpr bool APR = SP && SR_APREG;   /* (one taxon per thread: m == mt) */
+  int ra_ = 0, rb_ = 0, rt0 = 0, rf0 = 0, rt1 = 0, rf1 = 0;
+  if (APR && mt < ohi) {
+    ra_ = sab[mt]; rb_ = sab[M + mt];
+    rt0 = scnt[mt]; rf0 = scnt[M + mt]; rt1 = scnt[2 * M + mt]; rf1 = scnt[3 * M + mt];
+  }
 
   for (int call = 0; call < A.calls; ++call) {
     for (int sw = 0; sw < A.spc; ++sw) {
@@ -2213,7 +2225,9 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       /* ============ phase A: totals and the c, d draws (mcmc.c:768-825) */
       {
         int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-        for (int m = olo + tid; m < ohi; m += TB) { s0 += scnt[m]; s1 += scnt[M + m]; s2 += scnt[2 * M + m]; s3 += scnt[3 * M + m]; }
+        if constexpr (APR) { if (mt < ohi) { s0 = rt0; s1 = rf0; s2 = rt1; s3 = rf1; } }
+        else
+          for (int m = olo + tid; m < ohi; m += TB) { s0 += scnt[m]; s1 += scnt[M + m]; s2 += scnt[2 * M + m]; s3 += scnt[3 * M + m]; }
         s0 = wave_sum_i32(s0); s1 = wave_sum_i32(s1); s2 = wave_sum_i32(s2); s3 = wave_sum_i32(s3);
         int *tw = tot + (par * NWV + wave) * 4;
         if (lane == 0) { tw[0] = s0; tw[1] = s1; tw[2] = s2; tw[3] = s3; }
@@ -2327,8 +2341,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           const uint32_t *Pm = P + m;
           const double ua = rng_peek(R, 2 * (m - mlo)) / 4294967296.0;
           const double ub = rng_peek(R, 2 * (m - mlo) + 1) / 4294967296.0;
-          const int a0 = sab[m], b0 = sab[M + m];
-          int t0 = scnt[m], f0 = scnt[M + m], t1 = scnt[2 * M + m], f1 = scnt[3 * M + m];
+          const int a0 = APR ? ra_ : sab[m], b0 = APR ? rb_ : sab[M + m];
+          int t0 = APR ? rt0 : scnt[m], f0 = APR ? rf0 : scnt[M + m], t1 = APR ? rt1 : scnt[2 * M + m], f1 = APR ? rf1 : scnt[3 * M + m];
           /* a_m over [0, b_m], then b_m over the reversed column with limit N - a_new: one
              inlined copy of the draw, two trips */
           int na = a0, nb = b0;
@@ -2406,6 +2420,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             nchg += (na != a0) + (nb != b0);
             sab[m] = na; sab[M + m] = nb;
             scnt[m] = t0; scnt[M + m] = f0; scnt[2 * M + m] = t1; scnt[3 * M + m] = f1;
+            if constexpr (APR) { ra_ = na; rb_ = nb; rt0 = t0; rf0 = f0; rt1 = t1; rf1 = f1; }
             if (want_logl) {   /* mcmc_logl term (mcmc.c:643-644); manycd: the taxon's c, d (mcmc.c:641-642) */
               const double kcc = MCD ? cx[m] : K.cc, kd = MCD ? cv[M + m] : K.d, kdd = MCD ? cx[M + m] : K.dd,
                            kc = MCD ? cv[m] : K.c;
@@ -2723,7 +2738,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           const bool one = NWM > 0 || SP || M <= TXS;   /* register-walk kernels: M <= TB (sr_regwalk); SP: halves <= TB */
           int a1 = 0, b1 = 0;
           const HM hb1 = hbc;
-          if (one && mt < ohi) { a1 = sab[mt]; b1 = sab[M + mt]; }
+          if (one && mt < ohi) { a1 = APR ? ra_ : sab[mt]; b1 = APR ? rb_ : sab[M + mt]; }
           FST(13);
 #if defined(SR_STAMP_DRAWS)
           STAMP(5);
@@ -3007,17 +3022,25 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           constexpr bool GMR = GM && SR_SEGREV;   /* HBM columns: word-parallel reversals (prefix with the words) */
           for (int m = (PR && hf) ? M : olo + tx; m < ohi; m += TXS) {   /* PR: the even lane of each pair; SP: own taxa */
             uint32_t *Pm = P + m;
-            const int a = sab[m], b = sab[M + m];
+            const int a = APR ? ra_ : sab[m], b = APR ? rb_ : sab[M + m];
             int dt0, dt1;
             taxon_dt(kind, q, a, b, Pm, pre + m, M, kind == PK_PI3 ? hard_bits_col<HM>(Pm, M, hl, nh) : (HM)0, hcnt, nhall, dt0, dt1,
                      hbx);
-            scnt[m] += dt0; scnt[M + m] -= dt0; scnt[2 * M + m] += dt1; scnt[3 * M + m] -= dt1;
+            if constexpr (APR) {
+              rt0 += dt0; rf0 -= dt0; rt1 += dt1; rf1 -= dt1;
+              scnt[m] = rt0; scnt[M + m] = rf0; scnt[2 * M + m] = rt1; scnt[3 * M + m] = rf1;
+            } else {
+              scnt[m] += dt0; scnt[M + m] -= dt0; scnt[2 * M + m] += dt1; scnt[3 * M + m] -= dt1;
+            }
+            int na_ = a, nb_ = b;   /* HBM columns: the new limits, stored below when they change */
+            auto set_a = [&](int v) { if constexpr (GM) na_ = v; else sab[m] = v; };
+            auto set_b = [&](int v) { if constexpr (GM) nb_ = v; else sab[M + m] = v; };
             if (kind == PK_PI1) {                                  /* mcmc.c:1266-1297 */
               /* the shifted words read 8 at a time before they are rewritten (one memory round trip
                  per 8 words: the HBM-column kernels) */
               if (i < j) {
-                if (ii < a && a <= jj + 1) sab[m] = a - 1;
-                if (ii < b && b <= jj + 1) sab[M + m] = b - 1;
+                if (ii < a && a <= jj + 1) set_a(a - 1);
+                if (ii < b && b <= jj + 1) set_b(b - 1);
                 const uint32_t vb = (Pm[(i >> 5) * M] >> (i & 31)) & 1u;
                 int sacc = GMX ? (int)pre[(i >> 5) * M + m] : 0;   /* (HBM columns: prefix entries (i/32, j/32] here) */
                 for (int w0 = i >> 5; w0 <= (j >> 5); w0 += 8) {
@@ -3039,8 +3062,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                   }
                 }
               } else {
-                if (ii <= a && a <= jj) sab[m] = a + 1;
-                if (ii <= b && b <= jj) sab[M + m] = b + 1;
+                if (ii <= a && a <= jj) set_a(a + 1);
+                if (ii <= b && b <= jj) set_b(b + 1);
                 const uint32_t vb = (Pm[(i >> 5) * M] >> (i & 31)) & 1u;
                 int sacc = GMX ? (int)pre[((i >> 5) + 1) * M + m] : 0;   /* (entry i/32 + 1 does not change) */
                 for (int w0 = i >> 5; w0 >= (j >> 5); w0 -= 8) {
@@ -3065,9 +3088,9 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             } else {                                               /* mcmc.c:1446-1474, 1641-1670 */
               const int ain = ininterval(a, i, j + 1, inc1, inc2);
               const int bin = ininterval(b, i, j + 1, inc1, inc2);
-              if (ain && !bin) sab[m] = i + j + 1 - a;
-              else if (!ain && bin) sab[M + m] = i + j + 1 - b;
-              else if (ain && bin) { sab[M + m] = i + j + 1 - a; sab[m] = i + j + 1 - b; }
+              if (ain && !bin) set_a(i + j + 1 - a);
+              else if (!ain && bin) set_b(i + j + 1 - b);
+              else if (ain && bin) { set_b(i + j + 1 - a); set_a(i + j + 1 - b); }
               if constexpr (GMR) {
                 uint32_t *sc = reinterpret_cast<uint32_t *>(ckb + ckslot);
                 if (kind != PK_PI3) seg_reverse_gm<false>(Pm, pre + m, M, i, j, hbw, sc, CKS * (int)(sizeof(CKT) / 4));
@@ -3085,6 +3108,11 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                   if (b1 != b2) { Pm[(n >> 5) * M] ^= (1u << (n & 31)); Pm[(p2 >> 5) * M] ^= (1u << (p2 & 31)); }
                 }
               }
+            }
+            if constexpr (GM) {
+              if (na_ != a) sab[m] = na_;
+              if (nb_ != b) sab[M + m] = nb_;
+              if constexpr (APR) { ra_ = na_; rb_ = nb_; }
             }
             if (kind == PK_PI1 ? !GMX : !GMR) {   /* the move permutes positions [lo, hi] only: prefix entries (lo/32, hi/32] change
                             (HBM columns: rewritten with the words above) */

@@ -105,6 +105,12 @@ struct KArgs {
 #ifndef SR_APREG
 #define SR_APREG 0
 #endif
+/* split chains: the per-sweep totals and per-batch proposal sums exchanged as {sequence, value} words that
+   the other half polls directly (SR_XTAG 1), instead of data, s_waitcnt, barrier, flag, poll, barrier, data
+   (xsync) -- two memory round trips and two barriers fewer per exchange */
+#ifndef SR_XTAG
+#define SR_XTAG 0
+#endif
 #ifndef SR_PFUSE
 #define SR_PFUSE 0
 #endif
@@ -193,7 +199,10 @@ __host__ __device__ static constexpr inline Lay sr_layout(int N, int M, int NW, 
  * slots per chain (ints): [2 parity][2 half][4] totals, [2 parity][2 half][16][4] proposal sums,
  * [2 parity][KT] exact-delta chunk counts. */
 __host__ __device__ static inline int sr_sp_half(int M) { return (((M + 1) / 2) + 63) & ~63; }
-__host__ __device__ static inline size_t sr_sp_xb(int M) { return 16 + 256 + 2 * (size_t)((M + 63) / 64); }
+/* + tagged slots (SR_XTAG, 8-byte aligned): [2 parity][2 half][4] totals and [2 parity][2 half][16][4] proposal
+ * sums as {sequence, value} words, 272 u64 */
+__host__ __device__ static inline size_t sr_sp_xt0(int M) { return (16 + 256 + 2 * (size_t)((M + 63) / 64) + 1) & ~(size_t)1; }
+__host__ __device__ static inline size_t sr_sp_xb(int M) { return sr_sp_xt0(M) + 2 * 272; }
 /* per-chain HBM scratch of the gm variant (elements): pre u16, ck f64, lbuf f64, cbuf f64 */
 __host__ __device__ static inline size_t sr_gm_pre(int M, int NW) { return (size_t)(NW + 1) * M; }
 __host__ __device__ static inline size_t sr_gm_ck(int N, int M, int TB) { return (size_t)((N >> 5) + 1) * sr_ckstride(M, TB); }
@@ -2125,6 +2134,24 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   int *xb = SP ? A.xbuf + (size_t)chain * sr_sp_xb(M) : nullptr;
   int xseq = 0;
   bool xbroken = false;   /* thread 0: the other half missed a deadline once; stop waiting */
+  constexpr bool XTG = SP && SR_XTAG;
+  uint64_t *xt = XTG ? reinterpret_cast<uint64_t *>(xb + sr_sp_xt0(M)) : nullptr;
+  uint32_t tseq = 0;   /* tagged exchanges so far (block-uniform, the same sequence in both halves) */
+  auto tput = [&](uint64_t *q, int v) { xst(q, ((uint64_t)tseq << 32) | (uint64_t)(uint32_t)v); };
+  /* the other half's four tagged values of this exchange (bounded poll, as xsync's) */
+  auto tget4 = [&](const uint64_t *q, int &v0, int &v1, int &v2, int &v3) {
+    int n = 0;
+    while (true) {
+      const uint64_t w0 = xld(q), w1 = xld(q + 1), w2 = xld(q + 2), w3 = xld(q + 3);
+      if (xbroken || ((uint32_t)(w0 >> 32) == tseq && (uint32_t)(w1 >> 32) == tseq && (uint32_t)(w2 >> 32) == tseq &&
+                      (uint32_t)(w3 >> 32) == tseq)) {
+        v0 = (int)(uint32_t)w0; v1 = (int)(uint32_t)w1; v2 = (int)(uint32_t)w2; v3 = (int)(uint32_t)w3;
+        return;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      if (++n > (1 << 22)) { xbroken = true; xst(A.xerr, 1); }
+    }
+  };
   /* both halves' exchange writes done and visible: each thread's stores acknowledged, the block's
      flag raised, the other half's flag awaited (bounded: a half that never arrives -- not
      co-resident -- sets xerr and the launch completes with garbage the host refuses) */
@@ -2243,7 +2270,14 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           const int *tw = tot + (par * NWV + w) * 4;
           s0 += tw[0]; s1 += tw[1]; s2 += tw[2]; s3 += tw[3];
         }
-        if constexpr (SP) {   /* + the other half's totals */
+        if constexpr (XTG) {   /* + the other half's totals (tagged) */
+          ++tseq;
+          uint64_t *xq = xt + par * 8;
+          if (tid == 0) { tput(xq + 4 * half, s0); tput(xq + 4 * half + 1, s1); tput(xq + 4 * half + 2, s2); tput(xq + 4 * half + 3, s3); }
+          int o0, o1, o2, o3;
+          tget4(xq + 4 * (half ^ 1), o0, o1, o2, o3);
+          s0 += o0; s1 += o1; s2 += o2; s3 += o3;
+        } else if constexpr (SP) {   /* + the other half's totals */
           int *xt = xb + par * 8;
           if (tid == 0) { xst(xt + 4 * half, s0); xst(xt + 4 * half + 1, s1); xst(xt + 4 * half + 2, s2); xst(xt + 4 * half + 3, s3); }
           xsync();
@@ -2883,16 +2917,22 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           FST(4);
           __syncthreads();
           if constexpr (SP) {   /* this half's sums of the batch's proposals (lane p of wave 0), exchanged */
+            if constexpr (XTG) ++tseq;
             if (wave == 0 && lane >= p0 && lane < pend && lane < 16 && !((vpk >> 26) & 1)) {
               int X0 = 0, X1 = 0, Y0 = 0, Y1 = 0;
               for (int w = 0; w < NWV; ++w) {
                 const int *o = pw + (lane * NWV + w) * 8;
                 X0 += o[0]; X1 += o[1]; Y0 += o[2]; Y1 += o[3];
               }
-              int *xp = xb + 16 + ((bpar * 2 + half) * 16 + lane) * 4;
-              xst(xp, X0); xst(xp + 1, X1); xst(xp + 2, Y0); xst(xp + 3, Y1);
+              if constexpr (XTG) {
+                uint64_t *xq = xt + 16 + ((bpar * 2 + half) * 16 + lane) * 4;
+                tput(xq, X0); tput(xq + 1, X1); tput(xq + 2, Y0); tput(xq + 3, Y1);
+              } else {
+                int *xp = xb + 16 + ((bpar * 2 + half) * 16 + lane) * 4;
+                xst(xp, X0); xst(xp + 1, X1); xst(xp + 2, Y0); xst(xp + 3, Y1);
+              }
             }
-            xsync();
+            if constexpr (!XTG) xsync();
           }
           STAMP_E(5);
           FST(5);
@@ -2919,7 +2959,11 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                   const int *o = pw + (p * NWV + w) * 8;
                   X0 += o[0]; X1 += o[1]; Y0 += o[2]; Y1 += o[3];
                 }
-                if constexpr (SP) {   /* + the other half's */
+                if constexpr (XTG) {   /* + the other half's (tagged: polled here) */
+                  int o0, o1, o2, o3;
+                  tget4(xt + 16 + ((bpar * 2 + (half ^ 1)) * 16 + p) * 4, o0, o1, o2, o3);
+                  X0 += o0; X1 += o1; Y0 += o2; Y1 += o3;
+                } else if constexpr (SP) {   /* + the other half's */
                   const int *yp = xb + 16 + ((bpar * 2 + (half ^ 1)) * 16 + p) * 4;
                   X0 += xld(yp); X1 += xld(yp + 1); Y0 += xld(yp + 2); Y1 += xld(yp + 3);
                 }
@@ -3612,6 +3656,8 @@ extern "C" int srk_run(srk_dev *d, int calls, int spc, int save, int rec_base)
   A.calls = calls; A.spc = spc; A.save = save; A.rec_base = rec_base;
   sr_kfn k = sr_pick_kernel(d->TB, d->N, d->M, d->gm != 0, d->pr != 0, d->nh, d->sp != 0, d->mcd != 0);
   if (d->sp) HIPCHK(hipMemsetAsync(A.xflag, 0, (size_t)d->nchains * 2 * sizeof(int), d->stream));   /* exchange sequence restarts */
+  if (d->sp && SR_XTAG)   /* (and the tagged slots' sequence) */
+    HIPCHK(hipMemsetAsync(A.xbuf, 0, (size_t)d->nchains * sr_sp_xb(d->M) * sizeof(int), d->stream));
   if (d->have_events) HIPCHK(hipEventRecord(d->ev0, d->stream));
   if (d->jit) {   /* the run-time specialised kernel (same arguments; LDS columns: one workgroup per chain) */
     void *kp[] = {&A};

@@ -111,6 +111,10 @@ struct KArgs {
 #ifndef SR_XTAG
 #define SR_XTAG 0
 #endif
+/* HBM-column Gibbs draws: passes 0 and 1 fused into one walk over the words (SR_FUSE01 1, draw_fast) */
+#ifndef SR_FUSE01
+#define SR_FUSE01 0
+#endif
 #ifndef SR_PFUSE
 #define SR_PFUSE 0
 #endif
@@ -821,7 +825,71 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, const uint16_t *pre
      word-start q of the window (qmx), and window words whose start q lies more than SR_QSPAN below it
      are dropped from the ends (their entries hold < 2^-(SR_QSPAN-75) of the mass each; ABS covers it). */
   int klo = nk, khi = -1, Oklo = 0;
+  double y0 = 1.0, S = 0.0;
+  bool uf = false, done01 = false;
+  if constexpr (B8 && SR_FUSE01) {
+    /* HBM columns: passes 0 and 1 in one walk over the words (one round trip per SR_WCH words instead of
+       two), the chain scaled by 2^q relative to entry o rather than the window's largest word-start q:
+       window words start at q > -SR_WIN_T - 32 |vA|, so y stays normal unless a later word rises ~1000
+       bits above o, which overflows S (S >= 2^1000 or NaN) and sends the draw to the two-pass form.  The
+       sum runs on past the window's last word (not known yet) but S is taken after it; a word start
+       with y < 2^-700 (a dip) followed by a window word flags the draw, as pass 1 does. */
+    int O = 0;
+    double y = 0.0, Sk = 0.0;
+    bool dip = false, started = false;
+    for (int k0 = 0; k0 < nk; k0 += SR_WCH) {
+      uint32_t wv[SR_WCH];
+#pragma unroll
+      for (int t = 0; t < SR_WCH; ++t) wv[t] = (k0 + t < nk) ? walk_word(Pm, M, N, NW, rev, k0 + t) : 0u;
+#pragma unroll
+      for (int t = 0; t < SR_WCH; ++t) {
+        const int k = k0 + t;
+        if (k < nk) {
+          const uint32_t ww = wv[t];
+          const int nb = min(32, L + 1 - 32 * k);
+          const uint32_t vm = (nb >= 32) ? 0xffffffffu : ((1u << nb) - 1u);
+          const int w0 = 32 * k;
+          const double qs = (w0 <= o) ? ((double)((o - w0) - (POo - O)) * vA + (double)(POo - O) * vB)
+                                      : -((double)((w0 - o) - (O - POo)) * vA + (double)(O - POo) * vB);
+          const double ub = qs - (double)(nb - __popc(ww & vm)) * vA;
+          const bool inw = ub > -SR_WIN_T;
+          if (inw && !started) { started = true; klo = k; Oklo = O; y = exp2_split(qs); y0 = y; }
+          if (started) {
+            dip |= y < 0x1p-700;
+            if (inw) { uf |= dip; khi = k; }
+            const int nfk = nb >> 3, c8 = nb & 7;
+            double2 t8[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const uint32_t e = (g < nfk) ? ((ww >> (8 * g)) & 255u) : 256u;
+              t8[g] = *reinterpret_cast<const double2 *>(T8 + 2 * e);
+            }
+            const double w23 = __builtin_fma(t8[2].y, t8[3].x, t8[2].x);
+            const double w13 = __builtin_fma(t8[1].y, w23, t8[1].x);
+            const double W = __builtin_fma(t8[0].y, w13, t8[0].x);
+            const double pw = (t8[0].y * t8[1].y) * (t8[2].y * t8[3].y);
+            S = __builtin_fma(y, W, S);
+            y = y * pw;
+            if (c8 > 0) {   /* only the walk's last word */
+              const uint32_t eb = (ww >> (8 * nfk)) & 255u;
+              const double2 tlo = t4sp(T4, min(c8, 4), eb & 15u);
+              const double shi = t4s(T4, max(c8 - 4, 0), eb >> 4);
+              S = __builtin_fma(y, tlo.x, S);
+              S = __builtin_fma(y * tlo.y, shi, S);
+            }
+            if (inw) Sk = S;
+            if ((k - klo) % SR_CKG == SR_CKG - 1) ck[(SR_CKG > 1 ? (k - klo) / SR_CKG : k) * ckstride] = S;
+          }
+          O += __popc(ww);
+        }
+      }
+    }
+    S = Sk;
+    done01 = started && S > 0.0 && S < 0x1p1000 && !uf;
+    if (!done01) { klo = nk; khi = -1; Oklo = 0; y0 = 1.0; S = 0.0; uf = false; }
+  }
   double qlo = 0.0, qmx = -__builtin_inf(), qmn = __builtin_inf();
+  if (!done01) {
   {
     int O = 0;   /* ones among walk entries [0, 32k) */
     for (int k0 = 0; k0 < nk; k0 += SR_WCH) {
@@ -889,9 +957,7 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, const uint16_t *pre
   /* pass 1: S over the window, checkpoints; the chain scaled by 2^-qmx.  A chain that falls below
      2^-700 at a word start inside the window (q dipping far below qmx and possibly rising again)
      would lose precision: that draw takes the exact path (uf). */
-  const double y0 = exp2_split(qlo - (klo <= khi ? qmx : 0.0));
-  double S = 0.0;
-  bool uf = false;
+  y0 = exp2_split(qlo - (klo <= khi ? qmx : 0.0));
   {
     double y = y0;
     for (int k0 = klo; k0 <= khi; k0 += SR_WCH) {
@@ -946,6 +1012,7 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, const uint16_t *pre
       }
     }
   }
+  }   /* (!done01) */
   GSTAMP(2);
   /* pass 2: locate the word; y at its start from its own sum (no replay of the chain): the word's
      partial sums are Sp0 + y gs1[g] with gs1 its unscaled group-end sums (y = 1 at the word start)

@@ -15,5 +15,7 @@ for v in fuap fuse xtap; do
 done
 NOPARITY=1 BENCH_ARGS="--sites 1024 --taxa 2048 --calls-per-step 2 --block-threads 1024" bash tools/gpu_ab.sh ${OUT}_c5 apreg xtag xtap fuse fuap
 rc=$?
+[ $rc -eq 0 ] && SERIATION_LIB=$V/fuap/libseriation.so timeout -k 10 120 python tools/c5_fallbacks.py > gpurun_out/${OUT}/fb_fuap.json
+rc=$?
 echo "exit $rc"
 exit $rc

@@ -2306,8 +2306,9 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   const UDivM mdH = make_udivm((uint32_t)N - nhard > 0 ? (uint32_t)N - nhard : 1u);
   const UDivM mdH1 = make_udivm((uint32_t)N - nhard > 1 ? (uint32_t)N - nhard - 1 : 1u);
   STAMP_DECL
-  constexpr bool APR = SP && SR_APREG;   /* (one taxon per thread: m == mt) */
+  constexpr bool APR = SP && SR_APREG;   /* (one taxon per thread in phases A and C: m == mt) */
   int ra_ = 0, rb_ = 0, rt0 = 0, rf0 = 0, rt1 = 0, rf1 = 0;
+  bool rstale = false;   /* the Gibbs step's rounds gave the own taxon to another thread: reload in phase C */
   if (APR && mt < ohi) {
     ra_ = sab[mt]; rb_ = sab[M + mt];
     rt0 = scnt[mt]; rf0 = scnt[M + mt]; rt1 = scnt[2 * M + mt]; rf1 = scnt[3 * M + mt];
@@ -2432,6 +2433,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         unsigned long long nchg = 0;
         const int rcap = (SR_RING - 1) * SR_MT_N - (SR_MT_N - 1);
         const int nround = (2 * M + SR_RNG_SLACK <= rcap) ? 1 : (M + TB - 1) / TB;
+        bool gown = false;   /* APR: this thread's own taxon was its own Gibbs step */
         for (int rd = 0; rd < nround; ++rd) {
         const int mlo = (nround == 1) ? 0 : rd * TB, mhi = (nround == 1) ? M : min(M, mlo + TB);
         if (rd > 0) __syncthreads();   /* every thread is done with the previous round's words */
@@ -2442,8 +2444,10 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           const uint32_t *Pm = P + m;
           const double ua = rng_peek(R, 2 * (m - mlo)) / 4294967296.0;
           const double ub = rng_peek(R, 2 * (m - mlo) + 1) / 4294967296.0;
-          const int a0 = APR ? ra_ : sab[m], b0 = APR ? rb_ : sab[M + m];
-          int t0 = APR ? rt0 : scnt[m], f0 = APR ? rf0 : scnt[M + m], t1 = APR ? rt1 : scnt[2 * M + m], f1 = APR ? rf1 : scnt[3 * M + m];
+          const bool own = APR && m == mt;   /* (rounds of TB taxa can map another half's taxa here) */
+          gown |= own;
+          const int a0 = own ? ra_ : sab[m], b0 = own ? rb_ : sab[M + m];
+          int t0 = own ? rt0 : scnt[m], f0 = own ? rf0 : scnt[M + m], t1 = own ? rt1 : scnt[2 * M + m], f1 = own ? rf1 : scnt[3 * M + m];
           /* a_m over [0, b_m], then b_m over the reversed column with limit N - a_new: one
              inlined copy of the draw, two trips */
           int na = a0, nb = b0;
@@ -2521,7 +2525,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             nchg += (na != a0) + (nb != b0);
             sab[m] = na; sab[M + m] = nb;
             scnt[m] = t0; scnt[M + m] = f0; scnt[2 * M + m] = t1; scnt[3 * M + m] = f1;
-            if constexpr (APR) { ra_ = na; rb_ = nb; rt0 = t0; rf0 = f0; rt1 = t1; rf1 = f1; }
+            if (own) { ra_ = na; rb_ = nb; rt0 = t0; rf0 = f0; rt1 = t1; rf1 = f1; }
             if (want_logl) {   /* mcmc_logl term (mcmc.c:643-644); manycd: the taxon's c, d (mcmc.c:641-642) */
               const double kcc = MCD ? cx[m] : K.cc, kd = MCD ? cv[M + m] : K.d, kdd = MCD ? cx[M + m] : K.dd,
                            kc = MCD ? cv[m] : K.c;
@@ -2532,6 +2536,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         }
         rng_skip(R, 2 * (mhi - mlo));
         }
+        if (APR && !gown) rstale = true;
         const int nw = wave_sum_i32((int)nchg);
         if (lane == 0 && nw) atomicAdd((unsigned long long *)&misc[MS_CAB], (unsigned long long)nw);
       }
@@ -2593,6 +2598,12 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
            proposal where its fields are read), vkr = Kn | r0 << 16 (pi3) */
         int vpk = 1 << 26, vkr = 0, vuw = 1, vnd = 0, voff = 0;
         int p0 = 0;
+        if constexpr (SP) {   /* the Gibbs step's rounds of TB taxa gave some of this half's taxa to other threads
+                                 (a half not starting at a multiple of TB): their limits and counts, read by the
+                                 owner threads below, are ordered by a barrier */
+          const bool multi = 2 * M + SR_RNG_SLACK > (SR_RING - 1) * SR_MT_N - (SR_MT_N - 1);
+          if (multi && (olo % TB) != 0 && (olo / TB + 1) * TB < ohi) __syncthreads();
+        }
         /* the lane-parallel proposal tables (ptab) hold "a proposal of each kind starting at word o"
            for the 128 words from stream position (tblk, toff); a later batch of the sweep reuses them
            while its proposals stay inside those words and no hard site moved (block-uniform state) */
@@ -2839,6 +2850,13 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           const bool one = NWM > 0 || SP || M <= TXS;   /* register-walk kernels: M <= TB (sr_regwalk); SP: halves <= TB */
           int a1 = 0, b1 = 0;
           const HM hb1 = hbc;
+          if (APR && rstale) {   /* (phase C's barriers order the other thread's Gibbs stores before these loads) */
+            if (mt < ohi) {
+              ra_ = sab[mt]; rb_ = sab[M + mt];
+              rt0 = scnt[mt]; rf0 = scnt[M + mt]; rt1 = scnt[2 * M + mt]; rf1 = scnt[3 * M + mt];
+            }
+            rstale = false;
+          }
           if (one && mt < ohi) { a1 = APR ? ra_ : sab[mt]; b1 = APR ? rb_ : sab[M + mt]; }
           FST(13);
 #if defined(SR_STAMP_DRAWS)

@@ -2847,7 +2847,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           int *pw = part + (bpar * 16) * NWV * 8;
           const bool pack = N < 512;   /* one taxon per thread: per-wave sums fit 16-bit fields */
           /* own taxon's limits and hard-site bits, fixed for the batch (one taxon per thread) */
-          const bool one = NWM > 0 || SP || M <= TXS;   /* register-walk kernels: M <= TB (sr_regwalk); SP: halves <= TB */
+          /* register-walk kernels: M <= TB (sr_regwalk); 1024-thread split halves hold <= TB taxa (compile-time) */
+          const bool one = NWM > 0 || (SP && TB == 1024) || (SP && ohi - olo <= TB) || M <= TXS;
           int a1 = 0, b1 = 0;
           const HM hb1 = hbc;
           if (APR && rstale) {   /* (phase C's barriers order the other thread's Gibbs stores before these loads) */
@@ -2971,9 +2972,9 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               x0s[sI] = 0; x1s[sI] = 0; ys[sI] = 0;
               if (prop_kind(sI) == PK_PI3) anyp3 |= sI >= p0 && sI < pend && !vetoed(sI);
             }
-            for (int m0 = wave * 64; m0 < M; m0 += TB) {
+            for (int m0 = (SP ? olo : 0) + wave * 64; m0 < (SP ? ohi : M); m0 += TB) {   /* SP: own taxa */
               const int m = m0 + lane;
-              const bool mv = m < M;
+              const bool mv = m < (SP ? ohi : M);
               const int a = mv ? sab[m] : 0, b = mv ? sab[M + m] : 0;
               const HM hb = (anyp3 && mv) ? hard_bits_col<HM>(P + m, M, hl, nh) : (HM)0;
 #pragma unroll
@@ -3446,7 +3447,8 @@ static sr_kfn sr_pick_kernel(int TB, int N, int M, bool gm, bool pr, int nh, boo
   }
   if (pr) return (TB == 1024 && !gm) ? (sr_kfn)sr_sweep_kernel<1024, 9, false, true> : nullptr;
 #ifndef SR_STAMPS
-  if (sp) return (TB == 1024 && gm) ? (sr_kfn)sr_sweep_kernel<1024, 0, true, false, true> : nullptr;
+  if (sp) return !gm ? nullptr : TB == 1024 ? (sr_kfn)sr_sweep_kernel<1024, 0, true, false, true>
+                 : TB == 512 ? (sr_kfn)sr_sweep_kernel<512, 0, true, false, true> : nullptr;
 #else
   if (sp) return nullptr;   /* (stamp builds index their counters by block) */
 #endif
@@ -3651,7 +3653,10 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
     const int want = e ? atoi(e) : -1;
     const int Mh = sr_sp_half(st->M);
     sr_kfn ks = sr_pick_kernel(TB, st->N, st->M, true, false, st->nh, true);
-    if (want != 0 && !d->mcd && d->gm && ks && Mh <= TB && st->M > 128 && (st->M > TB || want == 1)) {
+    /* SR_SPLIT=2 (experiment): halves of up to two blocks' taxa, several taxa per thread (512 threads:
+       256 VGPRs, 8 waves per CU) */
+    if (want != 0 && !d->mcd && d->gm && ks && (Mh <= TB || (want == 2 && TB == 512 && Mh <= 2 * TB)) && st->M > 128 &&
+        (st->M > TB || want >= 1)) {
       int cus = 0, occ = 0, coop = 0;
       const int grid = 16 * ((st->nchains + 7) / 8);
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&

@@ -29,7 +29,7 @@ for name, txt, seeds, bi, sc in cases:
     ok = True
     for k, sd in enumerate(seeds):
         o = oracle_ref.run_chain(txt, sd, bi, sc, maxs=0)
-        ok = ok and o["rc"] == 0 and np.array_equal(ri[k], o["rec_int"]) and \\
+        ok = ok and o["rc"] == 0 and np.array_equal(ri[k], o["rec_int"]) and \
             np.array_equal(rd[k].view(np.uint64), o["rec_dbl"].view(np.uint64)) and summ[k]["consistent"] == 0
     out[name] = {"kernel": kern, "chains": len(seeds), "calls": bi + sc, "match": bool(ok)}
 print(json.dumps(out))

@@ -153,6 +153,27 @@ def test_split_chain_parity(monkeypatch, name, N, M, nh):
     np.testing.assert_array_equal(np.array(counts["1"]), np.array(counts["0"]))
 
 
+@pytest.mark.parametrize("name,N,M,nh", [("m1100", 64, 1100, 6), ("many-hard", 60, 1500, 30)], ids=["split512-m1100",
+                                                                                                  "split512-many-hard"])
+def test_split_512_thread_halves_parity(monkeypatch, name, N, M, nh):
+    """The opt-in 512-thread split (SR_SPLIT=2: halves of up to 1024 taxa, several taxa per thread, 256 VGPRs)
+    equals the oracle, ragged halves and the Gibbs step's rounds of 512 taxa included."""
+    monkeypatch.setenv("SR_SPLIT", "2")
+    text = make_text(N, M, nh, seed=N * 1000 + M)
+    ds = sa.Dataset.parse(text, maxs=0)
+    seeds = [5, 13, 21]
+    with sa.Session(ds, seeds, block_threads=512, columns="hbm") as s:
+        assert s.variant == "hbm" and s.kernel == "split" and s.block_threads == 512
+    summ, (ri, rd) = sa.run_chains(ds, seeds, burnin_calls=2, sample_calls=3, keep_records=True, block_threads=512,
+                                   columns="hbm")
+    for k, s in enumerate(seeds):
+        o = oracle_ref.run_chain(text, s, 2, 3, maxs=0)
+        assert o["rc"] == 0
+        np.testing.assert_array_equal(ri[k], o["rec_int"], err_msg="%s seed %d" % (name, s))
+        assert np.array_equal(rd[k].view(np.uint64), o["rec_dbl"].view(np.uint64)), (name, s)
+        assert summ[k]["consistent"] == 0
+
+
 def test_checkpoint_resume_continues_exactly(tmp_path):
     """sr_session_checkpoint after 10 calls + sr_session_restore + 20 calls == 30 calls straight."""
     import os

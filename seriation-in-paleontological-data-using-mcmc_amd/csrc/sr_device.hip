@@ -90,37 +90,8 @@ struct KArgs {
 #ifndef SR_CK32
 #define SR_CK32 0
 #endif
-/* HBM-column kernels: window words per stored Gibbs checkpoint (1, or 2: half the checkpoint stream again;
-   pass 2 then splits the chosen pair from the words' own sums) */
-/* HBM-column kernels: pi2 / swap / pi3 reversals word-parallel (seg_reverse_gm, 1) or by the per-bit
-   exchange loop (0, the default: the word-parallel form is bit-exact but measured 0.9 % slower on config 5,
-   r04h -- 0.25 accepted reversals per sweep, and its registers add 45 VGPR spills to the split kernel);
-   SR_PFUSE: pi1's column prefix entries rewritten with the shifted words instead of a second pass */
-#ifndef SR_SEGREV
-#define SR_SEGREV 0
-#endif
-/* split chains: the own taxon's limits and counts also kept in registers across the launch (SR_APREG 1;
-   HBM stays the state every other reader sees) -- a load round trip fewer at the start of the Gibbs step,
-   of every proposal batch and of every accepted move's update */
-#ifndef SR_APREG
-#define SR_APREG 0
-#endif
-/* split chains: the per-sweep totals and per-batch proposal sums exchanged as {sequence, value} words that
-   the other half polls directly (SR_XTAG 1), instead of data, s_waitcnt, barrier, flag, poll, barrier, data
-   (xsync) -- two memory round trips and two barriers fewer per exchange */
-#ifndef SR_XTAG
-#define SR_XTAG 0
-#endif
-/* HBM-column Gibbs draws: passes 0 and 1 fused into one walk over the words (SR_FUSE01 1, draw_fast) */
-#ifndef SR_FUSE01
-#define SR_FUSE01 0
-#endif
-#ifndef SR_PFUSE
-#define SR_PFUSE 0
-#endif
-#ifndef SR_SEGCH
-#define SR_SEGCH 4   /* output words per round trip of seg_reverse_gm's second pass */
-#endif
+/* HBM-column kernels: window words per stored Gibbs checkpoint (pass 2 re-sums the chosen group's words in
+   one round trip; 4 measured fastest: 4.56 / 4.44 / 4.39 ms per config-5 launch at 1 / 2 / 4, r04e-r04f) */
 #ifndef SR_CKG
 #define SR_CKG 4
 #endif
@@ -203,10 +174,7 @@ __host__ __device__ static constexpr inline Lay sr_layout(int N, int M, int NW, 
  * slots per chain (ints): [2 parity][2 half][4] totals, [2 parity][2 half][16][4] proposal sums,
  * [2 parity][KT] exact-delta chunk counts. */
 __host__ __device__ static inline int sr_sp_half(int M) { return (((M + 1) / 2) + 63) & ~63; }
-/* + tagged slots (SR_XTAG, 8-byte aligned): [2 parity][2 half][4] totals and [2 parity][2 half][16][4] proposal
- * sums as {sequence, value} words, 272 u64 */
-__host__ __device__ static inline size_t sr_sp_xt0(int M) { return (16 + 256 + 2 * (size_t)((M + 63) / 64) + 1) & ~(size_t)1; }
-__host__ __device__ static inline size_t sr_sp_xb(int M) { return sr_sp_xt0(M) + 2 * 272; }
+__host__ __device__ static inline size_t sr_sp_xb(int M) { return 16 + 256 + 2 * (size_t)((M + 63) / 64); }
 /* per-chain HBM scratch of the gm variant (elements): pre u16, ck f64, lbuf f64, cbuf f64 */
 __host__ __device__ static inline size_t sr_gm_pre(int M, int NW) { return (size_t)(NW + 1) * M; }
 __host__ __device__ static inline size_t sr_gm_ck(int N, int M, int TB) { return (size_t)((N >> 5) + 1) * sr_ckstride(M, TB); }
@@ -825,71 +793,7 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, const uint16_t *pre
      word-start q of the window (qmx), and window words whose start q lies more than SR_QSPAN below it
      are dropped from the ends (their entries hold < 2^-(SR_QSPAN-75) of the mass each; ABS covers it). */
   int klo = nk, khi = -1, Oklo = 0;
-  double y0 = 1.0, S = 0.0;
-  bool uf = false, done01 = false;
-  if constexpr (B8 && SR_FUSE01) {
-    /* HBM columns: passes 0 and 1 in one walk over the words (one round trip per SR_WCH words instead of
-       two), the chain scaled by 2^q relative to entry o rather than the window's largest word-start q:
-       window words start at q > -SR_WIN_T - 32 |vA|, so y stays normal unless a later word rises ~1000
-       bits above o, which overflows S (S >= 2^1000 or NaN) and sends the draw to the two-pass form.  The
-       sum runs on past the window's last word (not known yet) but S is taken after it; a word start
-       with y < 2^-700 (a dip) followed by a window word flags the draw, as pass 1 does. */
-    int O = 0;
-    double y = 0.0, Sk = 0.0;
-    bool dip = false, started = false;
-    for (int k0 = 0; k0 < nk; k0 += SR_WCH) {
-      uint32_t wv[SR_WCH];
-#pragma unroll
-      for (int t = 0; t < SR_WCH; ++t) wv[t] = (k0 + t < nk) ? walk_word(Pm, M, N, NW, rev, k0 + t) : 0u;
-#pragma unroll
-      for (int t = 0; t < SR_WCH; ++t) {
-        const int k = k0 + t;
-        if (k < nk) {
-          const uint32_t ww = wv[t];
-          const int nb = min(32, L + 1 - 32 * k);
-          const uint32_t vm = (nb >= 32) ? 0xffffffffu : ((1u << nb) - 1u);
-          const int w0 = 32 * k;
-          const double qs = (w0 <= o) ? ((double)((o - w0) - (POo - O)) * vA + (double)(POo - O) * vB)
-                                      : -((double)((w0 - o) - (O - POo)) * vA + (double)(O - POo) * vB);
-          const double ub = qs - (double)(nb - __popc(ww & vm)) * vA;
-          const bool inw = ub > -SR_WIN_T;
-          if (inw && !started) { started = true; klo = k; Oklo = O; y = exp2_split(qs); y0 = y; }
-          if (started) {
-            dip |= y < 0x1p-700;
-            if (inw) { uf |= dip; khi = k; }
-            const int nfk = nb >> 3, c8 = nb & 7;
-            double2 t8[4];
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              const uint32_t e = (g < nfk) ? ((ww >> (8 * g)) & 255u) : 256u;
-              t8[g] = *reinterpret_cast<const double2 *>(T8 + 2 * e);
-            }
-            const double w23 = __builtin_fma(t8[2].y, t8[3].x, t8[2].x);
-            const double w13 = __builtin_fma(t8[1].y, w23, t8[1].x);
-            const double W = __builtin_fma(t8[0].y, w13, t8[0].x);
-            const double pw = (t8[0].y * t8[1].y) * (t8[2].y * t8[3].y);
-            S = __builtin_fma(y, W, S);
-            y = y * pw;
-            if (c8 > 0) {   /* only the walk's last word */
-              const uint32_t eb = (ww >> (8 * nfk)) & 255u;
-              const double2 tlo = t4sp(T4, min(c8, 4), eb & 15u);
-              const double shi = t4s(T4, max(c8 - 4, 0), eb >> 4);
-              S = __builtin_fma(y, tlo.x, S);
-              S = __builtin_fma(y * tlo.y, shi, S);
-            }
-            if (inw) Sk = S;
-            if ((k - klo) % SR_CKG == SR_CKG - 1) ck[(SR_CKG > 1 ? (k - klo) / SR_CKG : k) * ckstride] = S;
-          }
-          O += __popc(ww);
-        }
-      }
-    }
-    S = Sk;
-    done01 = started && S > 0.0 && S < 0x1p1000 && !uf;
-    if (!done01) { klo = nk; khi = -1; Oklo = 0; y0 = 1.0; S = 0.0; uf = false; }
-  }
   double qlo = 0.0, qmx = -__builtin_inf(), qmn = __builtin_inf();
-  if (!done01) {
   {
     int O = 0;   /* ones among walk entries [0, 32k) */
     for (int k0 = 0; k0 < nk; k0 += SR_WCH) {
@@ -957,7 +861,9 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, const uint16_t *pre
   /* pass 1: S over the window, checkpoints; the chain scaled by 2^-qmx.  A chain that falls below
      2^-700 at a word start inside the window (q dipping far below qmx and possibly rising again)
      would lose precision: that draw takes the exact path (uf). */
-  y0 = exp2_split(qlo - (klo <= khi ? qmx : 0.0));
+  const double y0 = exp2_split(qlo - (klo <= khi ? qmx : 0.0));
+  double S = 0.0;
+  bool uf = false;
   {
     double y = y0;
     for (int k0 = klo; k0 <= khi; k0 += SR_WCH) {
@@ -1012,7 +918,6 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, const uint16_t *pre
       }
     }
   }
-  }   /* (!done01) */
   GSTAMP(2);
   /* pass 2: locate the word; y at its start from its own sum (no replay of the chain): the word's
      partial sums are Sp0 + y gs1[g] with gs1 its unscaled group-end sums (y = 1 at the word start)
@@ -1713,99 +1618,6 @@ __device__ __forceinline__ uint32_t range_mask(int w, int lo, int hi)
   return (n == 32) ? 0xffffffffu : (((1u << n) - 1u) << (lo - b0));
 }
 
-/* the bits of x at the set positions of msk, packed from bit 0 (pext), and the inverse (pdep): msk is
-   block-uniform and has few runs (a word's positions in a segment, less its hard sites) */
-__device__ __forceinline__ uint32_t bits_pack(uint32_t x, uint32_t msk)
-{
-  uint32_t r = 0u;
-  int o = 0;
-  while (msk) {
-    const int s = __builtin_ctz(msk);
-    const uint32_t t = ~(msk >> s);
-    const int l = t ? __builtin_ctz(t) : 32 - s;
-    const uint32_t lm = (l == 32) ? 0xffffffffu : ((1u << l) - 1u);
-    r |= ((x >> s) & lm) << o;
-    o += l;
-    msk &= ~(lm << s);
-  }
-  return r;
-}
-__device__ __forceinline__ uint32_t bits_unpack(uint32_t v, uint32_t msk)
-{
-  uint32_t r = 0u;
-  int o = 0;
-  while (msk) {
-    const int s = __builtin_ctz(msk);
-    const uint32_t t = ~(msk >> s);
-    const int l = t ? __builtin_ctz(t) : 32 - s;
-    const uint32_t lm = (l == 32) ? 0xffffffffu : ((1u << l) - 1u);
-    r |= ((v >> o) & lm) << s;
-    o += l;
-    msk &= ~(lm << s);
-  }
-  return r;
-}
-
-/* HBM columns: reverse a column's bits at the positions of [i, j] -- all of them (pi2 / swap, mcmc.c:
-   1446-1474) or the non-hard ones (HARD: pi3, mcmc.c:1641-1670, hard sites stay) -- word-parallel, and
-   rewrite the column prefix entries (i/32, j/32].  The per-bit exchange loop costs one dependent memory
-   round trip per bit pair on HBM columns (~170 for a mean pi2 / pi3 reversal at 1024 sites); here the
-   selected bits are packed into the thread's scratch D (Kt bits, in the Gibbs checkpoint slots, idle in
-   this phase), and each output word takes its c bits as the bit-reversed 32-bit window of D ending at
-   Kt - off (off: the selected positions before the word): D' bit k = D bit Kt - 1 - k. */
-template <bool HARD>
-__device__ void seg_reverse_gm(uint32_t *Pm, uint16_t *prem, int M, int i, int j, const uint32_t *hbw,
-                               uint32_t *sc, int scs)
-{
-  const int wlo = i >> 5, whi = j >> 5;
-  auto msk_of = [&](int w) -> uint32_t { const uint32_t r = range_mask(w, i, j); return HARD ? (r & ~hbw[w]) : r; };
-  uint64_t acc = 0;
-  int fill = 0, dn = 0;
-  for (int w0 = wlo; w0 <= whi; w0 += 8) {
-    uint32_t wv[8];
-#pragma unroll
-    for (int t = 0; t < 8; ++t) wv[t] = (w0 + t <= whi) ? Pm[(w0 + t) * M] : 0u;
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      if (w0 + t <= whi) {
-        const uint32_t mk = msk_of(w0 + t);
-        acc |= (uint64_t)bits_pack(wv[t], mk) << fill;
-        fill += __popc(mk);
-        if (fill >= 32) { sc[dn * scs] = (uint32_t)acc; ++dn; acc >>= 32; fill -= 32; }
-      }
-    }
-  }
-  if (fill > 0) sc[dn * scs] = (uint32_t)acc;
-  const int Kt = 32 * dn + fill, dtop = (Kt - 1) >> 5;
-  int off = 0, sacc = prem[wlo * M];
-  for (int w0 = wlo; w0 <= whi; w0 += SR_SEGCH) {
-    uint32_t wv[SR_SEGCH], d0[SR_SEGCH], d1[SR_SEGCH], mks[SR_SEGCH];
-    int offs[SR_SEGCH];
-#pragma unroll
-    for (int t = 0; t < SR_SEGCH; ++t) {
-      const bool in = w0 + t <= whi;
-      mks[t] = in ? msk_of(w0 + t) : 0u;
-      offs[t] = off;
-      off += __popc(mks[t]);
-      const int q = (Kt - offs[t] - 32) >> 5;   /* (floor: the window may start below bit 0) */
-      wv[t] = in ? Pm[(w0 + t) * M] : 0u;
-      d0[t] = (in && q >= 0) ? sc[q * scs] : 0u;
-      d1[t] = (in && q + 1 >= 0 && q + 1 <= dtop) ? sc[(q + 1) * scs] : 0u;
-    }
-#pragma unroll
-    for (int t = 0; t < SR_SEGCH; ++t) {
-      const int w = w0 + t;
-      if (w <= whi) {
-        const int sh = (Kt - offs[t] - 32) & 31;
-        const uint32_t win = (uint32_t)((((uint64_t)d1[t] << 32) | d0[t]) >> sh);
-        const uint32_t nw = (wv[t] & ~mks[t]) | bits_unpack(__brev(win), mks[t]);
-        Pm[w * M] = nw;
-        if (w < whi) { sacc += __popc(nw); prem[(w + 1) * M] = (uint16_t)sacc; }
-      }
-    }
-  }
-}
-
 /* ones of column m in [lo, mid) and [mid, hi) (one pass over the words) */
 __device__ __forceinline__ void ones_split(const uint32_t *Pm, int M, int lo, int mid, int hi, int &O1, int &O2)
 {
@@ -2201,24 +2013,6 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   int *xb = SP ? A.xbuf + (size_t)chain * sr_sp_xb(M) : nullptr;
   int xseq = 0;
   bool xbroken = false;   /* thread 0: the other half missed a deadline once; stop waiting */
-  constexpr bool XTG = SP && SR_XTAG;
-  uint64_t *xt = XTG ? reinterpret_cast<uint64_t *>(xb + sr_sp_xt0(M)) : nullptr;
-  uint32_t tseq = 0;   /* tagged exchanges so far (block-uniform, the same sequence in both halves) */
-  auto tput = [&](uint64_t *q, int v) { xst(q, ((uint64_t)tseq << 32) | (uint64_t)(uint32_t)v); };
-  /* the other half's four tagged values of this exchange (bounded poll, as xsync's) */
-  auto tget4 = [&](const uint64_t *q, int &v0, int &v1, int &v2, int &v3) {
-    int n = 0;
-    while (true) {
-      const uint64_t w0 = xld(q), w1 = xld(q + 1), w2 = xld(q + 2), w3 = xld(q + 3);
-      if (xbroken || ((uint32_t)(w0 >> 32) == tseq && (uint32_t)(w1 >> 32) == tseq && (uint32_t)(w2 >> 32) == tseq &&
-                      (uint32_t)(w3 >> 32) == tseq)) {
-        v0 = (int)(uint32_t)w0; v1 = (int)(uint32_t)w1; v2 = (int)(uint32_t)w2; v3 = (int)(uint32_t)w3;
-        return;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      if (++n > (1 << 22)) { xbroken = true; xst(A.xerr, 1); }
-    }
-  };
   /* both halves' exchange writes done and visible: each thread's stores acknowledged, the block's
      flag raised, the other half's flag awaited (bounded: a half that never arrives -- not
      co-resident -- sets xerr and the launch completes with garbage the host refuses) */
@@ -2306,13 +2100,6 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   const UDivM mdH = make_udivm((uint32_t)N - nhard > 0 ? (uint32_t)N - nhard : 1u);
   const UDivM mdH1 = make_udivm((uint32_t)N - nhard > 1 ? (uint32_t)N - nhard - 1 : 1u);
   STAMP_DECL
-  constexpr bool APR = SP && SR_APREG;   /* (one taxon per thread in phases A and C: m == mt) */
-  int ra_ = 0, rb_ = 0, rt0 = 0, rf0 = 0, rt1 = 0, rf1 = 0;
-  bool rstale = false;   /* the Gibbs step's rounds gave the own taxon to another thread: reload in phase C */
-  if (APR && mt < ohi) {
-    ra_ = sab[mt]; rb_ = sab[M + mt];
-    rt0 = scnt[mt]; rf0 = scnt[M + mt]; rt1 = scnt[2 * M + mt]; rf1 = scnt[3 * M + mt];
-  }
 
   for (int call = 0; call < A.calls; ++call) {
     for (int sw = 0; sw < A.spc; ++sw) {
@@ -2320,9 +2107,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       /* ============ phase A: totals and the c, d draws (mcmc.c:768-825) */
       {
         int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-        if constexpr (APR) { if (mt < ohi) { s0 = rt0; s1 = rf0; s2 = rt1; s3 = rf1; } }
-        else
-          for (int m = olo + tid; m < ohi; m += TB) { s0 += scnt[m]; s1 += scnt[M + m]; s2 += scnt[2 * M + m]; s3 += scnt[3 * M + m]; }
+        for (int m = olo + tid; m < ohi; m += TB) { s0 += scnt[m]; s1 += scnt[M + m]; s2 += scnt[2 * M + m]; s3 += scnt[3 * M + m]; }
         s0 = wave_sum_i32(s0); s1 = wave_sum_i32(s1); s2 = wave_sum_i32(s2); s3 = wave_sum_i32(s3);
         int *tw = tot + (par * NWV + wave) * 4;
         if (lane == 0) { tw[0] = s0; tw[1] = s1; tw[2] = s2; tw[3] = s3; }
@@ -2338,14 +2123,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           const int *tw = tot + (par * NWV + w) * 4;
           s0 += tw[0]; s1 += tw[1]; s2 += tw[2]; s3 += tw[3];
         }
-        if constexpr (XTG) {   /* + the other half's totals (tagged) */
-          ++tseq;
-          uint64_t *xq = xt + par * 8;
-          if (tid == 0) { tput(xq + 4 * half, s0); tput(xq + 4 * half + 1, s1); tput(xq + 4 * half + 2, s2); tput(xq + 4 * half + 3, s3); }
-          int o0, o1, o2, o3;
-          tget4(xq + 4 * (half ^ 1), o0, o1, o2, o3);
-          s0 += o0; s1 += o1; s2 += o2; s3 += o3;
-        } else if constexpr (SP) {   /* + the other half's totals */
+        if constexpr (SP) {   /* + the other half's totals */
           int *xt = xb + par * 8;
           if (tid == 0) { xst(xt + 4 * half, s0); xst(xt + 4 * half + 1, s1); xst(xt + 4 * half + 2, s2); xst(xt + 4 * half + 3, s3); }
           xsync();
@@ -2433,7 +2211,6 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         unsigned long long nchg = 0;
         const int rcap = (SR_RING - 1) * SR_MT_N - (SR_MT_N - 1);
         const int nround = (2 * M + SR_RNG_SLACK <= rcap) ? 1 : (M + TB - 1) / TB;
-        bool gown = false;   /* APR: this thread's own taxon was its own Gibbs step */
         for (int rd = 0; rd < nround; ++rd) {
         const int mlo = (nround == 1) ? 0 : rd * TB, mhi = (nround == 1) ? M : min(M, mlo + TB);
         if (rd > 0) __syncthreads();   /* every thread is done with the previous round's words */
@@ -2444,10 +2221,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           const uint32_t *Pm = P + m;
           const double ua = rng_peek(R, 2 * (m - mlo)) / 4294967296.0;
           const double ub = rng_peek(R, 2 * (m - mlo) + 1) / 4294967296.0;
-          const bool own = APR && m == mt;   /* (rounds of TB taxa can map another half's taxa here) */
-          gown |= own;
-          const int a0 = own ? ra_ : sab[m], b0 = own ? rb_ : sab[M + m];
-          int t0 = own ? rt0 : scnt[m], f0 = own ? rf0 : scnt[M + m], t1 = own ? rt1 : scnt[2 * M + m], f1 = own ? rf1 : scnt[3 * M + m];
+          const int a0 = sab[m], b0 = sab[M + m];
+          int t0 = scnt[m], f0 = scnt[M + m], t1 = scnt[2 * M + m], f1 = scnt[3 * M + m];
           /* a_m over [0, b_m], then b_m over the reversed column with limit N - a_new: one
              inlined copy of the draw, two trips */
           int na = a0, nb = b0;
@@ -2525,7 +2300,6 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             nchg += (na != a0) + (nb != b0);
             sab[m] = na; sab[M + m] = nb;
             scnt[m] = t0; scnt[M + m] = f0; scnt[2 * M + m] = t1; scnt[3 * M + m] = f1;
-            if (own) { ra_ = na; rb_ = nb; rt0 = t0; rf0 = f0; rt1 = t1; rf1 = f1; }
             if (want_logl) {   /* mcmc_logl term (mcmc.c:643-644); manycd: the taxon's c, d (mcmc.c:641-642) */
               const double kcc = MCD ? cx[m] : K.cc, kd = MCD ? cv[M + m] : K.d, kdd = MCD ? cx[M + m] : K.dd,
                            kc = MCD ? cv[m] : K.c;
@@ -2536,7 +2310,6 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         }
         rng_skip(R, 2 * (mhi - mlo));
         }
-        if (APR && !gown) rstale = true;
         const int nw = wave_sum_i32((int)nchg);
         if (lane == 0 && nw) atomicAdd((unsigned long long *)&misc[MS_CAB], (unsigned long long)nw);
       }
@@ -2851,14 +2624,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           const bool one = NWM > 0 || (SP && TB == 1024) || (SP && ohi - olo <= TB) || M <= TXS;
           int a1 = 0, b1 = 0;
           const HM hb1 = hbc;
-          if (APR && rstale) {   /* (phase C's barriers order the other thread's Gibbs stores before these loads) */
-            if (mt < ohi) {
-              ra_ = sab[mt]; rb_ = sab[M + mt];
-              rt0 = scnt[mt]; rf0 = scnt[M + mt]; rt1 = scnt[2 * M + mt]; rf1 = scnt[3 * M + mt];
-            }
-            rstale = false;
-          }
-          if (one && mt < ohi) { a1 = APR ? ra_ : sab[mt]; b1 = APR ? rb_ : sab[M + mt]; }
+          if (one && mt < ohi) { a1 = sab[mt]; b1 = sab[M + mt]; }
           FST(13);
 #if defined(SR_STAMP_DRAWS)
           STAMP(5);
@@ -3003,22 +2769,16 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           FST(4);
           __syncthreads();
           if constexpr (SP) {   /* this half's sums of the batch's proposals (lane p of wave 0), exchanged */
-            if constexpr (XTG) ++tseq;
             if (wave == 0 && lane >= p0 && lane < pend && lane < 16 && !((vpk >> 26) & 1)) {
               int X0 = 0, X1 = 0, Y0 = 0, Y1 = 0;
               for (int w = 0; w < NWV; ++w) {
                 const int *o = pw + (lane * NWV + w) * 8;
                 X0 += o[0]; X1 += o[1]; Y0 += o[2]; Y1 += o[3];
               }
-              if constexpr (XTG) {
-                uint64_t *xq = xt + 16 + ((bpar * 2 + half) * 16 + lane) * 4;
-                tput(xq, X0); tput(xq + 1, X1); tput(xq + 2, Y0); tput(xq + 3, Y1);
-              } else {
-                int *xp = xb + 16 + ((bpar * 2 + half) * 16 + lane) * 4;
-                xst(xp, X0); xst(xp + 1, X1); xst(xp + 2, Y0); xst(xp + 3, Y1);
-              }
+              int *xp = xb + 16 + ((bpar * 2 + half) * 16 + lane) * 4;
+              xst(xp, X0); xst(xp + 1, X1); xst(xp + 2, Y0); xst(xp + 3, Y1);
             }
-            if constexpr (!XTG) xsync();
+            xsync();
           }
           STAMP_E(5);
           FST(5);
@@ -3045,11 +2805,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                   const int *o = pw + (p * NWV + w) * 8;
                   X0 += o[0]; X1 += o[1]; Y0 += o[2]; Y1 += o[3];
                 }
-                if constexpr (XTG) {   /* + the other half's (tagged: polled here) */
-                  int o0, o1, o2, o3;
-                  tget4(xt + 16 + ((bpar * 2 + (half ^ 1)) * 16 + p) * 4, o0, o1, o2, o3);
-                  X0 += o0; X1 += o1; Y0 += o2; Y1 += o3;
-                } else if constexpr (SP) {   /* + the other half's */
+                if constexpr (SP) {   /* + the other half's */
                   const int *yp = xb + 16 + ((bpar * 2 + (half ^ 1)) * 16 + p) * 4;
                   X0 += xld(yp); X1 += xld(yp + 1); Y0 += xld(yp + 2); Y1 += xld(yp + 3);
                 }
@@ -3148,20 +2904,13 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           if (tid == 0) misc[MS_ACC + (kind == PK_PI1 ? 3 : kind == PK_PI2 ? 4 : kind == PK_SWAP ? 5 : 6)]++;
           loglik += delta;
           const int16_t *nhp = nhall + q.r0;   /* pi3: the non-hard positions of [i, j] in order */
-          constexpr bool GMX = GM && SR_PFUSE;    /* HBM columns: pi1's prefix entries with the shifted words */
-          constexpr bool GMR = GM && SR_SEGREV;   /* HBM columns: word-parallel reversals (prefix with the words) */
           for (int m = (PR && hf) ? M : olo + tx; m < ohi; m += TXS) {   /* PR: the even lane of each pair; SP: own taxa */
             uint32_t *Pm = P + m;
-            const int a = APR ? ra_ : sab[m], b = APR ? rb_ : sab[M + m];
+            const int a = sab[m], b = sab[M + m];
             int dt0, dt1;
             taxon_dt(kind, q, a, b, Pm, pre + m, M, kind == PK_PI3 ? hard_bits_col<HM>(Pm, M, hl, nh) : (HM)0, hcnt, nhall, dt0, dt1,
                      hbx);
-            if constexpr (APR) {
-              rt0 += dt0; rf0 -= dt0; rt1 += dt1; rf1 -= dt1;
-              scnt[m] = rt0; scnt[M + m] = rf0; scnt[2 * M + m] = rt1; scnt[3 * M + m] = rf1;
-            } else {
-              scnt[m] += dt0; scnt[M + m] -= dt0; scnt[2 * M + m] += dt1; scnt[3 * M + m] -= dt1;
-            }
+            scnt[m] += dt0; scnt[M + m] -= dt0; scnt[2 * M + m] += dt1; scnt[3 * M + m] -= dt1;
             int na_ = a, nb_ = b;   /* HBM columns: the new limits, stored below when they change */
             auto set_a = [&](int v) { if constexpr (GM) na_ = v; else sab[m] = v; };
             auto set_b = [&](int v) { if constexpr (GM) nb_ = v; else sab[M + m] = v; };
@@ -3172,7 +2921,6 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 if (ii < a && a <= jj + 1) set_a(a - 1);
                 if (ii < b && b <= jj + 1) set_b(b - 1);
                 const uint32_t vb = (Pm[(i >> 5) * M] >> (i & 31)) & 1u;
-                int sacc = GMX ? (int)pre[(i >> 5) * M + m] : 0;   /* (HBM columns: prefix entries (i/32, j/32] here) */
                 for (int w0 = i >> 5; w0 <= (j >> 5); w0 += 8) {
                   uint32_t wv[9];
 #pragma unroll
@@ -3187,7 +2935,6 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                       uint32_t nw = (old & ~m1) | (sh & m1);
                       if ((j >> 5) == w) nw = (nw & ~(1u << (j & 31))) | (vb << (j & 31));
                       Pm[w * M] = nw;
-                      if (GMX && w < (j >> 5)) { sacc += __popc(nw); pre[(w + 1) * M + m] = (uint16_t)sacc; }
                     }
                   }
                 }
@@ -3195,7 +2942,6 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 if (ii <= a && a <= jj) set_a(a + 1);
                 if (ii <= b && b <= jj) set_b(b + 1);
                 const uint32_t vb = (Pm[(i >> 5) * M] >> (i & 31)) & 1u;
-                int sacc = GMX ? (int)pre[((i >> 5) + 1) * M + m] : 0;   /* (entry i/32 + 1 does not change) */
                 for (int w0 = i >> 5; w0 >= (j >> 5); w0 -= 8) {
                   uint32_t wv[9];   /* wv[t] = word w0 - t */
 #pragma unroll
@@ -3210,7 +2956,6 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                       uint32_t nw = (old & ~m1) | (sh & m1);
                       if ((j >> 5) == w) nw = (nw & ~(1u << (j & 31))) | (vb << (j & 31));
                       Pm[w * M] = nw;
-                      if (GMX && w > (j >> 5)) { sacc -= __popc(nw); pre[w * M + m] = (uint16_t)sacc; }
                     }
                   }
                 }
@@ -3221,11 +2966,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               if (ain && !bin) set_a(i + j + 1 - a);
               else if (!ain && bin) set_b(i + j + 1 - b);
               else if (ain && bin) { set_b(i + j + 1 - a); set_a(i + j + 1 - b); }
-              if constexpr (GMR) {
-                uint32_t *sc = reinterpret_cast<uint32_t *>(ckb + ckslot);
-                if (kind != PK_PI3) seg_reverse_gm<false>(Pm, pre + m, M, i, j, hbw, sc, CKS * (int)(sizeof(CKT) / 4));
-                else seg_reverse_gm<true>(Pm, pre + m, M, i, j, hbw, sc, CKS * (int)(sizeof(CKT) / 4));
-              } else if (kind != PK_PI3) {
+              if (kind != PK_PI3) {
                 for (int n = i; n < i + j - n; ++n) {
                   const int p2 = i + j - n;
                   const uint32_t b1 = (Pm[(n >> 5) * M] >> (n & 31)) & 1u, b2 = (Pm[(p2 >> 5) * M] >> (p2 & 31)) & 1u;
@@ -3242,10 +2983,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             if constexpr (GM) {
               if (na_ != a) sab[m] = na_;
               if (nb_ != b) sab[M + m] = nb_;
-              if constexpr (APR) { ra_ = na_; rb_ = nb_; }
             }
-            if (kind == PK_PI1 ? !GMX : !GMR) {   /* the move permutes positions [lo, hi] only: prefix entries (lo/32, hi/32] change
-                            (HBM columns: rewritten with the words above) */
+            {   /* the move permutes positions [lo, hi] only: prefix entries (lo/32, hi/32] change */
               const int lo = min(i, j), hi = max(i, j), rlo = (lo >> 5) + 1, rhi = hi >> 5;
               uint16_t *prem = pre + m;
               int sacc = prem[(rlo - 1) * M];
@@ -3746,8 +3485,6 @@ extern "C" int srk_run(srk_dev *d, int calls, int spc, int save, int rec_base)
   A.calls = calls; A.spc = spc; A.save = save; A.rec_base = rec_base;
   sr_kfn k = sr_pick_kernel(d->TB, d->N, d->M, d->gm != 0, d->pr != 0, d->nh, d->sp != 0, d->mcd != 0);
   if (d->sp) HIPCHK(hipMemsetAsync(A.xflag, 0, (size_t)d->nchains * 2 * sizeof(int), d->stream));   /* exchange sequence restarts */
-  if (d->sp && SR_XTAG)   /* (and the tagged slots' sequence) */
-    HIPCHK(hipMemsetAsync(A.xbuf, 0, (size_t)d->nchains * sr_sp_xb(d->M) * sizeof(int), d->stream));
   if (d->have_events) HIPCHK(hipEventRecord(d->ev0, d->stream));
   if (d->jit) {   /* the run-time specialised kernel (same arguments; LDS columns: one workgroup per chain) */
     void *kp[] = {&A};

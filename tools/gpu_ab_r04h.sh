@@ -1,4 +1,5 @@
 #!/bin/bash
+# (historical recipe: the switches it compares were removed from the kernel source at 289d1cb after this A/B)
 # Round-4 config-5 A/B of the word-parallel reversals (seg_reverse_gm) and the prefix rewritten with the
 # moved words: the product vs noseg (SR_SEGREV=0: per-bit exchange loop + prefix pass), after the product's
 # parity on every HBM-column / split / manycd case.   tools/gpu_ab_r04h.sh OUT

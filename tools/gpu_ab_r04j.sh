@@ -1,4 +1,5 @@
 #!/bin/bash
+# (historical recipe: the switches it compares were removed from the kernel source at 289d1cb after this A/B)
 # Round-4 config-5 A/B of the split kernel's register-resident own-taxon state (SR_APREG), tagged exchanges
 # (SR_XTAG) and fused Gibbs passes 0/1 (SR_FUSE01): product vs apreg, xtag, xtap (both), fuse, fuap (fuse +
 # apreg); parity of fuap, fuse and xtap on the HBM-column / split cases first.   tools/gpu_ab_r04j.sh OUT

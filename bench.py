@@ -160,11 +160,15 @@ def main():
                     "(SR_F_RNG_PHILOX; not the reference's, so never the headline line)")
     ap.add_argument("--generic", action="store_true", help="the generic kernel (shape from the launch "
                     "arguments) instead of the default one compiled for the dataset's shape (SR_F_GENERIC_KERNEL)")
-    ap.add_argument("--parity-chains", type=int, default=2, help="after the timed region, rerun this many of the "
-                    "selected chains on the CPU oracle (burn-in = the warm-up calls) and require every saved record "
-                    "of the timed region to match bit for bit (0: skip)")
-    ap.add_argument("--parity-calls", type=int, default=0, help="compare only the first K saved records of each "
-                    "checked chain (0: all; the HBM-column workloads take minutes per chain on the CPU)")
+    ap.add_argument("--parity-chains", type=int, default=CHAINS_SELECTED, help="after the timed region, rerun this many "
+                    "of the selected chains plus --parity-rejected chains the selection rejected on the CPU oracle "
+                    "(burn-in = the warm-up calls) and require every compared saved record of the timed region to match "
+                    "bit for bit (0: skip)")
+    ap.add_argument("--parity-rejected", type=int, default=2, help="chains the one-sigma selection rejected that the "
+                    "parity leg also checks (the first and the last of rank 0's shard that were not selected)")
+    ap.add_argument("--parity-calls", type=int, default=-1, help="compare only the first K saved records of each "
+                    "checked chain (0: all; -1 auto: all for LDS-column sessions, 4 for HBM columns, whose oracle "
+                    "takes ~0.4 s per call)")
     ap.add_argument("--device-of-rank", default="", help="comma-separated HIP ordinal per local rank (default: the "
                     "local rank), e.g. 0,0 to rehearse two ranks on one GPU")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"), help="torch.distributed backend under "
@@ -176,7 +180,12 @@ def main():
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # one process per GPU: launch the ranks as children (this process has not touched the
-        # GPU and never will) and exit with their status
+        # GPU and never will) and exit with their status.  Counting devices does not initialise the GPU.
+        import torch
+        need = max(int(x) for x in args.device_of_rank.split(",")) + 1 if args.device_of_rank else args.gpus
+        have = torch.cuda.device_count()
+        if have < need:
+            raise SystemExit("bench.py: --gpus %d needs %d visible GPU(s), %d visible" % (args.gpus, need, have))
         return launch_ranks(args.gpus)
 
     rank = int(os.environ.get("RANK", "0"))
@@ -246,10 +255,6 @@ def main():
     for _ in range(args.warmup):
         sess.run(cps, save=False)
     sess.reset_records()
-    # pinned host workspace for the selected chains' records (allocated before the timed region)
-    nrec_ws = args.steps * cps if not args.no_save else 1
-    pin_ab = torch.empty((CHAINS_SELECTED, nrec_ws, 2 * ds.M + ds.N), dtype=torch.int16, pin_memory=True).numpy()
-    pin_cd = torch.empty((CHAINS_SELECTED, nrec_ws, 3), dtype=torch.float64, pin_memory=True).numpy()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -275,28 +280,22 @@ def main():
     else:
         gathered = rows
     selected = sd.select_chains(gathered, CHAINS_SELECTED)
-    mine = [c for c in selected if c in set(chain_ids)]
     t_sel = time.perf_counter()
     W = 2 * ds.M + ds.N
-    if len(mine) <= pin_ab.shape[0]:   # straight into the pinned workspace (one DMA copy per chain)
-        loc_ab, loc_cd = pin_ab[:len(mine)], pin_cd[:len(mine)]
-        for k, c in enumerate(mine):
-            sess.fetch_chain_records(chain_ids.index(c), out=(loc_ab[k], loc_cd[k]))
-    else:
-        loc = [sess.fetch_chain_records(chain_ids.index(c)) for c in mine]
-        loc_ab, loc_cd = np.stack([a for a, _ in loc]), np.stack([c for _, c in loc])
-    t_fetch = time.perf_counter()
-    if dist:
-        sel_ab, sel_cdl = sd.gather_selected_records(selected, C * world, mine, loc_ab, loc_cd, device=coll_dev)
-    else:
-        sel_ab, sel_cdl = loc_ab, loc_cd
+    # the selected chains' records: device-to-device copies out of the session's record buffer on this stream,
+    # then (N > 1) one all-gather per array over RCCL -- they never leave HBM inside the timed region
+    dev_ab, dev_cd = sd.gather_selected_records_device(
+        selected, C * world, chain_ids, lambda j, pa, pc: sess.copy_chain_records(j, pa, pc, count=nrec), nrec, W,
+        device=torch.device("cuda", device))
+    t_fetch = t_sel
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     tail_ms = (time.perf_counter() - t_kernels) * 1e3
     tail_parts = {"summaries_ms": (t_summ - t_kernels) * 1e3, "gather_select_ms": (t_sel - t_summ) * 1e3,
-                  "fetch_selected_ms": (t_fetch - t_sel) * 1e3, "gather_records_ms": (time.perf_counter() - t_fetch) * 1e3}
+                  "copy_gather_records_ms": (time.perf_counter() - t_fetch) * 1e3}
+    sel_ab, sel_cdl = dev_ab.cpu().numpy(), dev_cd.cpu().numpy()   # (host copies for the statistics: untimed)
     # posterior statistics of the selected chains (script.py:100-152), outside the timed region
     ec, ed, corr = sd.selection_statistics(sel_ab, sel_cdl, ds.N, ds.M, CHAINS_SELECTED)
     if dist:
@@ -375,9 +374,9 @@ def main():
         "cpu_baseline": cpu,
         "cpu_baseline_O0": cpu_o0,
         "timing": {"kernel_ms_per_step": kernel_ms, "gather_select_ms": tail_ms, "tail_parts": tail_parts,
-                   "note": "gather_select_ms: after the last kernel, the record fetch, summary all-gather, "
-                           "one-sigma selection and the gather of the selected chains' records (inside the "
-                           "timed region)"},
+                   "note": "gather_select_ms: after the last kernel, the per-chain summaries (exp_data kernel), "
+                           "their all-gather, the one-sigma selection, and the selected chains' records copied "
+                           "device to device and all-gathered on the device (inside the timed region)"},
         "selection": {"chains_selected": selected, "exp_c": ec, "exp_d": ed, "corr_mn": corr,
                       "samples_per_chain": nrec,
                       "records_sha256": hashlib.sha256(np.ascontiguousarray(sel_ab).tobytes() +
@@ -385,19 +384,42 @@ def main():
                       "note": "script.py:70-152 over every timed step's saved samples of the selected chains (the "
                               "reference divides by 1000: exact means at --steps 20 x 50 calls = 1000 samples)"},
     }
+    # parity leg inputs (outside the timed region, rank 0): besides the selected chains, chains the selection
+    # rejected -- the first and the last of this rank's shard that were not selected -- so the check does not
+    # sample only the best-loglik chains the records under test chose
+    want_parity = rank == 0 and args.parity_chains > 0 and not args.no_save and args.rng == "mt"
+    rej, rej_ab, rej_cd = [], None, None
+    if want_parity and args.parity_rejected > 0:
+        pool = [c for c in chain_ids if c not in set(selected)]
+        pick = pool[:1] + pool[1:][-1:] if args.parity_rejected >= 2 else pool[:1]
+        pick += [c for c in pool if c not in pick][:max(0, args.parity_rejected - len(pick))]
+        rej = sorted(pick)
+        rr = [sess.fetch_chain_records(chain_ids.index(c), count=nrec) for c in rej]
+        if rr:
+            rej_ab, rej_cd = np.stack([a for a, _ in rr]), np.stack([c for _, c in rr])
+    variant = sess.variant
     sess.close()
     if dist:   # (the ranks leave together; rank 0's CPU parity leg below runs after the process group is gone)
         dist.destroy_process_group()
-    # parity leg (after the timed region, rank 0): the CPU oracle reruns some selected chains and every saved
-    # record of the timed region must match bit for bit (tests/bench_parity.py; the checker, not measured)
+    # parity leg (after the timed region, rank 0): the CPU oracle reruns the checked chains and every compared
+    # saved record of the timed region must match bit for bit (tests/bench_parity.py; the checker, not measured)
     parity = None
-    if rank == 0 and args.parity_chains > 0 and not args.no_save and args.rng == "mt":
+    if want_parity:
         import bench_parity
         with open(args.dataset, "rb") as fh:
             text = fh.read()
         k = min(args.parity_chains, len(selected))
-        parity = bench_parity.check_selected(text, selected[:k], [c + 1 for c in selected[:k]], args.warmup * cps,
-                                             sel_ab[:k], sel_cdl[:k], calls=args.parity_calls or None)
+        chk = list(selected[:k]) + rej
+        ab = np.concatenate([sel_ab[:k]] + ([rej_ab] if rej else []))
+        cd = np.concatenate([sel_cdl[:k]] + ([rej_cd] if rej else []))
+        pc = args.parity_calls if args.parity_calls >= 0 else (0 if variant == "lds" else 4)
+        parity = bench_parity.check_selected(text, chk, [c + 1 for c in chk], args.warmup * cps, ab, cd,
+                                             calls=pc or None)
+        parity["selected_checked"] = [int(c) for c in selected[:k]]
+        parity["rejected_checked"] = [int(c) for c in rej]
+        if pc:
+            parity["calls_bound"] = ("--parity-calls %d" % pc if args.parity_calls > 0 else
+                                     "auto: HBM-column session, the oracle takes ~0.4 s per call at this size")
     out["parity"] = parity
     if rank == 0:
         print(json.dumps(out), flush=True)

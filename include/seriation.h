@@ -106,6 +106,16 @@ typedef int (*sr_sample_sink_fn)(void *ctx, int32_t chain_index, int32_t sample_
 
 void sr_default_opts(sr_run_opts *o);
 
+/* gsl_rng_env_setup (mcmc_init, mcmc.c:591-592; GSL 2.6 rng/env.c) for callers that take the seed from the
+ * environment as the reference CLI does: GSL_RNG_TYPE unset or "mt19937" -> SR_OK (verbose: the line
+ * "GSL_RNG_TYPE=mt19937" when set), then GSL_RNG_SEED (strtoul base 0, unset -> 0 = GSL's default 4357;
+ * verbose: "GSL_RNG_SEED=<value>") into *seed.  Another GSL generator -> SR_EUNSUPPORTED (the sampler
+ * implements MT19937's stream only), a name GSL does not know -> SR_EINVAL (verbose: GSL's "not recognized"
+ * message and list of generator types).  Every session / run entry point applies the same GSL_RNG_TYPE
+ * check (silently) and refuses with the same codes, so no run samples MT19937 where the environment named
+ * another generator. */
+int sr_rng_env_setup(uint64_t *seed, int32_t verbose);
+
 /* Run n_chains independent chains on one GPU (opts->device), burn-in then sampling;
  * per-sample records go to sink (may be NULL); out[n_chains] receives the summaries. */
 int sr_run_chains(const sr_dataset *ds, const sr_chain_spec *specs, int32_t n_chains,
@@ -148,6 +158,11 @@ int sr_session_reset_records(sr_session *s);
    (either may be NULL). */
 int sr_session_fetch_chain_records(sr_session *s, int32_t chain, int32_t first, int32_t count, int16_t *ab_pi,
                                    double *cdl);
+/* The same rows copied device to device into caller-owned memory on the session's GPU (dev_ab_pi [count][2M+N]
+   int16, dev_cdl [count][3]; either may be NULL), queued on the session stream without waiting: the records
+   never leave HBM (e.g. straight into the buffer of an RCCL all-gather on that stream). */
+int sr_session_copy_chain_records(sr_session *s, int32_t chain, int32_t first, int32_t count, int16_t *dev_ab_pi,
+                                  double *dev_cdl);
 /* manycd sessions: the per-taxon c, d of buffered records [first, first + count): cdv [n_chains][count][2M]
    (c[M] then d[M], log values as mcmc_save_chain exponentiates them); SR_EINVAL for manycd = 0 sessions. */
 int sr_session_fetch_cd_vectors(sr_session *s, int32_t first, int32_t count, double *cdv);

@@ -29,6 +29,8 @@
 #define OM_GSL_H
 #include <stdint.h>
 #include <stddef.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <math.h>
 #include "om_libm.h"
@@ -84,6 +86,49 @@ static inline void om_rng_seed(om_rng *r, unsigned long s)
   r->mti = OM_MT_N;
   r->ndraw = 0;
   r->philox = 0;
+}
+
+/* gsl_rng_env_setup (GSL 2.6 rng/env.c; called by mcmc_init, mcmc.c:591-592): GSL_RNG_TYPE names the
+   generator among gsl_rng_types_setup's list (rng/types.c order), "GSL_RNG_TYPE=<name>" on stderr when set;
+   GSL_RNG_SEED (strtoul base 0) and "GSL_RNG_SEED=<value>" after it.  Returns 0 for mt19937 (unset or named),
+   1 for another GSL generator (GSL would run it; the oracle has only mt19937 and refuses, as the product does),
+   2 for a name GSL does not know (GSL prints the list and aborts through gsl_error; here: the list, then 2). */
+static const char *const om_gsl_rng_names[] = {
+    "borosh13", "cmrg", "coveyou", "fishman18", "fishman20", "fishman2x", "gfsr4", "knuthran", "knuthran2",
+    "knuthran2002", "lecuyer21", "minstd", "mrg", "mt19937", "mt19937_1999", "mt19937_1998", "r250", "ran0", "ran1",
+    "ran2", "ran3", "rand", "rand48", "random128-bsd", "random128-glibc2", "random128-libc5", "random256-bsd",
+    "random256-glibc2", "random256-libc5", "random32-bsd", "random32-glibc2", "random32-libc5", "random64-bsd",
+    "random64-glibc2", "random64-libc5", "random8-bsd", "random8-glibc2", "random8-libc5", "random-bsd",
+    "random-glibc2", "random-libc5", "randu", "ranf", "ranlux", "ranlux389", "ranlxd1", "ranlxd2", "ranlxs0",
+    "ranlxs1", "ranlxs2", "ranmar", "slatec", "taus", "taus2", "taus113", "transputer", "tt800", "uni", "uni32",
+    "vax", "waterman14", "zuf", 0};
+
+static inline int om_rng_env_setup(unsigned long *seed)
+{
+  const char *p = getenv("GSL_RNG_TYPE");
+  *seed = 0;
+  if (p) {
+    int known = 0;
+    for (int k = 0; om_gsl_rng_names[k]; k++) known |= strcmp(p, om_gsl_rng_names[k]) == 0;
+    if (!known) {
+      fprintf(stderr, "GSL_RNG_TYPE=%s not recognized\n", p);
+      fprintf(stderr, "Valid generator types are:\n");
+      for (int k = 0; om_gsl_rng_names[k]; k++) {
+        fprintf(stderr, " %18s", om_gsl_rng_names[k]);
+        if ((k + 1) % 4 == 0) fputc('\n', stderr);
+      }
+      fputc('\n', stderr);
+      return 2;
+    }
+    if (strcmp(p, "mt19937") != 0) {
+      fprintf(stderr, "GSL_RNG_TYPE=%s: generator not available, only mt19937 (GSL's default) is implemented\n", p);
+      return 1;
+    }
+    fprintf(stderr, "GSL_RNG_TYPE=%s\n", p);
+  }
+  const char *s = getenv("GSL_RNG_SEED");
+  if (s) { *seed = strtoul(s, 0, 0); fprintf(stderr, "GSL_RNG_SEED=%lu\n", *seed); }
+  return 0;
 }
 
 static inline uint32_t om_rng_get(om_rng *r)

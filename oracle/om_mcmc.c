@@ -883,8 +883,7 @@ int main(int argc, char *argv[])
     return 1;
   }
   unsigned long seed = 0;
-  const char *s = getenv("GSL_RNG_SEED");
-  if (s) { seed = strtoul(s, 0, 0); fprintf(stderr, "GSL_RNG_SEED=%lu\n", seed); }
+  if (om_rng_env_setup(&seed)) return 1;   /* mcmc_init, mcmc.c:591-592 */
   size_t cap = 1 << 16, len = 0;
   char *text = (char *)malloc(cap);
   size_t got;

@@ -6,7 +6,8 @@
  *                                             reads its unset chain index there and crashes, mcmc.c:153)
  *
  * Reads the dataset on stdin (fgets(MAXS) semantics), seeds MT19937 from GSL_RNG_SEED
- * (strtoul base 0, unset -> GSL default), runs the chain on the GPU and writes
+ * (strtoul base 0, unset -> GSL default; GSL_RNG_TYPE as gsl_rng_env_setup reads it: mt19937 runs,
+ * another generator is refused with exit 1), runs the chain on the GPU and writes
  * Chains/chain_NN/{chain_data,exp_data,taxa,sites,hard_sites}.csv in the cwd.
  * Extension (not in the reference): SR_DEVICE=<ordinal> picks the GPU.
  * Exit 1 with the reference's messages on parse / consistency errors.
@@ -31,9 +32,9 @@ int main(int argc, char *argv[])
     fprintf(stderr, "usage: %s [manycd Tburnin T]\n", argv[0]);
     return 1;
   }
-  unsigned long seed = 0;
-  const char *s = getenv("GSL_RNG_SEED");
-  if (s) { seed = strtoul(s, 0, 0); fprintf(stderr, "GSL_RNG_SEED=%lu\n", seed); }
+  uint64_t seed = 0;
+  /* mcmc_init (mcmc.c:591-592): GSL_RNG_TYPE (mt19937 only; another generator exits 1) and GSL_RNG_SEED */
+  if (sr_rng_env_setup(&seed, 1)) return 1;
   size_t cap = 1 << 16, len = 0, got;
   char *text = malloc(cap);
   while (text && (got = fread(text + len, 1, cap - len, stdin)) > 0) {

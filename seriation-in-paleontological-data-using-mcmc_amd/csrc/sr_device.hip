@@ -3146,6 +3146,7 @@ struct srk_dev {
   int device, N, M, NW, nh, nchains, TB, TPT, rec_cap, gm, pr, sp, grid, coop;
   int mcd;                 /* manycd: per-taxon c, d (MCD kernels) */
   int jit;                 /* the launch uses the shape-specialised kernel (srk_spec_load) */
+  int jemb;                /* ... and its code object is the one embedded in the library */
   double *dsum;            /* srk_exp_data's per-chain sums (device) */
   hipModule_t mod;
   hipFunction_t jfn;
@@ -3273,21 +3274,32 @@ extern "C" int srk_plan(int N, int M, int nh, int block_threads, int gm_force, i
  * (sizeof KArgs, block, walk words, shape, LDS bytes) must equal this library's, else it is not used.
  * Any failure leaves the generic HIP kernel in place, with one stderr line per reason; there is no CPU
  * path either way. */
-static int srk_spec_load(srk_dev *d)
+/* where a session's specialised code object comes from, resolved before any HIP call of srk_create (a compile,
+   when one is needed, happens here and says so on stderr): embedded in the library (the shapes of
+   csrc/sr_embed_shapes.txt), else the cache, else compiled into it.  0 = found (img != NULL: embedded, else
+   path), -1 = the session runs no specialised kernel, else the sr_spec.c reason (already reported). */
+struct srk_spec_src { sr_spec_shape s; const void *img; size_t bytes; char path[4608]; };
+
+static int srk_spec_resolve(int N, int M, int nh, const srk_kplan &kp, srk_spec_src *src)
 {
 #if defined(SR_STAMPS)
-  (void)d;
+  (void)N; (void)M; (void)nh; (void)kp; (void)src;
   return -1;   /* (stamp builds: generic kernels only) */
 #else
-  srk_kplan kp = {d->TB, d->pr, d->gm, d->mcd, d->lds};
-  sr_spec_shape s;
-  if (!spec_shape_of(d->N, d->M, d->nh, kp, &s)) return -1;
-  char path[4608], log[4700];
-  const int rc = sr_spec_object(&s, path, sizeof path);
-  if (rc) {
-    sr_spec_note(rc, rc == SR_SPEC_ECC ? path : nullptr);
-    return rc;
-  }
+  if (!spec_shape_of(N, M, nh, kp, &src->s)) return -1;
+  src->img = sr_spec_embedded(&src->s, &src->bytes);
+  src->path[0] = 0;
+  if (src->img) return 0;
+  const int rc = sr_spec_object(&src->s, src->path, sizeof src->path, 1);
+  if (rc) sr_spec_note(rc, rc == SR_SPEC_ECC ? src->path : nullptr);
+  return rc;
+#endif
+}
+
+static int srk_spec_load(srk_dev *d, const srk_spec_src *src)
+{
+  const sr_spec_shape &s = src->s;
+  char log[4700];
   char name[128];
   snprintf(name, sizeof name, "_Z15sr_sweep_kernelILi%dELi%dELb0ELb0ELb0ELb0EEv5KArgs", s.TB, s.NWM);
   unsigned long long abi[4] = {0, 0, 0, 0};
@@ -3298,22 +3310,23 @@ static int srk_spec_load(srk_dev *d)
   hipDeviceptr_t ga = nullptr;
   size_t gbytes = 0;
   const char *what = nullptr;
-  if (hipModuleLoad(&d->mod, path) != hipSuccess) { d->mod = nullptr; what = "hipModuleLoad"; }
+  const hipError_t le = src->img ? hipModuleLoadData(&d->mod, src->img) : hipModuleLoad(&d->mod, src->path);
+  if (le != hipSuccess) { d->mod = nullptr; what = src->img ? "hipModuleLoadData" : "hipModuleLoad"; }
   else if (hipModuleGetFunction(&d->jfn, d->mod, name) != hipSuccess) what = "hipModuleGetFunction";
   else if (hipModuleGetGlobal(&ga, &gbytes, d->mod, "sr_spec_abi") != hipSuccess || gbytes != sizeof abi ||
            hipMemcpyDtoH(abi, ga, sizeof abi) != hipSuccess) what = "no ABI record";
   else if (memcmp(abi, want, sizeof abi) != 0) what = "ABI record differs";
   if (what) {
     (void)hipGetLastError();   /* the failed module call's error must not surface at the first generic launch */
-    snprintf(log, sizeof log, "%s (%s)", path, what);
+    snprintf(log, sizeof log, "%s (%s)", src->img ? "embedded code object" : src->path, what);
     sr_spec_note(SR_SPEC_ELOAD, log);
     if (d->mod) (void)hipModuleUnload(d->mod);
     d->mod = nullptr; d->jfn = nullptr;
     return SR_SPEC_ELOAD;
   }
   d->jit = 1;
+  d->jemb = src->img != nullptr;
   return 0;
-#endif
 }
 
 /* public (include/seriation.h): fill the specialised-kernel cache for a dataset without a GPU */
@@ -3331,8 +3344,10 @@ extern "C" int sr_specialize(const sr_dataset *ds, const sr_run_opts *opts)
 #if defined(SR_STAMPS)
   return 0;
 #else
+  size_t bytes = 0;
+  if (sr_spec_embedded(&s, &bytes)) return 1;   /* linked into the library: nothing to prepare */
   char path[4608];
-  const int rc = sr_spec_object(&s, path, sizeof path);
+  const int rc = sr_spec_object(&s, path, sizeof path, 0);
   if (rc) {
     sr_spec_note(rc, rc == SR_SPEC_ECC ? path : nullptr);
     return SR_EIO;
@@ -3375,6 +3390,10 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
 {
   srk_kplan kp;
   if (plan_kernel(st->N, st->M, st->nh, block_threads, gm_force, st->manycd, &kp)) return -6;
+  /* the specialised code object first: any compile happens before the device is touched */
+  srk_spec_src *ssrc = spec ? new srk_spec_src() : nullptr;
+  const int sres = ssrc ? srk_spec_resolve(st->N, st->M, st->nh, kp, ssrc) : -1;
+  struct Free { srk_spec_src *p; ~Free() { delete p; } } ssrc_free{ssrc};
   int ndev = srk_device_count();
   if (ndev <= 0 || device < 0 || device >= ndev) return -5;
   HIPCHK(hipSetDevice(device));
@@ -3392,9 +3411,10 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
     const int want = e ? atoi(e) : -1;
     const int Mh = sr_sp_half(st->M);
     sr_kfn ks = sr_pick_kernel(TB, st->N, st->M, true, false, st->nh, true);
-    /* SR_SPLIT=2 (experiment): halves of up to two blocks' taxa, several taxa per thread (512 threads:
-       256 VGPRs, 8 waves per CU) */
-    if (want != 0 && !d->mcd && d->gm && ks && (Mh <= TB || (want == 2 && TB == 512 && Mh <= 2 * TB)) && st->M > 128 &&
+    /* SR_SPLIT=2 (experiment, opt-in only): 512-thread halves of up to two blocks' taxa, several taxa per
+       thread (256 VGPRs, 8 waves per CU; measured slower) -- never chosen without it */
+    if (want != 0 && !d->mcd && d->gm && ks && ((TB == 1024 && Mh <= TB) || (want == 2 && TB == 512 && Mh <= 2 * TB)) &&
+        st->M > 128 &&
         (st->M > TB || want >= 1)) {
       int cus = 0, occ = 0, coop = 0;
       const int grid = 16 * ((st->nchains + 7) / 8);
@@ -3460,7 +3480,7 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
   if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) { srk_destroy(d); return -5; }
   d->own_stream = 1;
   if (hipEventCreate(&d->ev0) == hipSuccess && hipEventCreate(&d->ev1) == hipSuccess) d->have_events = 1;
-  if (spec) (void)srk_spec_load(d);
+  if (sres == 0) (void)srk_spec_load(d, ssrc);
   *out = d;
   return 0;
 }
@@ -3530,7 +3550,7 @@ extern "C" double srk_last_ms(srk_dev *d)
 
 extern "C" int srk_block_threads(const srk_dev *d) { return d->TB; }
 extern "C" int srk_variant(const srk_dev *d) { return d->gm ? (d->sp ? 3 : 1) : (d->pr ? 2 : 0); }
-extern "C" int srk_specialized(const srk_dev *d) { return d->jit; }
+extern "C" int srk_specialized(const srk_dev *d) { return d->jit ? (d->jemb ? 2 : 1) : 0; }   /* 2: embedded */
 
 extern "C" int srk_fetch_dbg(srk_dev *d, unsigned long long *out)
 {
@@ -3627,6 +3647,21 @@ extern "C" int srk_fetch_chain_records(srk_dev *d, int chain, int first, int cou
   const size_t W = 2 * (size_t)d->M + d->N, row = (size_t)chain * d->rec_cap + first;
   if (ab_pi) HIPCHK(hipMemcpy(ab_pi, d->args.rec_abpi + row * W, (size_t)count * W * sizeof(int16_t), hipMemcpyDeviceToHost));
   if (cdl) HIPCHK(hipMemcpy(cdl, d->args.rec_cdl + row * 3, (size_t)count * 3 * sizeof(double), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+extern "C" int srk_copy_chain_records(srk_dev *d, int chain, int first, int count, int16_t *ab_pi, double *cdl)
+{
+  if (chain < 0 || chain >= d->nchains || first < 0 || count < 0 || first + count > d->rec_cap) return -1;
+  if (count == 0) return 0;
+  HIPCHK(hipSetDevice(d->device));
+  const size_t W = 2 * (size_t)d->M + d->N, row = (size_t)chain * d->rec_cap + first;
+  if (ab_pi)
+    HIPCHK(hipMemcpyAsync(ab_pi, d->args.rec_abpi + row * W, (size_t)count * W * sizeof(int16_t), hipMemcpyDeviceToDevice,
+                          d->stream));
+  if (cdl)
+    HIPCHK(hipMemcpyAsync(cdl, d->args.rec_cdl + row * 3, (size_t)count * 3 * sizeof(double), hipMemcpyDeviceToDevice,
+                          d->stream));
   return 0;
 }
 

@@ -55,6 +55,62 @@ SR_API const char *sr_strerror(int code)
 
 SR_API int sr_device_count(void) { return srk_device_count(); }
 
+/* ------------------------------------------------------- GSL_RNG_TYPE / GSL_RNG_SEED */
+/* gsl_rng_env_setup's contract (GSL 2.6 rng/env.c; the reference's mcmc_init calls it, mcmc.c:591-592): the
+   generator named by GSL_RNG_TYPE out of gsl_rng_types_setup's list (rng/types.c, in its order), MT19937 when
+   unset.  The sampler implements MT19937 (and the opt-in Philox stream) only, so any other generator is
+   refused instead of silently sampling MT19937. */
+static const char *const sr_gsl_rng_names[] = {
+    "borosh13", "cmrg", "coveyou", "fishman18", "fishman20", "fishman2x", "gfsr4", "knuthran", "knuthran2",
+    "knuthran2002", "lecuyer21", "minstd", "mrg", "mt19937", "mt19937_1999", "mt19937_1998", "r250", "ran0", "ran1",
+    "ran2", "ran3", "rand", "rand48", "random128-bsd", "random128-glibc2", "random128-libc5", "random256-bsd",
+    "random256-glibc2", "random256-libc5", "random32-bsd", "random32-glibc2", "random32-libc5", "random64-bsd",
+    "random64-glibc2", "random64-libc5", "random8-bsd", "random8-glibc2", "random8-libc5", "random-bsd",
+    "random-glibc2", "random-libc5", "randu", "ranf", "ranlux", "ranlux389", "ranlxd1", "ranlxd2", "ranlxs0",
+    "ranlxs1", "ranlxs2", "ranmar", "slatec", "taus", "taus2", "taus113", "transputer", "tt800", "uni", "uni32",
+    "vax", "waterman14", "zuf", NULL};
+
+static int rng_type_check(int verbose)
+{
+  const char *p = getenv("GSL_RNG_TYPE");
+  if (!p) return SR_OK;
+  int known = 0;
+  for (int k = 0; sr_gsl_rng_names[k]; k++) known |= strcmp(p, sr_gsl_rng_names[k]) == 0;
+  if (!known) {   /* GSL: this list, then gsl_error("unknown generator") */
+    if (verbose) {
+      fprintf(stderr, "GSL_RNG_TYPE=%s not recognized\n", p);
+      fprintf(stderr, "Valid generator types are:\n");
+      for (int k = 0; sr_gsl_rng_names[k]; k++) {
+        fprintf(stderr, " %18s", sr_gsl_rng_names[k]);
+        if ((k + 1) % 4 == 0) fputc('\n', stderr);
+      }
+      fputc('\n', stderr);
+    }
+    return SR_EINVAL;
+  }
+  if (strcmp(p, "mt19937") != 0) {
+    if (verbose)
+      fprintf(stderr, "GSL_RNG_TYPE=%s: generator not available, only mt19937 (GSL's default) is implemented\n", p);
+    return SR_EUNSUPPORTED;
+  }
+  if (verbose) fprintf(stderr, "GSL_RNG_TYPE=%s\n", p);
+  return SR_OK;
+}
+
+SR_API int sr_rng_env_setup(uint64_t *seed, int32_t verbose)
+{
+  const int rc = rng_type_check(verbose);
+  if (rc) return rc;
+  unsigned long v = 0;
+  const char *s = getenv("GSL_RNG_SEED");
+  if (s) {
+    v = strtoul(s, 0, 0);
+    if (verbose) fprintf(stderr, "GSL_RNG_SEED=%lu\n", v);
+  }
+  if (seed) *seed = (uint64_t)v;
+  return SR_OK;
+}
+
 /* ------------------------------------------------------------------ parsing */
 
 /* one fgets(s, maxs, f) over the buffer; returns line length or -1 at EOF */
@@ -441,6 +497,9 @@ static int session_new(const sr_dataset *ds, const sr_chain_spec *specs, int32_t
      records, int16 a, b, pi records), M <= SR_MMAX taxa (several per thread beyond the block; the records hold
      positions only).  The LDS layout must also fit 160 KB (srk_create), else HBM columns. */
   if (ds->N > 4095 || ds->M > SR_MMAX) return SR_EUNSUPPORTED;
+  /* the environment names another GSL generator (mcmc.c:591-592): not MT19937's stream, refused */
+  const int rt = rng_type_check(0);
+  if (rt) return rt;
   sr_session *s = (sr_session *)calloc(1, sizeof(*s));
   if (!s) return SR_ENOMEM;
   s->ds.N = ds->N; s->ds.M = ds->M; s->ds.nh = ds->nh;
@@ -566,7 +625,17 @@ SR_API int32_t sr_session_records(const sr_session *s) { return s ? s->nrec : 0;
 SR_API int32_t sr_session_record_capacity(const sr_session *s) { return s ? s->rec_cap : 0; }
 SR_API int32_t sr_session_block_threads(const sr_session *s) { return s ? srk_block_threads(s->dev) : 0; }
 SR_API int32_t sr_session_variant(const sr_session *s) { return s ? srk_variant(s->dev) : -1; }
-SR_API int32_t sr_session_specialized(const sr_session *s) { return s ? srk_specialized(s->dev) : 0; }
+SR_API int32_t sr_session_specialized(const sr_session *s) { return s ? srk_specialized(s->dev) != 0 : 0; }
+/* test hook: 1 when the session's specialised code object is the one embedded in the library (no compiler,
+   no cache at run time), 0 otherwise */
+SR_API int32_t sr_session_spec_embedded(const sr_session *s) { return s ? srk_specialized(s->dev) == 2 : 0; }
+/* test hook: 1 when the library embeds the specialised code object a session of this shape would run */
+SR_API int sr_spec_is_embedded(int N, int M, int nh, int block_threads)
+{
+  sr_spec_shape sh;
+  size_t bytes = 0;
+  return srk_plan(N, M, nh, block_threads, -1, 0, &sh) == 1 && sr_spec_embedded(&sh, &bytes) != NULL && bytes > 0;
+}
 SR_API double sr_session_last_kernel_ms(sr_session *s) { return s ? srk_last_ms(s->dev) : -1.0; }
 
 SR_API int sr_session_fetch_records(sr_session *s, int32_t first, int32_t count, int16_t *ab_pi, double *cdl)
@@ -580,6 +649,13 @@ SR_API int sr_session_fetch_chain_records(sr_session *s, int32_t chain, int32_t 
 {
   if (!s || chain < 0 || chain >= s->nchains || first < 0 || count < 0 || first + count > s->nrec) return SR_EINVAL;
   return srk_fetch_chain_records(s->dev, chain, first, count, ab_pi, cdl) ? SR_EDEVICE : SR_OK;
+}
+
+SR_API int sr_session_copy_chain_records(sr_session *s, int32_t chain, int32_t first, int32_t count, int16_t *dev_ab_pi,
+                                        double *dev_cdl)
+{
+  if (!s || chain < 0 || chain >= s->nchains || first < 0 || count < 0 || first + count > s->nrec) return SR_EINVAL;
+  return srk_copy_chain_records(s->dev, chain, first, count, dev_ab_pi, dev_cdl) ? SR_EDEVICE : SR_OK;
 }
 
 SR_API int sr_session_fetch_cd_vectors(sr_session *s, int32_t first, int32_t count, double *cdv)

@@ -57,8 +57,15 @@ typedef struct { int TB, NWM, N, M, NH, force; } sr_spec_shape;
 #define SR_SPEC_ECACHE (-7)
 /* the cache path of the shape's code object (0), or a reason code */
 int sr_spec_path(const sr_spec_shape *s, char *path, size_t len);
-/* the path of the shape's code object, compiled into the cache first if it is missing (0), or a reason */
-int sr_spec_object(const sr_spec_shape *s, char *path, size_t len);
+/* the path of the shape's code object, compiled into the cache first if it is missing (0), or a reason;
+   announce: one stderr line when a compile starts (session creation: it can take seconds) */
+int sr_spec_object(const sr_spec_shape *s, char *path, size_t len, int announce);
+/* Code objects embedded in libseriation.so at build time (the shapes of csrc/sr_embed_shapes.txt, compiled by
+   build/srembed; build/sr_emb.c holds the table).  Weak and hidden: builds without the table (test variants,
+   the build tools) find none. */
+typedef struct { int TB, NWM, N, M, NH, force; const unsigned char *begin, *end; } sr_spec_emb;
+/* the embedded code object of this shape (*bytes its size), or NULL */
+const void *sr_spec_embedded(const sr_spec_shape *s, size_t *bytes);
 const char *sr_spec_reason(int code);
 /* one stderr line per reason and process: the session falls back to the generic kernel */
 void sr_spec_note(int code, const char *detail);
@@ -87,6 +94,8 @@ int srk_fetch_records(srk_dev *d, int first, int count, int16_t *ab_pi, double *
 /* per chain {sum -loglik, sum exp(c), sum exp(d)} over record rows [first, first + count) (compute_exp_data) */
 int srk_exp_data(srk_dev *d, int first, int count, double *sums);
 int srk_fetch_chain_records(srk_dev *d, int chain, int first, int count, int16_t *ab_pi, double *cdl);
+/* the same rows copied device to device into memory on the session's GPU, queued on the session stream */
+int srk_copy_chain_records(srk_dev *d, int chain, int first, int count, int16_t *ab_pi, double *cdl);
 int srk_download_state(srk_dev *d, sr_state_host *st);
 /* consume's last argument: manycd sessions' per-taxon c, d rows [nchains][count][2M], else NULL */
 int srk_run_pipelined(srk_dev *d, int total_calls, int cpl, int spc,

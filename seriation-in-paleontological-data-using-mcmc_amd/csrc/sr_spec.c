@@ -14,8 +14,12 @@
  *   - compile: `hipcc --genco` in a child process (posix_spawn, output to a log), never while a
  *     profiler tool library is preloaded (its library would initialise the GPU in every process
  *     of the compiler's exec chain): then the cache alone serves, else the generic kernel runs.
- * sr_specialize() (sr_device.hip) fills the cache ahead of time without a GPU; __graft_entry__
- * .build() does so for the reference's datasets.
+ *   - embedded: the shapes of csrc/sr_embed_shapes.txt (the reference's datasets, the bench matrix)
+ *     are compiled by `make` (build/srembed, this machinery with the cache in build/emb/) and linked
+ *     into libseriation.so itself (build/sr_emb.c); a session of such a shape loads its code object
+ *     from the library's memory -- no compiler, no cache, no snapshot needed at run time.
+ * sr_specialize() (sr_device.hip) fills the cache ahead of time without a GPU for other shapes;
+ * __graft_entry__.build() does so for the GPU tests' shapes.
  *
  * Built with -DSR_SPEC_TOOL it is the build's hash tool: `srhash <dir>` prints the snapshot hash.
  */
@@ -247,7 +251,23 @@ static void mkdirs(const char *dir)
   (void)mkdir(p, 0755);
 }
 
-int sr_spec_object(const sr_spec_shape *s, char *path, size_t len)
+extern const sr_spec_emb sr_spec_emb_table[] __attribute__((weak, visibility("hidden")));
+extern const int sr_spec_emb_count __attribute__((weak, visibility("hidden")));
+
+const void *sr_spec_embedded(const sr_spec_shape *s, size_t *bytes)
+{
+  if (!&sr_spec_emb_count || !sr_spec_emb_table) return NULL;
+  for (int k = 0; k < sr_spec_emb_count; ++k) {
+    const sr_spec_emb *e = &sr_spec_emb_table[k];
+    if (e->TB == s->TB && e->NWM == s->NWM && e->N == s->N && e->M == s->M && e->NH == s->NH && e->force == s->force) {
+      *bytes = (size_t)(e->end - e->begin);
+      return e->begin;
+    }
+  }
+  return NULL;
+}
+
+int sr_spec_object(const sr_spec_shape *s, char *path, size_t len, int announce)
 {
   int rc = sr_spec_path(s, path, len);
   if (rc) return rc;
@@ -271,6 +291,9 @@ int sr_spec_object(const sr_spec_shape *s, char *path, size_t len)
   snprintf(arch, sizeof arch, "--offload-arch=%s", SR_ARCH);
   defs_of(s, defs, sizeof defs);
   snprintf(fl, sizeof fl, "%s %s", SPEC_FLAGS, defs);
+  if (announce)
+    fprintf(stderr, "seriation: compiling the sweep kernel specialised for %d sites x %d taxa, %d hard sites (once: "
+                    "cached in %s)\n", s->N, s->M, s->NH, dir);
   char *argv[48];
   int na = 0;
   argv[na++] = (char *)cc;

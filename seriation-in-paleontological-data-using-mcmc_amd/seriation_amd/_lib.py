@@ -79,10 +79,10 @@ SINK_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, ctypes
 # every symbol include/seriation.h declares (tests/test_abi.py checks the export list)
 PUBLIC_SYMBOLS = [
     "sr_parse_dataset", "sr_load_dataset", "sr_free_dataset", "sr_save_dataset_bin", "sr_load_dataset_bin",
-    "sr_default_opts",
+    "sr_default_opts", "sr_rng_env_setup",
     "sr_run_chains", "sr_run_to_dirs", "sr_run_chains_multi", "sr_run_to_dirs_multi", "sr_session_create", "sr_session_set_stream",
     "sr_session_run", "sr_session_sync", "sr_session_records", "sr_session_record_capacity",
-    "sr_session_fetch_records", "sr_session_reset_records", "sr_session_fetch_chain_records", "sr_session_summaries",
+    "sr_session_fetch_records", "sr_session_reset_records", "sr_session_fetch_chain_records", "sr_session_copy_chain_records", "sr_session_summaries",
     "sr_session_fetch_cd_vectors", "sr_session_manycd", "sr_session_state_cd",
     "sr_session_state",
     "sr_session_accept_counts", "sr_session_fallback_counts", "sr_session_debug_flagged", "sr_session_last_kernel_ms", "sr_session_block_threads", "sr_session_variant", "sr_session_specialized",
@@ -109,6 +109,7 @@ def _lib():
         "sr_save_dataset_bin": (c_int, [P(sr_dataset), ctypes.c_char_p]),
         "sr_load_dataset_bin": (c_int, [ctypes.c_char_p, P(sr_dataset)]),
         "sr_default_opts": (None, [P(sr_run_opts)]),
+        "sr_rng_env_setup": (c_int, [P(ctypes.c_uint64), c_i32]),
         "sr_run_chains": (c_int, [P(sr_dataset), P(sr_chain_spec), c_i32, P(sr_run_opts), SINK_FN,
                                   c_void_p, P(sr_chain_summary)]),
         "sr_run_to_dirs": (c_int, [P(sr_dataset), P(sr_chain_spec), c_i32, P(sr_run_opts),
@@ -126,6 +127,7 @@ def _lib():
         "sr_session_fetch_records": (c_int, [c_void_p, c_i32, c_i32, P(ctypes.c_int16), P(c_double)]),
         "sr_session_reset_records": (c_int, [c_void_p]),
         "sr_session_fetch_chain_records": (c_int, [c_void_p, c_i32, c_i32, c_i32, P(ctypes.c_int16), P(c_double)]),
+        "sr_session_copy_chain_records": (c_int, [c_void_p, c_i32, c_i32, c_i32, c_void_p, c_void_p]),
         "sr_session_summaries": (c_int, [c_void_p, c_i32, c_i32, P(sr_chain_summary)]),
         "sr_session_fetch_cd_vectors": (c_int, [c_void_p, c_i32, c_i32, P(c_double)]),
         "sr_session_manycd": (c_i32, [c_void_p]),
@@ -158,6 +160,8 @@ def _lib():
                                        P(c_double), P(ctypes.c_uint64)]),
         "sr_spec_cache_path": (c_int, [c_int, c_int, c_int, c_int, ctypes.c_char_p, ctypes.c_size_t]),
         "sr_session_debug_counters": (c_int, [c_void_p, P(ctypes.c_ulonglong)]),
+        "sr_session_spec_embedded": (c_i32, [c_void_p]),
+        "sr_spec_is_embedded": (c_int, [c_int, c_int, c_int, c_int]),
         "sr_device_selftest_math": (c_int, [c_int, P(c_double), ctypes.c_long, P(c_double), P(c_double)]),
     }
     for name, (res, args) in sig.items():

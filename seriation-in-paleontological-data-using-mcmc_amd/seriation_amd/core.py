@@ -259,6 +259,16 @@ class Session:
                    "fetch_chain_records")
         return ab, cdl
 
+    def copy_chain_records(self, chain, ab_ptr, cdl_ptr, first=0, count=None):
+        """sr_session_copy_chain_records: one chain's buffered records copied device to device, queued on the
+        session stream, into device memory at ab_ptr ([count, 2M+N] int16) / cdl_ptr ([count, 3] float64)
+        (raw device addresses, e.g. a torch tensor's data_ptr(); 0 skips that array)."""
+        k = L.lib().sr_session_records(self.h)
+        count = k - first if count is None else count
+        _check(L.lib().sr_session_copy_chain_records(self.h, chain, first, count, ctypes.c_void_p(ab_ptr or None),
+                                                      ctypes.c_void_p(cdl_ptr or None)), "copy_chain_records")
+        return count
+
     def summaries(self, first=0, count=None):
         """sr_session_summaries: exp_data rows (chain_id, exp_loglik, exp_c, exp_d) [n, 4] of every chain
         over its buffered records (mcmc.c:53-67; divisor 1000 as the reference)."""

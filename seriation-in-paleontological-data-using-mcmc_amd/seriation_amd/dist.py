@@ -120,6 +120,46 @@ def gather_selected_records(selected, n_total, local_ids, ab_pi, cdl, device="cp
     return out_ab, out_cd
 
 
+def gather_selected_records_device(selected, n_total, local_ids, copy_chain, T, W, device, group=None):
+    """Step 2 on the device: the saved samples of the `selected` chain ids, in selection order, without a host
+    round trip.  Each rank queues device-to-device copies of the selected chains it owns (copy_chain(local_index,
+    ab_ptr, cdl_ptr): sr_session_copy_chain_records on the stream the collective runs on) into its slab of a
+    [k_max, T, W] int16 / [k_max, T, 3] float64 buffer on `device`, then ONE all-gather per array moves the slabs
+    (int16 rows as bytes: RCCL has no 16-bit integer type).  At world 1 (no process group) the copies alone.
+    Returns device tensors (ab_pi [k, T, W] int16, cdl [k, T, 3] float64).  With a gloo group (the one-GPU
+    rehearsal) the slabs cross through host tensors, as gloo requires."""
+    import torch
+    import torch.distributed as dist
+    on = dist.is_available() and dist.is_initialized()
+    world = dist.get_world_size(group) if on else 1
+    rank = dist.get_rank(group) if on else 0
+    owners = [owner(int(c), n_total, world) for c in selected]
+    k_max = max([owners.count(r) for r in range(world)] + [1])
+    pos = {int(c): k for k, c in enumerate(local_ids)}
+    mine = [int(c) for c, o in zip(selected, owners) if o == rank]
+    sab = torch.zeros((k_max, T, W), dtype=torch.int16, device=device)
+    scd = torch.zeros((k_max, T, 3), dtype=torch.float64, device=device)
+    for j, c in enumerate(mine):
+        copy_chain(pos[c], sab[j].data_ptr(), scd[j].data_ptr())
+    if world == 1:
+        return sab[:len(selected)], scd[:len(selected)]
+    gloo = dist.get_backend(group) == "gloo"
+    tab = sab.view(torch.uint8).cpu() if gloo else sab.view(torch.uint8)
+    tcd = scd.cpu() if gloo else scd
+    pab = [torch.empty_like(tab) for _ in range(world)]
+    pcd = [torch.empty_like(tcd) for _ in range(world)]
+    dist.all_gather(pab, tab, group=group)
+    dist.all_gather(pcd, tcd, group=group)
+    slot = [0] * world
+    idx = []
+    for o in owners:
+        idx.append((o, slot[o]))
+        slot[o] += 1
+    out_ab = torch.stack([pab[o][j] for o, j in idx]).to(device).view(torch.int16)
+    out_cd = torch.stack([pcd[o][j] for o, j in idx]).to(device)
+    return out_ab, out_cd
+
+
 def selection_statistics(ab_pi, cdl, N, M, chains_selected):
     """E[c], E[d], CORRMN of script.py:102-152 on the selected chains' records (record form of
     analysis.compute_exp_cd / compute_exp_ages)."""

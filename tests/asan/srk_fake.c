@@ -204,3 +204,15 @@ int srk_fetch_cdv(srk_dev *d, int first, int count, double *cdv)
     memcpy(cdv + (size_t)c * count * R2, d->rcv + ((size_t)c * d->rec_cap + first) * R2, (size_t)count * R2 * 8);
   return 0;
 }
+/* "device" memory of the fake is host memory: the device-to-device copy is a memcpy */
+int srk_copy_chain_records(srk_dev *d, int chain, int first, int count, int16_t *ab_pi, double *cdl)
+{
+  return srk_fetch_chain_records(d, chain, first, count, ab_pi, cdl);
+}
+/* no specialised kernels on the fake device */
+int srk_plan(int N, int M, int nh, int block_threads, int gm_force, int manycd, sr_spec_shape *shape)
+{
+  (void)N; (void)M; (void)nh; (void)block_threads; (void)gm_force; (void)manycd; (void)shape;
+  return 0;
+}
+const void *sr_spec_embedded(const sr_spec_shape *s, size_t *bytes) { (void)s; *bytes = 0; return NULL; }

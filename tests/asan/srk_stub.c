@@ -55,3 +55,14 @@ int srp_posterior_host(int device, int kind, const int16_t *ab, int n_sel, int c
 }
 void srk_destroy(srk_dev *d) { (void)d; }
 int srk_fetch_cdv(srk_dev *d, int f, int c, double *v) { (void)d; (void)f; (void)c; (void)v; return -5; }
+int srk_copy_chain_records(srk_dev *d, int ch, int f, int c, int16_t *a, double *x)
+{
+  (void)d; (void)ch; (void)f; (void)c; (void)a; (void)x;
+  return -5;
+}
+int srk_plan(int N, int M, int nh, int bt, int gm, int mcd, sr_spec_shape *s)
+{
+  (void)N; (void)M; (void)nh; (void)bt; (void)gm; (void)mcd; (void)s;
+  return 0;
+}
+const void *sr_spec_embedded(const sr_spec_shape *s, size_t *bytes) { (void)s; *bytes = 0; return NULL; }

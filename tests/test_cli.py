@@ -173,3 +173,95 @@ def test_product_cli_manycd_byte_identical(tmp_path):
     """manycd = 1 through the drop-in CLI: the five files byte-identical to the oracle CLI's (per-taxon c, d in
     chain_data.csv and taxa.csv)."""
     _compare(tmp_path, "g10s10.txt", ["1", "5", "12"], 11, "chain_00")
+
+
+# ---- GSL_RNG_TYPE (gsl_rng_env_setup, mcmc.c:591-592): mt19937 echoed and run, any other generator refused
+RNG_TYPES = [(None, 0), ("mt19937", 0), ("ranlxd2", 1), ("no_such_rng", 1)]
+
+
+def run_cli_env(exe, cwd, dataset, args, env_extra, chain_dir="chain_00"):
+    os.makedirs(os.path.join(cwd, "Chains", chain_dir), exist_ok=True)
+    env = {k: v for k, v in os.environ.items() if k != "GSL_RNG_TYPE"}
+    env.update(env_extra)
+    with open(os.path.join(DS, dataset), "rb") as fin:
+        return subprocess.run([exe] + list(args), cwd=cwd, stdin=fin, env=env, capture_output=True, timeout=900)
+
+
+def gsl_lines(err):
+    """stderr lines of gsl_rng_env_setup and of the refusal (the HIP runtime may add lines of its own)"""
+    txt = err.decode() if isinstance(err, bytes) else err
+    keep = ("GSL_RNG_", "Valid generator types are:", " ")
+    return [l for l in txt.splitlines() if l.startswith(keep) and not l.startswith("  HIP")]
+
+
+def _fake_cli():
+    pkg = os.path.join(ROOT, "seriation-in-paleontological-data-using-mcmc_amd")
+    r = subprocess.run(["make", "-s", "-C", pkg, "build/fake/mcmc"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return os.path.join(pkg, "build", "fake", "mcmc")
+
+
+@pytest.mark.parametrize("rtype,code", RNG_TYPES)
+def test_gsl_rng_type_oracle_and_fake_device(tmp_path, rtype, code):
+    """unset / mt19937 run (mt19937 echoed as GSL_RNG_TYPE=mt19937 before the seed line); another GSL generator
+    (ranlxd2) and an unknown name exit 1 before reading the dataset -- the oracle CLI and the product CLI (host
+    layer on the fake device) print the same lines and return the same code."""
+    if not os.path.exists(ORACLE_CLI):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    env = {"GSL_RNG_SEED": "5"}
+    if rtype:
+        env["GSL_RNG_TYPE"] = rtype
+    pa = run_cli_env(ORACLE_CLI, str(tmp_path / "o"), "g2s2.txt", ["0", "1", "1"], env)
+    pb = run_cli_env(_fake_cli(), str(tmp_path / "p"), "g2s2.txt", ["0", "1", "1"], env)
+    assert pa.returncode == code and pb.returncode == code, (pa.stderr, pb.stderr)
+    la, lb = gsl_lines(pa.stderr), gsl_lines(pb.stderr)
+    assert la == lb
+    if rtype == "mt19937":
+        assert la[:2] == ["GSL_RNG_TYPE=mt19937", "GSL_RNG_SEED=5"]
+    elif rtype is None:
+        assert la[0] == "GSL_RNG_SEED=5"
+    elif rtype == "ranlxd2":
+        assert la == ["GSL_RNG_TYPE=ranlxd2: generator not available, only mt19937 (GSL's default) is implemented"]
+    else:
+        assert la[:2] == ["GSL_RNG_TYPE=no_such_rng not recognized", "Valid generator types are:"]
+        assert "mt19937" in " ".join(la[2:]).split() and not any(l.startswith("GSL_RNG_SEED") for l in la)
+    if code:
+        assert not os.path.exists(os.path.join(str(tmp_path / "p"), "Chains", "chain_00", "chain_data.csv"))
+
+
+def test_gsl_rng_type_library_refuses(monkeypatch):
+    """the library entry points apply the same check: sr_rng_env_setup's codes, and sr_session_create refuses
+    another generator before any device call (SR_EUNSUPPORTED / SR_EINVAL), whatever the device."""
+    import ctypes
+    import seriation_amd as sa
+    lib = L.lib()
+    seed = ctypes.c_uint64(99)
+    for rtype, want in [("mt19937", L.SR_OK), ("ranlxd2", L.SR_EUNSUPPORTED), ("bogus", L.SR_EINVAL)]:
+        monkeypatch.setenv("GSL_RNG_TYPE", rtype)
+        monkeypatch.setenv("GSL_RNG_SEED", "0x10")
+        assert lib.sr_rng_env_setup(ctypes.byref(seed), 0) == want
+        if want == L.SR_OK:
+            assert seed.value == 16
+        else:
+            ds = sa.Dataset.load(os.path.join(DS, "g2s2.txt"))
+            h = ctypes.c_void_p()
+            o = sa.core.make_opts()
+            assert lib.sr_session_create(ctypes.byref(ds.c), sa.core.make_specs([1]), 1, ctypes.byref(o),
+                                         ctypes.byref(h)) == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rtype,code", RNG_TYPES)
+def test_gsl_rng_type_product_cli_gpu(tmp_path, rtype, code):
+    """on the GPU: the same stderr lines and exit codes as the oracle CLI; the mt19937 run's files equal the
+    unset run's (the same generator) and the oracle's."""
+    env = {"GSL_RNG_SEED": "5"}
+    if rtype:
+        env["GSL_RNG_TYPE"] = rtype
+    pa = run_cli_env(ORACLE_CLI, str(tmp_path / "o"), "g2s2.txt", ["0", "2", "3"], env)
+    pb = run_cli_env(PRODUCT_CLI, str(tmp_path / "p"), "g2s2.txt", ["0", "2", "3"], env)
+    assert pa.returncode == code and pb.returncode == code, (pa.stderr, pb.stderr)
+    assert gsl_lines(pa.stderr) == gsl_lines(pb.stderr)
+    if code == 0:
+        fa, fb = read_dir(str(tmp_path / "o"), "chain_00"), read_dir(str(tmp_path / "p"), "chain_00")
+        assert fa == fb

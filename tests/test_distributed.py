@@ -79,7 +79,18 @@ def _worker(rank, world, port, n_total, out):
         sel = sd.select_chains(allrows, K)
         sab, scd = sd.gather_selected_records(sel, n_total, ids, ab, cdl)   # collective 2
         stats = sd.selection_statistics(sab, scd, 124, 139, K)
-        out[rank] = (allrows.tobytes(), sel, sab.tobytes(), scd.tobytes(), stats)
+        # collective 2 in bench.py's form (gather_selected_records_device): the rank's selected records copied
+        # by pointer into one slab buffer (sr_session_copy_chain_records there; a memmove from the shard's
+        # records here, CPU tensors under gloo), one all-gather per array
+        import ctypes
+
+        def copy_chain(j, pa, pc):
+            ctypes.memmove(pa, np.ascontiguousarray(ab[j]).ctypes.data, ab[j].nbytes)
+            ctypes.memmove(pc, np.ascontiguousarray(cdl[j]).ctypes.data, cdl[j].nbytes)
+
+        dab, dcd = sd.gather_selected_records_device(sel, n_total, ids, copy_chain, TS, ab.shape[2], device="cpu")
+        dev_same = dab.numpy().tobytes() == sab.tobytes() and dcd.numpy().tobytes() == scd.tobytes()
+        out[rank] = (allrows.tobytes(), sel, sab.tobytes(), scd.tobytes(), stats, dev_same)
     finally:
         dist.destroy_process_group()
 
@@ -102,7 +113,8 @@ def test_gloo_world2_matches_single_process(n_total):
     rows, sel, sab, scd, stats = _single_process(n_total)
     assert 0 < len(sel) <= K
     for r in range(2):
-        b, s_, ab_b, cd_b, st = out[r]
+        b, s_, ab_b, cd_b, st, dev_same = out[r]
+        assert dev_same
         assert b == rows.tobytes()
         assert s_ == sel
         assert ab_b == sab.tobytes() and cd_b == scd.tobytes()

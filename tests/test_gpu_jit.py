@@ -135,6 +135,8 @@ PLANTED = textwrap.dedent("""
     ds = sa.Dataset.load(sys.argv[1], maxs=0)
     buf = ctypes.create_string_buffer(4096)
     assert sa.lib().sr_spec_cache_path(ds.N, ds.M, ds.nh, 0, buf, 4096) == 0
+    import os
+    os.makedirs(os.path.dirname(buf.value), exist_ok=True)
     with open(buf.value, "wb") as fh:
         fh.write(sys.argv[2].encode())
     with sa.Session(ds, [1, 2]) as s:
@@ -166,13 +168,47 @@ def test_specialized_shards_compile_together(tmp_path):
 
 def test_bad_code_object_falls_back_to_generic(tmp_path):
     """A corrupt object under the session's own key: hipModuleLoad fails, one stderr line names it, and
-    the session runs the generic kernel (same records as the oracle)."""
-    out, err = _child(PLANTED, {"SR_JIT_CACHE": str(tmp_path)}, os.path.join(HERE, "golden", "datasets", "g10s10.txt"),
-                      "not a code object")
+    the session runs the generic kernel (same records as the oracle).  (A shape the library does not embed:
+    the embedded ones never consult the cache.)"""
+    text = make_text(120, 130, 9, seed=120130)
+    path = tmp_path / "subject.txt"
+    path.write_bytes(text)
+    out, err = _child(PLANTED, {"SR_JIT_CACHE": str(tmp_path / "cache")}, str(path), "not a code object")
     assert out["specialized"] is False
     assert "did not load" in err and "hipModuleLoad" in err, err
-    with open(os.path.join(HERE, "golden", "datasets", "g10s10.txt"), "rb") as fh:
-        text = fh.read()
     for k, s in enumerate([1, 2]):
         o = oracle_ref.run_chain(text, s, 1, 2)
         np.testing.assert_array_equal(np.array(out["rec"][k]), o["rec_int"])
+
+
+EMBEDDED_RUN = textwrap.dedent("""
+    import json, sys
+    sys.path.insert(0, %r)
+    import numpy as np
+    import seriation_amd as sa
+    ds = sa.Dataset.load(sys.argv[1], maxs=0)
+    with sa.Session(ds, [4, 9]) as s:
+        spec, emb = s.specialized, int(sa.lib().sr_session_spec_embedded(s.h))
+    _, (ri, rd) = sa.run_chains(ds, [4, 9], burnin_calls=1, sample_calls=3, keep_records=True)
+    print(json.dumps({"specialized": spec, "embedded": emb, "rec": ri.tolist(), "dbl": rd.view(np.uint64).tolist()}))
+""" % PKG)
+
+
+@pytest.mark.parametrize("name", ["synth_256x512.txt", "g10s10.txt"])
+def test_embedded_kernel_needs_no_compiler_or_cache(tmp_path, name):
+    """The bench matrix and the reference's datasets run the specialised kernel linked into libseriation.so:
+    with no compiler (SR_HIPCC=/nonexistent) and an empty cache the session still reports specialized, its
+    code object is the embedded one, nothing is written to the cache, no fallback note, and the records equal
+    the oracle's."""
+    path = os.path.join(HERE, "golden", "datasets", name)
+    out, err = _child(EMBEDDED_RUN, {"SR_JIT_CACHE": str(tmp_path / "cache"), "SR_HIPCC": "/nonexistent/bin/hipcc"},
+                      path)
+    assert out["specialized"] is True and out["embedded"] == 1, err
+    assert not (tmp_path / "cache").exists()
+    assert "unavailable" not in err and "compiling" not in err, err
+    with open(path, "rb") as fh:
+        text = fh.read()
+    for k, s in enumerate([4, 9]):
+        o = oracle_ref.run_chain(text, s, 1, 3, maxs=0)
+        np.testing.assert_array_equal(np.array(out["rec"][k]), o["rec_int"])
+        np.testing.assert_array_equal(np.array(out["dbl"][k], dtype=np.uint64), o["rec_dbl"].view(np.uint64))

@@ -78,3 +78,10 @@ def test_bench_two_ranks_on_one_gpu_equals_single_process():
     for k in ("exp_c", "exp_d", "corr_mn"):
         assert a[k] == b[k], k
     assert single["parity"]["match"] and two["parity"]["match"]
+    # the parity legs check every selected chain and two the selection rejected (rank 0's first and last)
+    for line in (single, two):
+        p = line["parity"]
+        assert p["selected_checked"] == line["selection"]["chains_selected"]
+        assert len(p["rejected_checked"]) == 2 and not set(p["rejected_checked"]) & set(p["selected_checked"])
+        assert p["chains"] == p["selected_checked"] + p["rejected_checked"]
+    assert two["parity"]["rejected_checked"][-1] < 24   # rank 0's shard

@@ -17,6 +17,21 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "seriation-in-paleontological-data-using-mcmc_amd")
 LIBDIR = os.path.join(PKG, "build")
 SYNTH = os.path.join(ROOT, "tests", "golden", "datasets", "synth_256x512.txt")
+
+
+def _subject():
+    """a 250 x 500 dataset (12 hard sites): the bench kernel's block and walk (TB 512, 9 words) but a shape the
+    library does not embed, so its kernel goes through the cache / compiler machinery tested here"""
+    import tempfile
+    from test_gpu_edge import make_text
+    path = os.path.join(tempfile.gettempdir(), "sr_spec_subject_250x500.txt")
+    if not os.path.exists(path):
+        with open(path, "wb") as fh:
+            fh.write(make_text(250, 500, 12, seed=250500))
+    return path
+
+
+SUBJECT = _subject()
 HIPCC = "/opt/rocm/bin/hipcc"
 BENCH_KERNEL = b"_Z15sr_sweep_kernelILi512ELi9ELb0ELb0ELb0ELb0EEv5KArgs"
 
@@ -37,7 +52,7 @@ CHILD = textwrap.dedent("""
 """ % PKG)
 
 
-def child(env_extra, dataset=SYNTH, block_threads=0, lib=None):
+def child(env_extra, dataset=SUBJECT, block_threads=0, lib=None):
     env = dict(os.environ)
     env.pop("SR_JIT_CACHE", None)
     env.update(env_extra)
@@ -79,8 +94,7 @@ def test_key_covers_shape_block_and_compiler_version(tmp_path, datasets_dir):
     base, _ = child({"SR_JIT_CACHE": str(tmp_path), "SR_HIPCC": "/nonexistent/bin/hipcc"})
     g10, _ = child({"SR_JIT_CACHE": str(tmp_path), "SR_HIPCC": "/nonexistent/bin/hipcc"},
                    dataset=os.path.join(datasets_dir, "g10s10.txt"))
-    tb512, _ = child({"SR_JIT_CACHE": str(tmp_path), "SR_HIPCC": "/nonexistent/bin/hipcc"},
-                     dataset=os.path.join(datasets_dir, "g10s10.txt"), block_threads=512)
+    tb256, _ = child({"SR_JIT_CACHE": str(tmp_path), "SR_HIPCC": "/nonexistent/bin/hipcc"}, block_threads=256)
     # a compiler of another ROCm release: <hipcc>/../.info/version
     fake = tmp_path / "rocm"
     (fake / "bin").mkdir(parents=True)
@@ -90,19 +104,20 @@ def test_key_covers_shape_block_and_compiler_version(tmp_path, datasets_dir):
     cc.write_text("#!/bin/sh\nexit 3\n")
     cc.chmod(0o755)
     other, err = child({"SR_JIT_CACHE": str(tmp_path), "SR_HIPCC": str(cc)})
-    assert all(o["path_rc"] == 0 for o in (base, g10, tb512, other))
-    paths = {base["path"], g10["path"], tb512["path"], other["path"]}
+    assert all(o["path_rc"] == 0 for o in (base, g10, tb256, other))
+    paths = {base["path"], g10["path"], tb256["path"], other["path"]}
     assert len(paths) == 4, paths
-    # no compiler: nothing cached -> SR_EIO and one line on stderr; a failing compiler likewise
-    assert base["rc"] == -7 and other["rc"] == -7
+    # no compiler: nothing cached -> SR_EIO and one line on stderr; a failing compiler likewise (g10s10's kernel
+    # is embedded in the library: ready without either)
+    assert base["rc"] == -7 and other["rc"] == -7 and g10["rc"] == 1
     assert "compile failed" in err and ".log" in err
     assert not os.path.exists(other["path"])
 
 
 @needs_hipcc
 def test_entry_under_another_key_is_not_used(tmp_path, datasets_dir):
-    """A code object cached under another shape's key is never picked up: the bench shape compiles its own."""
-    other, _ = child({"SR_JIT_CACHE": str(tmp_path)}, dataset=os.path.join(datasets_dir, "g10s10.txt"))
+    """A code object cached under another shape's key is never picked up: the subject shape compiles its own."""
+    other, _ = child({"SR_JIT_CACHE": str(tmp_path)}, block_threads=256)
     assert other["rc"] == 1
     junk = open(other["path"], "rb").read()
     out, _ = child({"SR_JIT_CACHE": str(tmp_path)})
@@ -145,3 +160,32 @@ def test_unwritable_cache_is_reported(tmp_path):
     blocker.write_text("x")
     out, err = child({"SR_JIT_CACHE": str(blocker / "cache")})
     assert out["rc"] == -7 and "cache directory" in err
+
+
+EMBEDDED = [("g10s10.txt", 124, 139, 11), ("g10s2.txt", 501, 139, 14), ("g2s2.txt", 526, 296, 15),
+            ("g5s5.txt", 273, 202, 14), ("synth_256x512.txt", 256, 512, 12)]
+
+
+@pytest.mark.parametrize("name,N,M,nh", EMBEDDED, ids=[e[0] for e in EMBEDDED])
+def test_reference_shapes_are_embedded_without_compiler_or_cache(tmp_path, datasets_dir, name, N, M, nh):
+    """The reference's datasets and the bench matrix run code objects linked into libseriation.so at build time
+    (csrc/sr_embed_shapes.txt): with no compiler (SR_HIPCC=/nonexistent) and an empty cache, sr_specialize
+    reports the kernel ready (1) and writes nothing; the GPU side (tests/test_gpu_jit.py) loads them."""
+    import seriation_amd as sa
+    assert sa.lib().sr_spec_is_embedded(N, M, nh, 0) == 1
+    out, err = child({"SR_JIT_CACHE": str(tmp_path / "cache"), "SR_HIPCC": "/nonexistent/bin/hipcc"},
+                     dataset=os.path.join(datasets_dir, name))
+    assert out["rc"] == 1, (out, err)
+    assert not (tmp_path / "cache").exists()
+    assert "unavailable" not in err
+
+
+def test_embedded_objects_are_in_the_library():
+    """one code object per embedded shape inside the library file, each with the bench kernel family's symbol
+    and its ABI record; shapes outside the list (other block sizes, the test-only subject) are not embedded"""
+    import seriation_amd as sa
+    blob = open(os.path.join(LIBDIR, "libseriation.so"), "rb").read()
+    assert blob.count(b"sr_spec_abi") >= len(EMBEDDED)
+    assert BENCH_KERNEL in blob
+    assert sa.lib().sr_spec_is_embedded(250, 500, 12, 0) == 0
+    assert sa.lib().sr_spec_is_embedded(256, 512, 12, 1024) == 0

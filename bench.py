@@ -255,6 +255,9 @@ def main():
     for _ in range(args.warmup):
         sess.run(cps, save=False)
     sess.reset_records()
+    # device workspace of the selected chains' records (allocated before the timed region)
+    nrec_ws = args.steps * cps if not args.no_save else 1
+    rec_ws = sd.selected_records_workspace(CHAINS_SELECTED, nrec_ws, 2 * ds.M + ds.N, torch.device("cuda", device))
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -286,7 +289,7 @@ def main():
     # then (N > 1) one all-gather per array over RCCL -- they never leave HBM inside the timed region
     dev_ab, dev_cd = sd.gather_selected_records_device(
         selected, C * world, chain_ids, lambda j, pa, pc: sess.copy_chain_records(j, pa, pc, count=nrec), nrec, W,
-        device=torch.device("cuda", device))
+        device=torch.device("cuda", device), ws=rec_ws if nrec == nrec_ws else None)
     t_fetch = t_sel
     torch.cuda.synchronize()
     if dist:

@@ -208,8 +208,11 @@ int32_t sr_session_specialized(const sr_session *s);
  * object could not be produced (stderr says why), SR_EUNSUPPORTED / SR_EINVAL as sr_session_create. */
 int sr_specialize(const sr_dataset *ds, const sr_run_opts *opts);
 /* Checkpoint / resume (the reference has none): the full chain state (columns, pi,
-   limits, counts, c/d/loglik, MT19937 ring and cursor, acceptance counters) to a file; restoring
-   it over the same dataset continues every chain exactly where it stopped.  Records are not kept. */
+   limits, counts, c/d/loglik, MT19937 ring and cursor, acceptance counters) and the session's buffered
+   records to a file; restoring it over the same dataset continues every chain exactly where it stopped,
+   with the records in the new session's buffer (its capacity: the larger of opts->calls_per_launch and the
+   record count), so summaries over a resumed sampling phase equal an uninterrupted run's.  Files without
+   records (versions 3 / 4, before round 5) still restore, with an empty record buffer. */
 int sr_session_checkpoint(sr_session *s, const char *path);
 int sr_session_restore(const sr_dataset *ds, const char *path, const sr_run_opts *opts, sr_session **out);
 void sr_session_destroy(sr_session *s);

@@ -95,6 +95,11 @@ struct KArgs {
 #ifndef SR_CKG
 #define SR_CKG 4
 #endif
+/* the sweep's proposal tables filled by all threads before the phase-A barrier, and the swap drawn from them
+   (round 5; 0 = each wave fills its own at the start of phase C and the swap takes the scalar path) */
+#ifndef SR_COOP_TABLES
+#define SR_COOP_TABLES 1
+#endif
 #ifndef SR_KARG_RELOAD
 #define SR_KARG_RELOAD 0
 #endif
@@ -162,7 +167,7 @@ __host__ __device__ static constexpr inline Lay sr_layout(int N, int M, int NW, 
   L.part = o;  o = sr_al16(o + (size_t)2 * 16 * NWV * 8 * 4);         /* [2][proposal][wave] count sums */
   L.tot = o;   o = sr_al16(o + (size_t)2 * NWV * 4 * 4);               /* [2][wave] t0, f0, t1, f1 */
   L.xs = o;    o = sr_al16(o + (size_t)NWV * sizeof(double));          /* per-wave broadcast slot */
-  L.ptab = o;  o = sr_al16(o + 4 * 128 * 4);                          /* lane-parallel proposal tables (shared) */
+  L.ptab = o;  o = sr_al16(o + 5 * 128 * 4);                          /* lane-parallel proposal tables (shared) */
   L.misc = o;  o = sr_al16(o + 64 * 8);
   L.total = o;
   return L;
@@ -1787,6 +1792,71 @@ __device__ __forceinline__ void build_hard_tables(const int *hp, int nh, int N, 
   wsync();
 }
 
+/* One entry of the lane-parallel proposal tables (ptab, [5][128] u32 in LDS): "a proposal of kind `part`
+ * starting at word offset o" from the stream position whose ring index is `base` (`avail` words resident
+ * from it), with the GSL draws of mcmc.c under the hypothesis that no uniform_int rejects and the
+ * uniform_pos word is nonzero (ok bit 25; else the scalar path takes over at that proposal):
+ *   part 0  pi1  (mcmc.c:1133-1160): words o, o+1, uniform_pos at o+2;  i | j << 12 | veto << 24 | ok << 25
+ *   part 1  pi2  (mcmc.c:1317-1364): words o, o+1, [o+2, o+3 inc], uniform_pos at o+4; + inc1 << 26 | inc2 << 27
+ *   part 2  pi3  (mcmc.c:1495-1565): words o..o+3, uniform_pos at o+4; + ranks {r0, Kn} at ptab[384 + o]
+ *   part 3  swap (mcmc.c:1317-1364, j = i + 1): word o, [o+1, o+2 inc], uniform_pos at o+3 (at 512 + o)
+ * part -1: parts 0-2 together from one load of the words (a wave's own refresh).
+ * hcnt / nhall: the caller's wave copy of the hard-site tables (identical in every wave). */
+__device__ __forceinline__ void ptab_fill(uint32_t *ptab, const uint32_t *ring, uint32_t base, int avail, int o, int part,
+                                          int N, int nh, const int16_t *hcnt, const int16_t *nhall, const UDivM &mdN,
+                                          const UDivM &mdN1, const UDivM &md2, const UDivM &mdH, const UDivM &mdH1)
+{
+  uint32_t w[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    uint32_t idx = base + (uint32_t)min(o + k, avail - 1);
+    idx = (idx >= SR_RING * SR_MT_N) ? idx - SR_RING * SR_MT_N : idx;
+    w[k] = sr_mt_temper(ring[idx]);
+  }
+  if (part == 3) {   /* the swap: i uniform_int(N - 1), j = i + 1 */
+    const bool in = o + 4 <= avail;
+    const uint32_t qi = udivm_v(w[0], mdN1.m, mdN1.l);
+    const uint32_t qa = udivm_v(w[1], md2.m, md2.l), qb = udivm_v(w[2], md2.m, md2.l);
+    const int ic = min((int)qi, N - 2);
+    const bool veto = hcnt[ic + 2] - hcnt[ic] > 1;
+    const bool ok = in && qi < mdN1.n && (veto || (qa < 2u && qb < 2u && w[3] != 0u));
+    ptab[512 + o] = (uint32_t)ic | (veto ? 1u << 24 : 0u) | (ok ? 1u << 25 : 0u) | ((qa & 1u) << 26) | ((qb & 1u) << 27);
+    return;
+  }
+  const bool in = o + 5 <= avail;
+  const uint32_t qN = udivm_v(w[0], mdN.m, mdN.l), qN1 = udivm_v(w[1], mdN1.m, mdN1.l);
+  const uint32_t qa = udivm_v(w[2], md2.m, md2.l), qb = udivm_v(w[3], md2.m, md2.l);
+  const bool okN = in && qN < mdN.n && qN1 < mdN1.n;
+  const bool okab = qa < 2u && qb < 2u;
+  if (part <= 0) {
+    const int i = (int)qN, j = (int)qN1 + ((int)qN1 >= (int)qN ? 1 : 0);
+    const int ic = min(i, N - 1), jc = min(j, N - 1);
+    const bool veto = (hcnt[ic + 1] != hcnt[ic]) && (hcnt[max(ic, jc) + 1] - hcnt[min(ic, jc)] > 1);
+    const bool ok = okN && (veto || w[2] != 0u);
+    ptab[o] = (uint32_t)ic | ((uint32_t)jc << 12) | (veto ? 1u << 24 : 0u) | (ok ? 1u << 25 : 0u);
+  }
+  if (part < 0 || part == 1) {
+    int i = (int)qN, j = (int)qN1;
+    if (j >= i) j++; else { const int t = i; i = j; j = t; }
+    const int ic = min(i, N - 1), jc = min(j, N - 1);
+    const bool veto = hcnt[jc + 1] - hcnt[ic] > 1;
+    const bool ok = okN && (veto || (okab && w[4] != 0u));
+    ptab[128 + o] = (uint32_t)ic | ((uint32_t)jc << 12) | (veto ? 1u << 24 : 0u) | (ok ? 1u << 25 : 0u) | ((qa & 1u) << 26) |
+                    ((qb & 1u) << 27);
+  }
+  if (part < 0 || part == 2) {
+    const uint32_t qH = udivm_v(w[0], mdH.m, mdH.l), qH1 = udivm_v(w[1], mdH1.m, mdH1.l);
+    int ri, rj;
+    if ((int)qH <= (int)qH1) { ri = (int)qH; rj = (int)qH1 + 1; } else { ri = (int)qH1; rj = (int)qH; }
+    const int NH = N - nh;
+    ri = min(ri, max(NH - 1, 0)); rj = min(rj, max(NH - 1, 0));
+    const int i = nhall[ri], j = nhall[rj];
+    const bool ok = in && NH >= 2 && qH < mdH.n && qH1 < mdH1.n && okab && w[4] != 0u;
+    ptab[256 + o] = (uint32_t)i | ((uint32_t)j << 12) | (ok ? 1u << 25 : 0u) | ((qa & 1u) << 26) | ((qb & 1u) << 27);
+    ptab[384 + o] = (uint32_t)ri | ((uint32_t)(rj - ri + 1) << 16);
+  }
+}
+
 /* Count changes of one taxon (limits a, b; position-ordered column Pm) under proposal q:
  * dt0 (zeros inside), dt1 (ones inside); the reference's df0 = -dt0 and df1 = -dt1 always
  * (mcmc.c:1175-1256 pi1, 1367-1436 pi2, 1568-1631 pi3).  hcnt/nhall: the wave's hard-site tables. */
@@ -2006,7 +2076,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   int *tot = (int *)(smem + L.tot);
   double *xs = (double *)(smem + L.xs) + wave;
   uint64_t *misc = (uint64_t *)(smem + L.misc);
-  uint32_t *ptab = (uint32_t *)(smem + L.ptab);   /* [4][128]: pi1, pi2, pi3 records and pi3 ranks per word offset */
+  uint32_t *ptab = (uint32_t *)(smem + L.ptab);   /* [5][128]: pi1, pi2, pi3 records, pi3 ranks, swaps per word offset */
   /* SP exchange: flags [2], slots (sr_sp_xb); xseq counts exchanges (block-uniform, the same
      sequence in both halves) */
   int *xfl = SP ? A.xflag + 2 * (size_t)chain : nullptr;
@@ -2104,6 +2174,27 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   for (int call = 0; call < A.calls; ++call) {
     for (int sw = 0; sw < A.spc; ++sw) {
       const bool want_logl = (sw == A.spc - 1);
+      /* this sweep's lane-parallel proposal tables, filled cooperatively (one entry per thread) before the
+         phase-A barrier, at the stream position phase C most likely starts from: the c, d draws' fast path
+         takes 8 words, the Gibbs step 2M (one round: the ring holds them all).  Phase C uses them when it
+         starts there or a little later and no hard site has moved since; otherwise each wave refreshes its
+         own copy as before (ptab_fill).  The previous sweep's readers are past the end-of-sweep barrier. */
+      uint32_t tblk = 0u, toff = 0u;
+      bool tvalid = false;
+      if constexpr (!MCD && SR_COOP_TABLES) {
+        if (8 + 2 * M + SR_RNG_SLACK <= (SR_RING - 1) * SR_MT_N - (SR_MT_N - 1)) {
+          rng_ensure(R, 8 + 2 * M + SR_RNG_SLACK, tid, TB);
+          const uint32_t sp = R.off + 8u + 2u * (uint32_t)M;
+          tblk = R.blk + sp / SR_MT_N;
+          toff = sp % SR_MT_N;
+          const uint32_t sbase = (tblk & (SR_RING - 1)) * SR_MT_N + toff;
+          const int savail = min((int)((R.gen - tblk) * SR_MT_N - toff), 128);
+          for (int k = tid; k < 4 * 128; k += TB)
+            ptab_fill(ptab, ring, sbase, savail, k & 127, k >> 7, N, nh, hcnt, nhall, mdN, mdN1, md2, mdH, mdH1);
+          tvalid = true;
+        }
+      }
+      FST(15);
       /* ============ phase A: totals and the c, d draws (mcmc.c:768-825) */
       {
         int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
@@ -2378,10 +2469,9 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           if (multi && (olo % TB) != 0 && (olo / TB + 1) * TB < ohi) __syncthreads();
         }
         /* the lane-parallel proposal tables (ptab) hold "a proposal of each kind starting at word o"
-           for the 128 words from stream position (tblk, toff); a later batch of the sweep reuses them
-           while its proposals stay inside those words and no hard site moved (block-uniform state) */
-        uint32_t tblk = 0u, toff = 0u;
-        bool tvalid = false;
+           for the 128 words from stream position (tblk, toff) (the sweep's cooperative fill, or a wave's
+           refresh); a later batch of the sweep reuses them while its proposals stay inside those words and
+           no hard site moved (block-uniform state) */
         while (p0 < 16) {
           p0 = __builtin_amdgcn_readfirstlane(p0);   /* block-uniform: keep the control flow scalar */
           const int hl = (lane < nh) ? hp[lane] : 0;  /* lane k: hard position k */
@@ -2474,8 +2564,27 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               pend = p + 1;
               return true;
           };
-          /* the swap (accepted ~44 %) is drawn first and forms its own batch */
-          if (p0 == 0) (void)scalar_one(0);
+          /* the swap (accepted ~44 %) is drawn first and forms its own batch: from the sweep's table when
+             phase C starts inside it and the entry is on the fast path, else by the scalar path */
+          if (p0 == 0) {
+            const int dlt = tvalid ? (int)((rblk - tblk) * SR_MT_N + roff) - (int)toff : -1;
+            const uint32_t e = (SR_COOP_TABLES && dlt >= 0 && dlt < 128) ? ptab[512 + dlt] : 0u;
+            if ((e >> 25) & 1u) {
+              const bool veto = (e >> 24) & 1u;
+              const int i = (int)(e & 4095u);
+              uint32_t iu = base + 3u;   /* the uniform_pos word (not drawn after a veto) */
+              iu = (iu >= SR_RING * SR_MT_N) ? iu - SR_RING * SR_MT_N : iu;
+              const uint32_t uw = veto ? 1u : sr_mt_temper(ring[iu]);
+              vpk = (lane == 0) ? (i | ((i + 1) << 12) | (int)(((e >> 26) & 3u) << 24) | (veto ? 1 << 26 : 0)) : vpk;
+              vkr = (lane == 0) ? 0 : vkr;
+              vuw = (lane == 0) ? (int)uw : vuw;
+              vnd = (lane == 0) ? (veto ? 1 : 3) : vnd;
+              voff = (lane == 0) ? (veto ? 1 : 4) : voff;
+              pend = 1;
+            } else {
+              (void)scalar_one(0);
+            }
+          }
           /* (the swap in one batch with proposals 1..15 measured no faster: profiles/r03e_ab_phasec.json) */
           if (p0 > 0) {
             /* Lane-parallel draws: lane l evaluates "a pi1 / pi2 / pi3 proposal starting at word
@@ -2485,55 +2594,12 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                are shared by the waves: every wave writes the same values (block-uniform inputs), and
                no wave reads them past the batch barrier that every wave's next write follows. */
             int delta = tvalid ? (int)((rblk - tblk) * SR_MT_N + roff) - (int)toff : 0;
-            if (!tvalid || delta + 5 * (16 - p0) + 5 > 128) {
+            if (!tvalid || delta < 0 || delta + 5 * (16 - p0) + 5 > 128) {
               delta = 0;
               tblk = rblk; toff = roff; tvalid = true;
 #pragma unroll
-              for (int h = 0; h < 2; ++h) {
-                const int o = lane + 64 * h;
-                uint32_t w[5];
-#pragma unroll
-                for (int k = 0; k < 5; ++k) {
-                  uint32_t idx = base + (uint32_t)min(o + k, avail - 1);
-                  idx = (idx >= SR_RING * SR_MT_N) ? idx - SR_RING * SR_MT_N : idx;
-                  w[k] = sr_mt_temper(ring[idx]);
-                }
-                const bool in = o + 5 <= avail;
-                const uint32_t qN = udivm_v(w[0], mdN.m, mdN.l), qN1 = udivm_v(w[1], mdN1.m, mdN1.l);
-                const uint32_t qa = udivm_v(w[2], md2.m, md2.l), qb = udivm_v(w[3], md2.m, md2.l);
-                const bool okN = in && qN < mdN.n && qN1 < mdN1.n;
-                const bool okab = qa < 2u && qb < 2u;
-                /* pi1 (mcmc.c:1133-1160): words o, o+1, uniform_pos at o+2 */
-                {
-                  const int i = (int)qN, j = (int)qN1 + ((int)qN1 >= (int)qN ? 1 : 0);
-                  const int ic = min(i, N - 1), jc = min(j, N - 1);
-                  const bool veto = (hcnt[ic + 1] != hcnt[ic]) && (hcnt[max(ic, jc) + 1] - hcnt[min(ic, jc)] > 1);
-                  const bool ok = okN && (veto || w[2] != 0u);
-                  ptab[o] = (uint32_t)ic | ((uint32_t)jc << 12) | (veto ? 1u << 24 : 0u) | (ok ? 1u << 25 : 0u);
-                }
-                /* pi2 (mcmc.c:1317-1364): words o, o+1, [o+2, o+3 inc], uniform_pos at o+4 */
-                {
-                  int i = (int)qN, j = (int)qN1;
-                  if (j >= i) j++; else { const int t = i; i = j; j = t; }
-                  const int ic = min(i, N - 1), jc = min(j, N - 1);
-                  const bool veto = hcnt[jc + 1] - hcnt[ic] > 1;
-                  const bool ok = okN && (veto || (okab && w[4] != 0u));
-                  ptab[128 + o] = (uint32_t)ic | ((uint32_t)jc << 12) | (veto ? 1u << 24 : 0u) | (ok ? 1u << 25 : 0u) |
-                                  (qa << 26) | (qb << 27);
-                }
-                /* pi3 (mcmc.c:1495-1565): words o..o+3, uniform_pos at o+4 */
-                {
-                  const uint32_t qH = udivm_v(w[0], mdH.m, mdH.l), qH1 = udivm_v(w[1], mdH1.m, mdH1.l);
-                  int ri, rj;
-                  if ((int)qH <= (int)qH1) { ri = (int)qH; rj = (int)qH1 + 1; } else { ri = (int)qH1; rj = (int)qH; }
-                  const int NH = N - nh;
-                  ri = min(ri, max(NH - 1, 0)); rj = min(rj, max(NH - 1, 0));
-                  const int i = nhall[ri], j = nhall[rj];
-                  const bool ok = in && NH >= 2 && qH < mdH.n && qH1 < mdH1.n && okab && w[4] != 0u;
-                  ptab[256 + o] = (uint32_t)i | ((uint32_t)j << 12) | (ok ? 1u << 25 : 0u) | (qa << 26) | (qb << 27);
-                  ptab[384 + o] = (uint32_t)ri | ((uint32_t)(rj - ri + 1) << 16);
-                }
-              }
+              for (int h = 0; h < 2; ++h)
+                ptab_fill(ptab, ring, base, avail, lane + 64 * h, -1, N, nh, hcnt, nhall, mdN, mdN1, md2, mdH, mdH1);
               wsync();
             }
             FST(15);
@@ -3774,6 +3840,25 @@ extern "C" int srk_fetch_cdv(srk_dev *d, int first, int count, double *cdv)
   const size_t row = 2 * (size_t)d->M;
   HIPCHK(hipMemcpy2D(cdv, count * row * 8, d->args.rec_cdv + (size_t)first * row, d->rec_cap * row * 8, count * row * 8,
                      d->nchains, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+/* record rows [0, count) of every chain uploaded (a restored checkpoint's records: ab_pi [nchains][count][2M+N],
+   cdl [nchains][count][3], manycd sessions' cdv [nchains][count][2M]) */
+extern "C" int srk_upload_records(srk_dev *d, int count, const int16_t *ab_pi, const double *cdl, const double *cdv)
+{
+  if (count < 0 || count > d->rec_cap || (cdv && !d->mcd)) return -1;
+  if (count == 0) return 0;
+  HIPCHK(hipSetDevice(d->device));
+  HIPCHK(hipStreamSynchronize(d->stream));
+  const size_t W = 2 * (size_t)d->M + d->N, R2 = 2 * (size_t)d->M;
+  HIPCHK(hipMemcpy2D(d->args.rec_abpi, d->rec_cap * W * 2, ab_pi, count * W * 2, count * W * 2, d->nchains,
+                     hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy2D(d->args.rec_cdl, d->rec_cap * 3 * 8, cdl, count * 3 * 8, count * 3 * 8, d->nchains,
+                     hipMemcpyHostToDevice));
+  if (cdv)
+    HIPCHK(hipMemcpy2D(d->args.rec_cdv, d->rec_cap * R2 * 8, cdv, count * R2 * 8, count * R2 * 8, d->nchains,
+                       hipMemcpyHostToDevice));
   return 0;
 }
 

@@ -705,10 +705,12 @@ static int download(sr_session *s, sr_state_host *st)
 }
 
 /* ---- checkpoint / resume (the reference restarts every run; optional here) ----
- * File: "SRCK" | u32 version 2 | i32 N, M, nh, nchains | u64 FNV-1a of the dataset (X, hard) |
- * sr_chain_spec[nchains] | the device state as sr_state_host arrays (P, rpi, hp, ab, cnt, cdl, mt,
- * rng, acc), little-endian.  Restoring uploads the same words, so the continued chains are the
- * ones an uninterrupted session produces (tests/test_gpu_edge.py). */
+ * File: "SRCK" | u32 version | i32 N, M, nh, nchains | u64 FNV-1a of the dataset (X, hard) | [v5, v6: i32 nrec]
+ * | sr_chain_spec[nchains] | the device state as sr_state_host arrays (P, rpi, hp, ab, cnt, cdl, mt, rng, acc;
+ * manycd: cdv) | [v5, v6: the session's buffered records: ab_pi [nchains][nrec][2M+N] i16, cdl [nchains][nrec][3]
+ * f64, manycd: cdv [nchains][nrec][2M] f64], little-endian.  Restoring uploads the same words, so the continued
+ * chains are the ones an uninterrupted session produces, and summaries over the records (compute_exp_data,
+ * mcmc.c:53-67) span the whole sampling phase across the interruption (tests/test_gpu_edge.py). */
 static uint64_t dataset_hash(const sr_dataset *ds)
 {
   uint64_t h = 1469598103934665603ULL;
@@ -720,6 +722,8 @@ static uint64_t dataset_hash(const sr_dataset *ds)
 typedef struct { size_t bytes; void *p; } ck_part;
 #define SR_CK_VERSION 3   /* 2: SR_NACC counters per chain; 3: SR_NHMAX = 64 hard positions per chain */
 #define SR_CK_VERSION_MANYCD 4   /* version 3 + the per-taxon c, d of every chain (manycd sessions) */
+#define SR_CK_VERSION_REC 5      /* version 3 + the buffered records (written since round 5) */
+#define SR_CK_VERSION_REC_MANYCD 6   /* version 4 + the buffered records */
 #define SR_CK_PARTS 10
 
 static int ck_parts(sr_state_host *st, ck_part *pt)
@@ -734,18 +738,27 @@ static int ck_parts(sr_state_host *st, ck_part *pt)
   return st->manycd ? 10 : 9;
 }
 
-static int ck_write(const char *path, const sr_dataset *ds, const sr_chain_spec *specs, int32_t n, sr_state_host *st)
+typedef struct { int32_t nrec; int16_t *ab; double *cdl, *cdv; } ck_records;
+
+static int ck_write(const char *path, const sr_dataset *ds, const sr_chain_spec *specs, int32_t n, sr_state_host *st,
+                    const ck_records *rec)
 {
   FILE *f = fopen(path, "wb");
   if (!f) return SR_EIO;
-  const uint32_t ver = st->manycd ? SR_CK_VERSION_MANYCD : SR_CK_VERSION;
+  const uint32_t ver = st->manycd ? SR_CK_VERSION_REC_MANYCD : SR_CK_VERSION_REC;
   const int32_t dims[4] = {ds->N, ds->M, ds->nh, n};
   const uint64_t h = dataset_hash(ds);
+  const int32_t nrec = rec ? rec->nrec : 0;
   int ok = fwrite("SRCK", 1, 4, f) == 4 && fwrite(&ver, 4, 1, f) == 1 && fwrite(dims, 4, 4, f) == 4 &&
-           fwrite(&h, 8, 1, f) == 1 && fwrite(specs, sizeof(sr_chain_spec), n, f) == (size_t)n;
+           fwrite(&h, 8, 1, f) == 1 && fwrite(&nrec, 4, 1, f) == 1 && fwrite(specs, sizeof(sr_chain_spec), n, f) == (size_t)n;
   ck_part pt[SR_CK_PARTS];
   const int np = ck_parts(st, pt);
   for (int k = 0; k < np && ok; k++) ok = fwrite(pt[k].p, 1, pt[k].bytes, f) == pt[k].bytes;
+  if (ok && nrec > 0) {
+    const size_t rows = (size_t)n * nrec, W = 2 * (size_t)ds->M + ds->N;
+    ok = fwrite(rec->ab, 2 * W, rows, f) == rows && fwrite(rec->cdl, 24, rows, f) == rows &&
+         (!st->manycd || fwrite(rec->cdv, 16 * (size_t)ds->M, rows, f) == rows);
+  }
   if (fclose(f) != 0) ok = 0;
   return ok ? SR_OK : SR_EIO;
 }
@@ -756,7 +769,18 @@ SR_API int sr_session_checkpoint(sr_session *s, const char *path)
   sr_state_host st;
   int rc = download(s, &st);
   if (rc) return rc;
-  rc = ck_write(path, &s->ds, s->specs, s->nchains, &st);
+  ck_records r = {s->nrec, NULL, NULL, NULL};
+  if (r.nrec > 0) {   /* the buffered records travel with the state (v5 / v6) */
+    const size_t rows = (size_t)s->nchains * r.nrec, W = 2 * (size_t)s->ds.M + s->ds.N;
+    r.ab = (int16_t *)malloc(rows * W * 2);
+    r.cdl = (double *)malloc(rows * 24);
+    r.cdv = s->opts.manycd ? (double *)malloc(rows * 16 * (size_t)s->ds.M) : NULL;
+    if (!r.ab || !r.cdl || (s->opts.manycd && !r.cdv)) rc = SR_ENOMEM;
+    else if (srk_fetch_records(s->dev, 0, r.nrec, r.ab, r.cdl) || (r.cdv && srk_fetch_cdv(s->dev, 0, r.nrec, r.cdv)))
+      rc = SR_EDEVICE;
+  }
+  if (!rc) rc = ck_write(path, &s->ds, s->specs, s->nchains, &st, &r);
+  free(r.ab); free(r.cdl); free(r.cdv);
   state_free(&st);
   return rc;
 }
@@ -770,12 +794,12 @@ SR_API int sr_host_initial_checkpoint(const sr_dataset *ds, const sr_chain_spec 
   int rc = state_alloc(&st, ds->N, ds->M, ds->nh, n_chains, 0);
   if (rc) return rc;
   for (int c = 0; c < n_chains && rc == SR_OK; c++) rc = init_chain(ds, specs[c].seed, &st, c, 0);
-  if (rc == SR_OK) rc = ck_write(path, ds, specs, n_chains, &st);
+  if (rc == SR_OK) rc = ck_write(path, ds, specs, n_chains, &st, NULL);
   state_free(&st);
   return rc;
 }
 
-typedef struct { FILE *f; const sr_dataset *ds; } ck_reader;
+typedef struct { FILE *f; const sr_dataset *ds; int records; } ck_reader;
 
 static int check_chain(const sr_dataset *ds, const sr_state_host *st, int c);
 
@@ -807,7 +831,7 @@ static int ck_restore(void *ctx, sr_state_host *st)
   const int np = ck_parts(st, pt);
   for (int k = 0; k < np; k++)
     if (fread(pt[k].p, 1, pt[k].bytes, r->f) != pt[k].bytes) return SR_EPARSE;
-  if (fgetc(r->f) != EOF) return SR_EPARSE;
+  if (!r->records && fgetc(r->f) != EOF) return SR_EPARSE;   /* (v5 / v6: the records follow) */
   return ck_validate(r->ds, st);
 }
 
@@ -818,15 +842,21 @@ SR_API int sr_session_restore(const sr_dataset *ds, const char *path, const sr_r
   if (!f) return SR_EIO;
   char magic[4];
   uint32_t ver = 0;
-  int32_t dims[4];
+  int32_t dims[4], nrec = 0;
   uint64_t h = 0;
   int rc = SR_OK;
   sr_chain_spec *specs = NULL;
+  int16_t *rab = NULL;
+  double *rcd = NULL, *rcv = NULL;
   if (fread(magic, 1, 4, f) != 4 || memcmp(magic, "SRCK", 4) != 0 || fread(&ver, 4, 1, f) != 1 ||
-      (ver != SR_CK_VERSION && ver != SR_CK_VERSION_MANYCD) ||
+      (ver != SR_CK_VERSION && ver != SR_CK_VERSION_MANYCD && ver != SR_CK_VERSION_REC && ver != SR_CK_VERSION_REC_MANYCD) ||
       fread(dims, 4, 4, f) != 4 || fread(&h, 8, 1, f) != 1 || dims[3] <= 0)
     rc = SR_EPARSE;
-  else if (dims[0] != ds->N || dims[1] != ds->M || dims[2] != ds->nh || h != dataset_hash(ds))
+  const int with_rec = ver == SR_CK_VERSION_REC || ver == SR_CK_VERSION_REC_MANYCD;
+  const int mcd = ver == SR_CK_VERSION_MANYCD || ver == SR_CK_VERSION_REC_MANYCD;
+  if (rc == SR_OK && with_rec && (fread(&nrec, 4, 1, f) != 1 || nrec < 0)) rc = SR_EPARSE;
+  if (rc) { fclose(f); return rc; }
+  if (dims[0] != ds->N || dims[1] != ds->M || dims[2] != ds->nh || h != dataset_hash(ds))
     rc = SR_EINVAL;   /* the checkpoint belongs to another dataset */
   else if (!(specs = (sr_chain_spec *)malloc(sizeof(sr_chain_spec) * dims[3])))
     rc = SR_ENOMEM;
@@ -835,11 +865,30 @@ SR_API int sr_session_restore(const sr_dataset *ds, const char *path, const sr_r
   if (rc == SR_OK) {   /* the checkpoint's kind (manycd or not) decides; a caller's opts naming the other is an error */
     sr_run_opts o;
     if (opts) o = *opts; else sr_default_opts(&o);
-    if (opts && (o.manycd != 0) != (ver == SR_CK_VERSION_MANYCD)) rc = SR_EINVAL;
-    o.manycd = ver == SR_CK_VERSION_MANYCD;
-    ck_reader r = {f, ds};
+    if (opts && (o.manycd != 0) != mcd) rc = SR_EINVAL;
+    o.manycd = mcd;
+    /* the record buffer holds the checkpoint's records and the caller's further calls */
+    if (auto_calls_per_launch(&o) < nrec) o.calls_per_launch = nrec;
+    ck_reader r = {f, ds, with_rec};
     if (rc == SR_OK) rc = session_new(ds, specs, dims[3], &o, ck_restore, &r, out);
   }
+  if (rc == SR_OK && with_rec) {   /* the buffered records, uploaded into the new session's record buffer */
+    const size_t rows = (size_t)dims[3] * nrec, W = 2 * (size_t)ds->M + ds->N;
+    if (rows) {
+      rab = (int16_t *)malloc(rows * W * 2);
+      rcd = (double *)malloc(rows * 24);
+      rcv = mcd ? (double *)malloc(rows * 16 * (size_t)ds->M) : NULL;
+      if (!rab || !rcd || (mcd && !rcv)) rc = SR_ENOMEM;
+      else if (fread(rab, 2 * W, rows, f) != rows || fread(rcd, 24, rows, f) != rows ||
+               (mcd && fread(rcv, 16 * (size_t)ds->M, rows, f) != rows))
+        rc = SR_EPARSE;
+    }
+    if (rc == SR_OK && fgetc(f) != EOF) rc = SR_EPARSE;
+    if (rc == SR_OK && rows && srk_upload_records((*out)->dev, nrec, rab, rcd, rcv)) rc = SR_EDEVICE;
+    if (rc == SR_OK) (*out)->nrec = nrec;
+    else { sr_session_destroy(*out); *out = NULL; }
+  }
+  free(rab); free(rcd); free(rcv);
   free(specs);
   fclose(f);
   return rc;

@@ -102,6 +102,8 @@ int srk_run_pipelined(srk_dev *d, int total_calls, int cpl, int spc,
                       int (*consume)(void *, int, int, const int16_t *, const double *, const double *), void *ctx);
 /* manycd: per-taxon c, d of record rows [first, first + count), [nchains][count][2M] */
 int srk_fetch_cdv(srk_dev *d, int first, int count, double *cdv);
+/* record rows [0, count) of every chain uploaded (checkpoint restore); cdv only for manycd sessions */
+int srk_upload_records(srk_dev *d, int count, const int16_t *ab_pi, const double *cdl, const double *cdv);
 /* the session's record buffer in HBM: [nchains][rec_cap][2M+N] int16 */
 int srk_records_device(srk_dev *d, const int16_t **rec, int *rec_cap, int *device, void **stream);
 

@@ -141,7 +141,7 @@ class Session:
         self.h = h
 
     def checkpoint(self, path):
-        """sr_session_checkpoint: the full chain state to `path` (records are not kept)."""
+        """sr_session_checkpoint: the full chain state and the buffered records to `path`."""
         _check(L.lib().sr_session_checkpoint(self.h, os.fsencode(path)), "sr_session_checkpoint")
 
     @classmethod

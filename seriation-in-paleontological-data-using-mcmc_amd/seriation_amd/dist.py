@@ -120,7 +120,27 @@ def gather_selected_records(selected, n_total, local_ids, ab_pi, cdl, device="cp
     return out_ab, out_cd
 
 
-def gather_selected_records_device(selected, n_total, local_ids, copy_chain, T, W, device, group=None):
+def selected_records_workspace(k_cap, T, W, device, group=None):
+    """Device buffers for gather_selected_records_device, allocated ahead of a timed region (up to k_cap
+    selected chains per rank): the slab, the per-rank receive buffers and the output."""
+    import torch
+    import torch.distributed as dist
+    on = dist.is_available() and dist.is_initialized()
+    world = dist.get_world_size(group) if on else 1
+    gloo = on and dist.get_backend(group) == "gloo"
+    rdev = "cpu" if gloo else device
+    ws = {"k_cap": k_cap,
+          "sab": torch.zeros((k_cap, T, W), dtype=torch.int16, device=device),
+          "scd": torch.zeros((k_cap, T, 3), dtype=torch.float64, device=device)}
+    if world > 1:
+        ws["pab"] = [torch.empty((k_cap, T, 2 * W), dtype=torch.uint8, device=rdev) for _ in range(world)]
+        ws["pcd"] = [torch.empty((k_cap, T, 3), dtype=torch.float64, device=rdev) for _ in range(world)]
+        ws["out_ab"] = torch.empty((k_cap, T, 2 * W), dtype=torch.uint8, device=rdev)
+        ws["out_cd"] = torch.empty((k_cap, T, 3), dtype=torch.float64, device=rdev)
+    return ws
+
+
+def gather_selected_records_device(selected, n_total, local_ids, copy_chain, T, W, device, group=None, ws=None):
     """Step 2 on the device: the saved samples of the `selected` chain ids, in selection order, without a host
     round trip.  Each rank queues device-to-device copies of the selected chains it owns (copy_chain(local_index,
     ab_ptr, cdl_ptr): sr_session_copy_chain_records on the stream the collective runs on) into its slab of a
@@ -137,8 +157,12 @@ def gather_selected_records_device(selected, n_total, local_ids, copy_chain, T, 
     k_max = max([owners.count(r) for r in range(world)] + [1])
     pos = {int(c): k for k, c in enumerate(local_ids)}
     mine = [int(c) for c, o in zip(selected, owners) if o == rank]
-    sab = torch.zeros((k_max, T, W), dtype=torch.int16, device=device)
-    scd = torch.zeros((k_max, T, 3), dtype=torch.float64, device=device)
+    if ws is not None and ws["k_cap"] >= k_max and ws["k_cap"] >= len(selected):
+        sab, scd = ws["sab"][:k_max], ws["scd"][:k_max]
+    else:
+        ws = None
+        sab = torch.zeros((k_max, T, W), dtype=torch.int16, device=device)
+        scd = torch.zeros((k_max, T, 3), dtype=torch.float64, device=device)
     for j, c in enumerate(mine):
         copy_chain(pos[c], sab[j].data_ptr(), scd[j].data_ptr())
     if world == 1:
@@ -146,8 +170,11 @@ def gather_selected_records_device(selected, n_total, local_ids, copy_chain, T, 
     gloo = dist.get_backend(group) == "gloo"
     tab = sab.view(torch.uint8).cpu() if gloo else sab.view(torch.uint8)
     tcd = scd.cpu() if gloo else scd
-    pab = [torch.empty_like(tab) for _ in range(world)]
-    pcd = [torch.empty_like(tcd) for _ in range(world)]
+    if ws is not None:
+        pab, pcd = [t[:k_max] for t in ws["pab"]], [t[:k_max] for t in ws["pcd"]]
+    else:
+        pab = [torch.empty_like(tab) for _ in range(world)]
+        pcd = [torch.empty_like(tcd) for _ in range(world)]
     dist.all_gather(pab, tab, group=group)
     dist.all_gather(pcd, tcd, group=group)
     slot = [0] * world
@@ -155,9 +182,14 @@ def gather_selected_records_device(selected, n_total, local_ids, copy_chain, T, 
     for o in owners:
         idx.append((o, slot[o]))
         slot[o] += 1
-    out_ab = torch.stack([pab[o][j] for o, j in idx]).to(device).view(torch.int16)
-    out_cd = torch.stack([pcd[o][j] for o, j in idx]).to(device)
-    return out_ab, out_cd
+    k = len(selected)
+    if ws is not None:
+        out_ab = torch.stack([pab[o][j] for o, j in idx], out=ws["out_ab"][:k])
+        out_cd = torch.stack([pcd[o][j] for o, j in idx], out=ws["out_cd"][:k])
+    else:
+        out_ab = torch.stack([pab[o][j] for o, j in idx])
+        out_cd = torch.stack([pcd[o][j] for o, j in idx])
+    return out_ab.to(device).view(torch.int16), out_cd.to(device)
 
 
 def selection_statistics(ab_pi, cdl, N, M, chains_selected):

@@ -216,3 +216,14 @@ int srk_plan(int N, int M, int nh, int block_threads, int gm_force, int manycd, 
   return 0;
 }
 const void *sr_spec_embedded(const sr_spec_shape *s, size_t *bytes) { (void)s; *bytes = 0; return NULL; }
+int srk_upload_records(srk_dev *d, int count, const int16_t *ab_pi, const double *cdl, const double *cdv)
+{
+  if (count < 0 || count > d->rec_cap) return -1;
+  const size_t W = 2 * (size_t)d->st.M + d->st.N, R2 = 2 * (size_t)d->st.M;
+  for (int c = 0; c < d->st.nchains; c++) {
+    memcpy(d->rec + (size_t)c * d->rec_cap * W, ab_pi + (size_t)c * count * W, (size_t)count * W * 2);
+    memcpy(d->rcd + (size_t)c * d->rec_cap * 3, cdl + (size_t)c * count * 3, (size_t)count * 24);
+    if (cdv && d->rcv) memcpy(d->rcv + (size_t)c * d->rec_cap * R2, cdv + (size_t)c * count * R2, (size_t)count * R2 * 8);
+  }
+  return 0;
+}

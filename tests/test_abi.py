@@ -131,8 +131,18 @@ def test_restore_validates_chain_state(tmp_path):
         return rc
 
     assert restore(good) in (0, L.SR_EDEVICE)
+    raw5 = good.read_bytes()
+    assert raw5[:4] == b"SRCK" and np.frombuffer(raw5, "<u4", 1, 4)[0] == 5   # version 5: records follow the state
+    assert np.frombuffer(raw5, "<i4", 1, 32)[0] == 0                          # (none in an initial checkpoint)
+    # a version-3 file (before round 5: no record count, no records) still restores
+    v3 = tmp_path / "v3.srck"
+    v3.write_bytes(raw5[:4] + np.array([3], "<u4").tobytes() + raw5[8:32] + raw5[36:])
+    assert restore(v3) in (0, L.SR_EDEVICE)
+    trunc = tmp_path / "trunc.srck"
+    trunc.write_bytes(raw5[:-8])
+    assert restore(trunc) == -2
     N, M, nh, NW = ds.N, ds.M, ds.nh, (ds.N + 31) // 32
-    off = 32 + C * ctypes.sizeof(L.sr_chain_spec)
+    off = 36 + C * ctypes.sizeof(L.sr_chain_spec)
     sizes = [("P", C * NW * M * 4), ("rpi", C * N * 4), ("hp", C * 64 * 4), ("ab", C * 2 * M * 4),
              ("cnt", C * 4 * M * 4), ("cdl", C * 4 * 8), ("mt", C * 8 * 624 * 4), ("rng", C * 2 * 8), ("acc", C * 10 * 8)]
     base = {}
@@ -222,7 +232,7 @@ def test_checkpoint_many_hard_sites(tmp_path):
         L.lib().sr_session_destroy(h)
     assert rc in (0, L.SR_EDEVICE)
     NW = (N + 31) // 32
-    off = 32 + C * ctypes.sizeof(L.sr_chain_spec) + C * NW * M * 4 + C * N * 4
+    off = 36 + C * ctypes.sizeof(L.sr_chain_spec) + C * NW * M * 4 + C * N * 4
     raw = bytearray(good.read_bytes())
     assert len(raw) == off + C * 128 * 4 + C * 2 * M * 4 + C * 4 * M * 4 + C * 4 * 8 + C * 8 * 624 * 4 + C * 2 * 8 + C * 10 * 8
     hp = np.frombuffer(bytes(raw), "<i4", C * 128, off).reshape(C, 128)

@@ -90,6 +90,9 @@ def _worker(rank, world, port, n_total, out):
 
         dab, dcd = sd.gather_selected_records_device(sel, n_total, ids, copy_chain, TS, ab.shape[2], device="cpu")
         dev_same = dab.numpy().tobytes() == sab.tobytes() and dcd.numpy().tobytes() == scd.tobytes()
+        ws = sd.selected_records_workspace(K, TS, ab.shape[2], "cpu")   # bench.py's preallocated form
+        wab, wcd = sd.gather_selected_records_device(sel, n_total, ids, copy_chain, TS, ab.shape[2], device="cpu", ws=ws)
+        dev_same = dev_same and wab.numpy().tobytes() == sab.tobytes() and wcd.numpy().tobytes() == scd.tobytes()
         out[rank] = (allrows.tobytes(), sel, sab.tobytes(), scd.tobytes(), stats, dev_same)
     finally:
         dist.destroy_process_group()

@@ -10,6 +10,7 @@ import pytest
 
 import oracle_ref
 import seriation_amd as sa
+from seriation_amd import _lib as L
 
 pytestmark = pytest.mark.gpu
 
@@ -174,6 +175,46 @@ def test_split_512_thread_halves_parity(monkeypatch, name, N, M, nh):
         assert summ[k]["consistent"] == 0
 
 
+# Ragged split halves (round 5 audit, DESIGN.md 4 "cross-thread orderings"): the second half starts at
+# olo = sr_sp_half(M), not a multiple of the block, so the Gibbs step's rounds of TB taxa (taken when 2M words
+# exceed the resident RNG ring, M > 1360) hand some of the half's taxa to threads other than their owners in
+# phases A / C; a barrier orders those writes before phase C.  One geometry per case: Gibbs rounds touching the
+# half (1, 2, 3), block 1024 or the opt-in 512 (several taxa per thread), more than 64 hard sites (the bitmap
+# paths) -- name, N, M, nh, block_threads, SR_SPLIT, Gibbs rounds inside the second half.
+RAGGED = [("r1-nh100", 150, 1000, 100, 1024, "1", 1), ("r2-nh80", 120, 1700, 80, 1024, "-1", 2),
+          ("r2-tb512-nh70", 100, 1500, 70, 512, "2", 2), ("r3-tb512-nh66", 100, 1900, 66, 512, "2", 3)]
+
+
+def _sp_half(M):
+    return (((M + 1) // 2) + 63) & ~63
+
+
+@pytest.mark.parametrize("name,N,M,nh,tb,split,rounds", RAGGED, ids=["ragged-" + c[0] for c in RAGGED])
+def test_split_ragged_half_geometries(monkeypatch, name, N, M, nh, tb, split, rounds):
+    olo = _sp_half(M)
+    assert olo % tb != 0   # the ragged second half
+    ring_rounds = 1 if 2 * M + 1024 <= 7 * 624 - 623 else -(-M // tb)
+    touching = 1 if ring_rounds == 1 else len({m // tb for m in range(olo, M)})
+    assert touching == rounds, (name, touching)
+    if split == "-1":
+        monkeypatch.delenv("SR_SPLIT", raising=False)
+    else:
+        monkeypatch.setenv("SR_SPLIT", split)
+    text = make_text(N, M, nh, seed=N * 1000 + M + 5)
+    ds = sa.Dataset.parse(text, maxs=0)
+    seeds = [3, 8, 30]
+    with sa.Session(ds, seeds, block_threads=tb, columns="hbm") as s:
+        assert s.variant == "hbm" and s.kernel == "split" and s.block_threads == tb
+    summ, (ri, rd) = sa.run_chains(ds, seeds, burnin_calls=2, sample_calls=3, keep_records=True, block_threads=tb,
+                                   columns="hbm")
+    for k, sd_ in enumerate(seeds):
+        o = oracle_ref.run_chain(text, sd_, 2, 3, maxs=0)
+        assert o["rc"] == 0
+        np.testing.assert_array_equal(ri[k], o["rec_int"], err_msg="%s seed %d" % (name, sd_))
+        assert np.array_equal(rd[k].view(np.uint64), o["rec_dbl"].view(np.uint64)), (name, sd_)
+        assert summ[k]["consistent"] == 0
+
+
 def test_checkpoint_resume_continues_exactly(tmp_path):
     """sr_session_checkpoint after 10 calls + sr_session_restore + 20 calls == 30 calls straight."""
     import os
@@ -196,6 +237,44 @@ def test_checkpoint_resume_continues_exactly(tmp_path):
         r.close()
     assert np.array_equal(ab_full[:, 10:], ab2)
     assert np.array_equal(cdl_full[:, 10:].view(np.uint64), cdl2.view(np.uint64))
+
+
+@pytest.mark.parametrize("manycd", [0, 1])
+def test_checkpoint_carries_records(tmp_path, manycd):
+    """Checkpoints keep the buffered records (version 5 / 6): 500 saved calls + checkpoint + restore + 500 saved
+    calls give the same 1000 records and the same exp_data rows (compute_exp_data over the whole sampling phase,
+    mcmc.c:53-67) bit for bit as 1000 calls straight -- manycd sessions with their per-taxon c, d too."""
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "datasets", "g10s10.txt")
+    ds = sa.Dataset.load(path)
+    seeds = [5, 6, 7]
+    T, H = (1000, 500) if not manycd else (60, 25)
+    with sa.Session(ds, seeds, calls_per_launch=T, manycd=manycd) as s:
+        s.run(T, save=True)
+        ab_full, cdl_full = s.fetch_records()
+        sum_full = s.summaries()
+        cv_full = s.fetch_cd_vectors() if manycd else None
+    ck = str(tmp_path / "rec.srck")
+    with sa.Session(ds, seeds, calls_per_launch=H, manycd=manycd) as s:
+        s.run(H, save=True)
+        s.checkpoint(ck)
+    with open(ck, "rb") as fh:
+        head = fh.read(36)
+    assert np.frombuffer(head, "<u4", 1, 4)[0] == (6 if manycd else 5) and np.frombuffer(head, "<i4", 1, 32)[0] == H
+    r = sa.Session.restore(ds, ck, calls_per_launch=T, manycd=manycd)
+    try:
+        assert L.lib().sr_session_records(r.h) == H
+        r.run(T - H, save=True)
+        ab2, cdl2 = r.fetch_records()
+        sum2 = r.summaries()
+        cv2 = r.fetch_cd_vectors() if manycd else None
+    finally:
+        r.close()
+    assert np.array_equal(ab_full, ab2)
+    assert np.array_equal(cdl_full.view(np.uint64), cdl2.view(np.uint64))
+    assert np.array_equal(sum_full.view(np.uint64), sum2.view(np.uint64))
+    if manycd:
+        assert np.array_equal(cv_full.view(np.uint64), cv2.view(np.uint64))
 
 
 def _all_ones_text(N, M, hard_rows):

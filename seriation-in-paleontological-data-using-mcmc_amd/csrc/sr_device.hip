@@ -100,6 +100,19 @@ struct KArgs {
 #ifndef SR_COOP_TABLES
 #define SR_COOP_TABLES 1
 #endif
+/* the proposal sums of a batch of at least this many proposals by one transposed reduction per wave
+   (wave_sum32_t; 0 = one reduction per slot) */
+#ifndef SR_TSUMS
+#define SR_TSUMS 0
+#endif
+/* the main batch's proposal slots without per-slot branches (one-taxon kernels) */
+#ifndef SR_FULL_BATCH
+#define SR_FULL_BATCH 0
+#endif
+/* branch-free proposal terms (taxon_dt: no exec-mask branches, indices clamped, results selected) */
+#ifndef SR_BF_TERMS
+#define SR_BF_TERMS 0
+#endif
 #ifndef SR_KARG_RELOAD
 #define SR_KARG_RELOAD 0
 #endif
@@ -708,6 +721,15 @@ __device__ __forceinline__ int col_pre(const uint16_t *prem, const uint32_t *Pm,
 {
   const int w = x >> 5, bits = x & 31;
   const uint32_t word = bits ? Pm[w * M] : 0u;
+  return (int)prem[w * M] + __popc(word & ((1u << bits) - 1u));
+}
+
+/* the same without a branch: the word read always (row 0 when x is a multiple of 32, masked to nothing),
+   so a proposal's taxon terms carry no exec-mask branches and the slots' reads can be in flight together */
+__device__ __forceinline__ int col_pre_bf(const uint16_t *prem, const uint32_t *Pm, int M, int x)
+{
+  const int w = x >> 5, bits = x & 31;
+  const uint32_t word = Pm[(bits ? w : 0) * M];
   return (int)prem[w * M] + __popc(word & ((1u << bits) - 1u));
 }
 
@@ -1697,6 +1719,58 @@ __device__ __forceinline__ int wave_sum_i32(int x)
 }
 
 
+/* The wave sums of 32 values at once by a transposed butterfly: at exchange step k (partner lane ^ 2^k) a lane
+ * keeps one half of the values it holds (by lane bit k) and adds its partner's copy of that half, so 32 values
+ * cost 16 + 8 + 4 + 2 + 1 + 1 adds (plus the selects and moves) instead of 32 six-step reductions each read
+ * out by one lane.  Partners: quad_perm (xor 1, 2), row_shl/row_shr by 4 and 8 with bank masks (xor 4, 8),
+ * ds_swizzle (xor 16), ds_bpermute (xor 32).  Integer adds: exact in any order.  On return lane l (and l ^ 32)
+ * holds the total of value u[16 (l & 1) + s], s = 8 b1 + 4 b2 + 2 b3 + b4 with b_k = bit k of l. */
+__device__ __forceinline__ uint32_t wave_sum32_t(uint32_t (&u)[32], int lane)
+{
+  {
+    const bool b = lane & 1;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t keep = b ? u[16 + k] : u[k], send = b ? u[k] : u[16 + k];
+      u[k] = keep + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)send, 0xB1, 0xF, 0xF, false);   /* xor 1 */
+    }
+  }
+  {
+    const bool b = (lane >> 1) & 1;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t keep = b ? u[8 + k] : u[k], send = b ? u[k] : u[8 + k];
+      u[k] = keep + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)send, 0x4E, 0xF, 0xF, false);   /* xor 2 */
+    }
+  }
+  {
+    const bool b = (lane >> 2) & 1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t keep = b ? u[4 + k] : u[k], send = b ? u[k] : u[4 + k];
+      int r = __builtin_amdgcn_update_dpp(0, (int)send, 0x104, 0xF, 0x5, false);   /* row_shl:4 into banks 0, 2 */
+      r = __builtin_amdgcn_update_dpp(r, (int)send, 0x114, 0xF, 0xA, false);       /* row_shr:4 into banks 1, 3 */
+      u[k] = keep + (uint32_t)r;
+    }
+  }
+  {
+    const bool b = (lane >> 3) & 1;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const uint32_t keep = b ? u[2 + k] : u[k], send = b ? u[k] : u[2 + k];
+      int r = __builtin_amdgcn_update_dpp(0, (int)send, 0x108, 0xF, 0x3, false);   /* row_shl:8 into banks 0, 1 */
+      r = __builtin_amdgcn_update_dpp(r, (int)send, 0x118, 0xF, 0xC, false);       /* row_shr:8 into banks 2, 3 */
+      u[k] = keep + (uint32_t)r;
+    }
+  }
+  {
+    const bool b = (lane >> 4) & 1;
+    const uint32_t keep = b ? u[1] : u[0], send = b ? u[0] : u[1];
+    u[0] = keep + (uint32_t)__builtin_amdgcn_ds_swizzle((int)send, 0x401F);   /* bit mode: lane ^ 16 */
+  }
+  return u[0] + (uint32_t)__builtin_amdgcn_ds_bpermute((lane ^ 32) << 2, (int)u[0]);
+}
+
 /* Exact delta: the reference's sequential `delta += term` over ascending m (mcmc.c:1214,
  * 1435, 1630), computed by lane 0 of the calling wave and broadcast through its slot.
  * Zero terms are skipped (adding +-0 is exact; s is never -0.0).  Nonzero terms were
@@ -1887,7 +1961,7 @@ __device__ __forceinline__ HM hard_bits_col(const uint32_t *Pm, int M, int hl, i
 template <typename HM>
 __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, const uint32_t *Pm, const uint16_t *prem,
                                          int M, HM hbm, const int16_t *hcnt, const int16_t *nhall, int &dt0, int &dt1,
-                                         const uint32_t *hbx = nullptr)
+                                         const uint32_t *hbx, int N_)
 {
   const int i = q.i, j = q.j;
   dt0 = 0; dt1 = 0;
@@ -1906,6 +1980,17 @@ __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, 
   } else if (kind != PK_PI3) {
     const int ain = ininterval(a, i, j + 1, q.inc1, q.inc2);
     const int bin = ininterval(b, i, j + 1, q.inc1, q.inc2);
+#if SR_BF_TERMS
+    {   /* branch-free: every lane reads the three prefixes, lanes with ain == bin keep zeros */
+      const int sp = ain ? a : b;
+      const int c0 = col_pre_bf(prem, Pm, M, i), c1 = col_pre_bf(prem, Pm, M, sp), c2 = col_pre_bf(prem, Pm, M, j + 1);
+      const int O1 = c1 - c0, O2 = c2 - c1;
+      const int Z1 = (sp - i) - O1, Z2 = (j + 1 - sp) - O2;
+      const bool on = ain != bin;
+      dt1 = on ? (ain ? O1 - O2 : O2 - O1) : 0;
+      dt0 = on ? (ain ? Z2 - Z1 : Z1 - Z2) : 0;
+    }
+#else
     if (ain != bin) {
       const int sp = ain ? a : b;
       const int c0 = col_pre(prem, Pm, M, i), c1 = col_pre(prem, Pm, M, sp), c2 = col_pre(prem, Pm, M, j + 1);
@@ -1914,6 +1999,7 @@ __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, 
       if (ain) { dt1 = O1 - O2; dt0 = Z2 - Z1; }
       else { dt1 = O2 - O1; dt0 = Z1 - Z2; }
     }
+#endif
   } else {
     const int ain = ininterval(a, i, j + 1, q.inc1, q.inc2);
     const int bin = ininterval(b, i, j + 1, q.inc1, q.inc2);
@@ -1930,6 +2016,16 @@ __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, 
     const int ri = q.r0;                                   /* = i - hcnt[i] */
     const int s_lo = (xa - hcnt[xa]) - ri, s_hi = (xb - hcnt[xb]) - ri;
     auto hard_ones = [&](int lo, int hi, int &cnt) -> int {   /* hard positions in [lo, hi] */
+#if SR_BF_TERMS
+      if (!hbx) {   /* branch-free: indices clamped into the tables, an empty range counts nothing */
+        const bool e = hi < lo;
+        const int kl = hcnt[min(max(lo, 0), N_)], kh = hcnt[min(max(hi + 1, 0), N_)];
+        cnt = e ? 0 : kh - kl;
+        constexpr int HB = 8 * (int)sizeof(HM);
+        const HM km = ((kh >= HB) ? ~(HM)0 : (((HM)1 << kh) - (HM)1)) & ~((kl >= HB) ? ~(HM)0 : (((HM)1 << kl) - (HM)1));
+        return e ? 0 : (int)__popcll((uint64_t)(hbm & km));
+      }
+#endif
       if (hi < lo) { cnt = 0; return 0; }
       const int kl = hcnt[lo], kh = hcnt[hi + 1];
       cnt = kh - kl;
@@ -1944,8 +2040,21 @@ __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, 
     };
     const int wlo = max(a, i), whi = min(b - 1, j);
     const int sizeW = max(0, whi - wlo + 1);
-    const int onesW = (whi >= wlo) ? col_pre(prem, Pm, M, whi + 1) - col_pre(prem, Pm, M, wlo) : 0;
     int onesI = 0, sizeI = 0;
+#if SR_BF_TERMS
+    const int onesW = (whi >= wlo) ? col_pre_bf(prem, Pm, M, max(whi + 1, 0)) - col_pre_bf(prem, Pm, M, wlo) : 0;
+    {   /* branch-free: nhall indices and the positions read clamped into range, an empty rank range adds 0 */
+      const bool on = s_lo < s_hi;
+      const int pl = min(max((int)nhall[min(max(ri + q.Kn - s_hi, 0), N_ - 1)], 0), N_ - 1);
+      const int ph = min(max((int)nhall[min(max(ri + q.Kn - s_lo - 1, 0), N_ - 1)], 0), N_ - 1);
+      int hc;
+      const int ho = hard_ones(pl, ph, hc);
+      const int oI = col_pre_bf(prem, Pm, M, ph + 1) - col_pre_bf(prem, Pm, M, pl) - ho;
+      onesI = on ? oI : 0;
+      sizeI = on ? s_hi - s_lo : 0;
+    }
+#else
+    const int onesW = (whi >= wlo) ? col_pre(prem, Pm, M, whi + 1) - col_pre(prem, Pm, M, wlo) : 0;
     if (s_lo < s_hi) {
       const int pl = nhall[ri + q.Kn - s_hi], ph = nhall[ri + q.Kn - s_lo - 1];
       int hc;
@@ -1953,6 +2062,7 @@ __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, 
       onesI = col_pre(prem, Pm, M, ph + 1) - col_pre(prem, Pm, M, pl) - ho;
       sizeI = s_hi - s_lo;
     }
+#endif
     {
       int hc;
       const int ho = hard_ones(max(na, i), min(nb - 1, j), hc);
@@ -1977,7 +2087,7 @@ __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, 
  * each taxon's term (mcmc.c:1212-1214 reads c, d per taxon) */
 template <bool PR, bool GM, bool SP, typename XSync>
 __device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const int32_t *sab, const uint32_t *P, const uint16_t *pre,
-                                              int M, int KT, int olo, int ohi,
+                                              int M, int N, int KT, int olo, int ohi,
                                               int hl, int nh, const int16_t *hcnt, const int16_t *nhall, const uint32_t *hbx,
                                               double *cb, int *cc, double *xs,
                                               int lane, int wave, int TB, XSync &&xsync, const double *kv = nullptr,
@@ -1990,7 +2100,7 @@ __device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const i
     int dt0 = 0, dt1 = 0;
     if (m < M && ev)
       taxon_dt(kind, q, sab[m], sab[M + m], P + m, pre + m, M, kind == PK_PI3 ? hard_bits_col<uint64_t>(P + m, M, hl, nh) : 0ull,
-               hcnt, nhall, dt0, dt1, hbx);
+               hcnt, nhall, dt0, dt1, hbx, N);
     CD Km = K;
     if (kv && m < M) { Km.c = kv[m]; Km.d = kv[M + m]; Km.cc = kx[m]; Km.dd = kx[M + m]; }
     const double tv = (m < M && ev) ? qval(dt0, -dt0, dt1, -dt1, Km) : 0.0;
@@ -2720,7 +2830,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 q.Kn = hf ? qb.Kn : qa.Kn; q.r0 = hf ? qb.r0 : qa.r0;
                 int d0 = 0, d1 = 0;
                 if ((hf ? vb : va) && tx < M)
-                  taxon_dt(prop_kind(pa), q, a1, b1, P + tx, pre + tx, M, hb1, hcnt, nhall, d0, d1, hbx);
+                  taxon_dt(prop_kind(pa), q, a1, b1, P + tx, pre + tx, M, hb1, hcnt, nhall, d0, d1, hbx, N);
                 int Xa0, Xa1, Ya, Xb0, Xb1, Yb;
                 if (prop_kind(pa) == PK_PI1) {   /* dt in {-1, 0, 1}, dt0 dt1 = 0: ballot counts per parity */
                   const uint64_t p0m = __ballot(d0 > 0), n0m = __ballot(d0 < 0);
@@ -2749,20 +2859,66 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                kind prop_kind(s), so each copy holds one kind's code and the slots' loads, ALU
                and reductions are independent */
             int d0s[16], d1s[16];
+            /* the sweep's main batch (proposals 1..15 all drawn): every slot unconditionally, vetoed slots and
+               lanes without a taxon masked afterwards, so no branch separates the slots' reads (a lane without a
+               taxon reads the half's last column: in range in LDS and in HBM) */
+            const bool full = SR_FULL_BATCH && p0 == 1 && pend == 16;
+            if (full) {
+              d0s[0] = 0; d1s[0] = 0;
+              const int mtc = min(mt, ohi - 1);
+#pragma unroll
+              for (int sI = 1; sI < 16; ++sI) {
+                const Prop q = load_prop(sI);
+                int dt0 = 0, dt1 = 0;
+                taxon_dt(prop_kind(sI), q, a1, b1, P + mtc, pre + mtc, M, hb1, hcnt, nhall, dt0, dt1, hbx, N);
+                const bool use = mt < ohi && !vetoed(sI);
+                d0s[sI] = use ? dt0 : 0; d1s[sI] = use ? dt1 : 0;
+              }
+            } else {
 #pragma unroll
             for (int sI = 0; sI < 16; ++sI) {
               d0s[sI] = 0; d1s[sI] = 0;
               if (sI >= p0 && sI < pend && !vetoed(sI)) {
                 const Prop q = load_prop(sI);
                 int dt0 = 0, dt1 = 0;
-                if (mt < ohi) taxon_dt(prop_kind(sI), q, a1, b1, P + mt, pre + mt, M, hb1, hcnt, nhall, dt0, dt1, hbx);
+                if (mt < ohi) taxon_dt(prop_kind(sI), q, a1, b1, P + mt, pre + mt, M, hb1, hcnt, nhall, dt0, dt1, hbx, N);
                 d0s[sI] = dt0; d1s[sI] = dt1;
               }
             }
+            }
             FST(3);
+            if (SR_TSUMS && pack && pend - p0 >= SR_TSUMS) {
+              /* all 16 slots' sums of one wave in one transposed reduction (wave_sum32_t): values 0-15 the packed
+                 X = (dt0 + N) | (dt1 + N) << 16, values 16-31 the nonzero counts (dt0 | dt1 != 0) | (dt0 != 0) << 16;
+                 lanes 0-31 then hold one (list, slot) total each and write it (slots outside the batch: zeros,
+                 never read) */
+              uint32_t u[32];
+#pragma unroll
+              for (int sI = 0; sI < 16; ++sI) {
+                u[sI] = (uint32_t)(d0s[sI] + N) | ((uint32_t)(d1s[sI] + N) << 16);
+                u[16 + sI] = (uint32_t)((d0s[sI] | d1s[sI]) != 0) | ((uint32_t)(d0s[sI] != 0) << 16);
+              }
+              const uint32_t v = wave_sum32_t(u, lane);
+              const int sl = (((lane >> 1) & 1) << 3) | (((lane >> 2) & 1) << 2) | (((lane >> 3) & 1) << 1) | ((lane >> 4) & 1);
+              const uint32_t pk = (uint32_t)__builtin_amdgcn_ds_bpermute(sl << 2, vpk);   /* slot sl's record */
+              if (lane < 32) {
+                int w0, w1;
+                if (!(lane & 1)) { w0 = (int)(v & 0xffffu) - 64 * N; w1 = (int)(v >> 16) - 64 * N; }
+                else {
+                  const int any = (int)(v & 0xffffu), c0 = (int)(v >> 16);
+                  const int pi = (int)(pk & 4095u), pj = (int)((pk >> 12) & 4095u);
+                  /* pi1: exact nonzero counts (dt0 dt1 = 0); the reversals: the bound of the per-slot path */
+                  const bool p1 = sl > 0 && (sl - 1) % 3 == 0;
+                  w0 = p1 ? c0 : any * 2 * (max(pi, pj) - min(pi, pj) + 1);
+                  w1 = p1 ? any - c0 : w0;
+                }
+                int *o = pw + (sl * NWV + wave) * 8 + 2 * (lane & 1);
+                o[0] = w0; o[1] = w1;
+              }
+            } else {
 #pragma unroll
             for (int sI = 0; sI < 16; ++sI) {
-              if (sI >= p0 && sI < pend && !vetoed(sI)) {
+              if (full ? sI >= 1 : (sI >= p0 && sI < pend && !vetoed(sI))) {   /* (full: vetoed sums unread) */
                 int X0, X1, Y0, Y1;
                 if (prop_kind(sI) == PK_PI1) {   /* pi1: dt in {-1, 0, 1} and dt0 dt1 = 0: every sum is a ballot count */
                   const int cp0 = (int)__popcll(__ballot(d0s[sI] > 0)), cn0 = (int)__popcll(__ballot(d0s[sI] < 0));
@@ -2791,6 +2947,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 }
               }
             }
+            }
             STAMP_K(PK_PI3);
           } else {
             /* several taxa per thread (M > TB; the HBM-column kernels): per taxon, every proposal slot
@@ -2814,7 +2971,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 if (sI >= p0 && sI < pend && !vetoed(sI)) {
                   const Prop q = load_prop(sI);
                   int dt0 = 0, dt1 = 0;
-                  if (mv) taxon_dt(prop_kind(sI), q, a, b, P + m, pre + m, M, hb, hcnt, nhall, dt0, dt1, hbx);
+                  if (mv) taxon_dt(prop_kind(sI), q, a, b, P + m, pre + m, M, hb, hcnt, nhall, dt0, dt1, hbx, N);
                   x0s[sI] += dt0; x1s[sI] += dt1; ys[sI] += abs(dt0) + abs(dt1);
                 }
               }
@@ -2929,11 +3086,11 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             }
             if (!decided || (accept && want_logl && !have_exact)) {   /* the exact sequential delta */
               if constexpr (SP)
-                dl = sr_exact_delta<PR, GM, SP>(kind, q, K, sab, P, pre, M, KTC, olo, ohi, hl, nh, hcnt, nhall, hbx,
+                dl = sr_exact_delta<PR, GM, SP>(kind, q, K, sab, P, pre, M, N, KTC, olo, ohi, hl, nh, hcnt, nhall, hbx,
                                                 cbuf + xpar * KTC * sr_chunk(PR), xb + 272 + xpar * KTC, xs, lane, wave,
                                                 TB, xsync);
               else   /* (no exchange: the one-workgroup kernels never see the split machinery) */
-                dl = sr_exact_delta<PR, GM, SP>(kind, q, K, sab, P, pre, M, KTC, 0, M, hl, nh, hcnt, nhall, hbx,
+                dl = sr_exact_delta<PR, GM, SP>(kind, q, K, sab, P, pre, M, N, KTC, 0, M, hl, nh, hcnt, nhall, hbx,
                                                 cbuf + xpar * KTC * sr_chunk(PR), ccnt + xpar * KTC, xs, lane, wave, TB,
                                                 [] {}, cv, cx);
               xpar ^= 1;
@@ -2975,7 +3132,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             const int a = sab[m], b = sab[M + m];
             int dt0, dt1;
             taxon_dt(kind, q, a, b, Pm, pre + m, M, kind == PK_PI3 ? hard_bits_col<HM>(Pm, M, hl, nh) : (HM)0, hcnt, nhall, dt0, dt1,
-                     hbx);
+                     hbx, N);
             scnt[m] += dt0; scnt[M + m] -= dt0; scnt[2 * M + m] += dt1; scnt[3 * M + m] -= dt1;
             int na_ = a, nb_ = b;   /* HBM columns: the new limits, stored below when they change */
             auto set_a = [&](int v) { if constexpr (GM) na_ = v; else sab[m] = v; };
@@ -3105,7 +3262,25 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           }
           FST(10);
           /* the hard tables only when a hard site moved (the columns' hard-site bits never change) */
-          if (hmoved) { wsync(); build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane); tvalid = false; }
+          if (hmoved) {   /* (block-uniform: every wave holds the same hard positions) */
+            wsync();
+            build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane);
+            tvalid = false;
+            if (SR_COOP_TABLES > 1 && p0 < 16) {
+              /* the proposal tables depend on the hard positions: refilled here by all threads at the next
+                 batch's start (every wave is past this batch's table reads: the terms barrier), one barrier
+                 instead of each wave refilling its own copy */
+              rng_ensure(R, 133, tid, TB);
+              tblk = R.blk;
+              toff = R.off;
+              const uint32_t sbase = (tblk & (SR_RING - 1)) * SR_MT_N + toff;
+              const int savail = min((int)((R.gen - tblk) * SR_MT_N - toff), 128);
+              for (int k = tid; k < 3 * 128; k += TB)
+                ptab_fill(ptab, ring, sbase, savail, k & 127, k >> 7, N, nh, hcnt, nhall, mdN, mdN1, md2, mdH, mdH1);
+              __syncthreads();
+              tvalid = true;
+            }
+          }
           FST(9);
           wsync();
           STAMP(7);

@@ -103,7 +103,7 @@ struct KArgs {
 /* the proposal sums of a batch of at least this many proposals by one transposed reduction per wave
    (wave_sum32_t; 0 = one reduction per slot) */
 #ifndef SR_TSUMS
-#define SR_TSUMS 0
+#define SR_TSUMS 4
 #endif
 /* the main batch's proposal slots without per-slot branches (one-taxon kernels) */
 #ifndef SR_FULL_BATCH
@@ -2914,6 +2914,21 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 }
                 int *o = pw + (sl * NWV + wave) * 8 + 2 * (lane & 1);
                 o[0] = w0; o[1] = w1;
+              }
+            } else if (SR_TSUMS && !pack && pend - p0 >= SR_TSUMS) {
+              /* N >= 512 (the packed fields would overflow): two transposed reductions of 32 plain sums each,
+                 (X0, X1) and (|dt0|, |dt1|) -- the per-slot path's exact Y */
+              uint32_t u[32];
+#pragma unroll
+              for (int sI = 0; sI < 16; ++sI) { u[sI] = (uint32_t)d0s[sI]; u[16 + sI] = (uint32_t)d1s[sI]; }
+              const int vx = (int)wave_sum32_t(u, lane);
+#pragma unroll
+              for (int sI = 0; sI < 16; ++sI) { u[sI] = (uint32_t)abs(d0s[sI]); u[16 + sI] = (uint32_t)abs(d1s[sI]); }
+              const int vy = (int)wave_sum32_t(u, lane);
+              const int sl = (((lane >> 1) & 1) << 3) | (((lane >> 2) & 1) << 2) | (((lane >> 3) & 1) << 1) | ((lane >> 4) & 1);
+              if (lane < 32) {
+                int *o = pw + (sl * NWV + wave) * 8 + (lane & 1);
+                o[0] = vx; o[2] = vy;
               }
             } else {
 #pragma unroll

@@ -105,6 +105,35 @@ struct KArgs {
 #ifndef SR_TSUMS
 #define SR_TSUMS 4
 #endif
+/* diagnostic builds (tools/build_variant.sh): SR_DOUBLE = k does phase k's work twice, the second result folded
+   in through an opaque zero (the chain is unchanged), so the time difference is the phase's marginal cost:
+   1 proposal terms, 2 proposal sums, 3 Gibbs draws, 7 the sweep's table fill */
+#ifndef SR_DOUBLE
+#define SR_DOUBLE 0
+#endif
+__device__ __forceinline__ int sr_opaque_zero()
+{
+  int z;
+  __asm__ volatile("s_mov_b32 %0, 0" : "=s"(z));
+  return z;
+}
+/* the swap drawn into one batch with proposals 1..15 (its acceptance, ~44 %, then wastes their terms) */
+#ifndef SR_MERGE_SWAP
+#define SR_MERGE_SWAP 0
+#endif
+/* at most this many proposals per batch (a smaller batch wastes fewer evaluations after an accepted proposal,
+   at the cost of more batches) */
+#ifndef SR_BATCH_MAX
+#define SR_BATCH_MAX 16
+#endif
+/* ininterval as one unsigned range compare per lane */
+#ifndef SR_ININT_FAST
+#define SR_ININT_FAST 1
+#endif
+/* an accepted pi1 applied from registers: the taxon's words, moved bit and prefix read before any write */
+#ifndef SR_APPLY_REG
+#define SR_APPLY_REG 1
+#endif
 /* the main batch's proposal slots without per-slot branches (one-taxon kernels) */
 #ifndef SR_FULL_BATCH
 #define SR_FULL_BATCH 0
@@ -1676,11 +1705,20 @@ __device__ __forceinline__ void col_pre_build(uint16_t *prem, const uint32_t *Pm
 
 __device__ __forceinline__ int ininterval(int i, int a, int b, int inc1, int inc2)   /* mcmc.c:1097-1124 */
 {
+  /* i inside the interval of ends a, b (ordered first; inc1 / inc2 include the lower / upper end): for integers
+     that is L <= i <= H with L = lo + !inc1, H = hi - !inc2, one unsigned compare per lane (the ends and flags
+     are block-uniform: scalar ALU) */
+#if SR_ININT_FAST
+  const int lo = min(a, b), hi = max(a, b);
+  const int L = lo + (inc1 ? 0 : 1), H = hi - (inc2 ? 0 : 1);
+  return (H >= L) && (uint32_t)(i - L) <= (uint32_t)(H - L);
+#else
   int r;
   if (a > b) { r = a; a = b; b = r; }
   r = inc1 ? (a <= i) : (a < i);
   if (r) r = inc2 ? (i <= b) : (i < b);
   return r;
+#endif
 }
 
 /* hard-site positions hp[0..nh) are ascending (their relative order never changes) */
@@ -2301,6 +2339,11 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           const int savail = min((int)((R.gen - tblk) * SR_MT_N - toff), 128);
           for (int k = tid; k < 4 * 128; k += TB)
             ptab_fill(ptab, ring, sbase, savail, k & 127, k >> 7, N, nh, hcnt, nhall, mdN, mdN1, md2, mdH, mdH1);
+          if (SR_DOUBLE == 7) {   /* (the same entries again) */
+            const int z = sr_opaque_zero();
+            for (int k = tid; k < 4 * 128; k += TB)
+              ptab_fill(ptab, ring, sbase, savail + z, (k & 127) + z, k >> 7, N, nh, hcnt, nhall, mdN, mdN1, md2, mdH, mdH1);
+          }
           tvalid = true;
         }
       }
@@ -2477,8 +2520,15 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 #pragma unroll
                 for (int k = 0; k < NWM; ++k) wk[k] = rw[k];
               }
-              const int res = draw_fast_s<NWM>(wk, Pm, M, N, rev, rev ? N - b0 : a0, rev ? N - na : b0, rev ? POb : POa,
-                                               rev ? ub : ua, K, tb, vA, vB, T4w, T8w, &misc[MS_FBK], d0, e0, d1, e1);
+              int res = draw_fast_s<NWM>(wk, Pm, M, N, rev, rev ? N - b0 : a0, rev ? N - na : b0, rev ? POb : POa,
+                                         rev ? ub : ua, K, tb, vA, vB, T4w, T8w, &misc[MS_FBK], d0, e0, d1, e1);
+              if (SR_DOUBLE == 3) {
+                const int z = sr_opaque_zero();
+                int q0, q1, q2, q3;
+                const int r2 = draw_fast_s<NWM>(wk, Pm, M, N, rev, (rev ? N - b0 : a0) + z, rev ? N - na : b0, rev ? POb : POa,
+                                                (rev ? ub : ua) + (double)z, K, tb, vA, vB, T4w, T8w, &misc[MS_FBK], q0, q1, q2, q3);
+                res |= r2 & z; d0 |= q0 & z; e0 |= q1 & z; d1 |= q2 & z; e1 |= q3 & z;
+              }
               t0 += d0; f0 += e0; t1 += d1; f1 += e1;
               if (rev) nb = N - res; else na = res;
             }
@@ -2691,12 +2741,14 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               vnd = (lane == 0) ? (veto ? 1 : 3) : vnd;
               voff = (lane == 0) ? (veto ? 1 : 4) : voff;
               pend = 1;
+              off = veto ? 1 : 4;
             } else {
               (void)scalar_one(0);
             }
           }
-          /* (the swap in one batch with proposals 1..15 measured no faster: profiles/r03e_ab_phasec.json) */
-          if (p0 > 0) {
+          /* (the swap in one batch with proposals 1..15 measured no faster at round 3: profiles/r03e_ab_phasec.json;
+             SR_MERGE_SWAP re-tests it) */
+          if (p0 > 0 || (SR_MERGE_SWAP && pend == 1)) {
             /* Lane-parallel draws: lane l evaluates "a pi1 / pi2 / pi3 proposal starting at word
                offset o" for o = l and o = l + 64 (words o..o+4) into ptab; the scan below then walks
                the batch's actual offsets reading those results.  ok = no GSL rejection and a nonzero
@@ -2732,7 +2784,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             int vstart = 0;
 #pragma unroll
             for (int sI = 1; sI < 16; ++sI) {
-              if (sI < p0 || pend != sI || off + 5 > 128) continue;
+              if (sI < p0 || pend != sI || off + 5 > 128 || sI >= p0 + SR_BATCH_MAX) continue;
               const int kind = prop_kind(sI);
               const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)lent, off & 63) >> (16 * (off >> 6));
               bool ok;
@@ -2766,7 +2818,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             }
           }
           for (int p = pend; p < 16; ++p) {   /* scalar path: the batch's first proposal after a fast-path stop */
-            if (p0 == 0 && p == 1) break;     /* the swap batch */
+            if (p0 == 0 && p == 1) break;     /* the swap batch (merged: the lane-parallel scan's proposals follow) */
             if (p > p0) break;                /* only the batch's first proposal goes scalar */
             if (!scalar_one(p)) break;
           }
@@ -2885,6 +2937,18 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 d0s[sI] = dt0; d1s[sI] = dt1;
               }
             }
+            if (SR_DOUBLE == 1) {
+              const int z = sr_opaque_zero();
+#pragma unroll
+              for (int sI = 0; sI < 16; ++sI) {
+                if (sI >= p0 && sI < pend && !vetoed(sI)) {
+                  const Prop q = load_prop(sI);
+                  int dt0 = 0, dt1 = 0;
+                  if (mt < ohi) taxon_dt(prop_kind(sI), q, a1 + z, b1, P + mt, pre + mt, M, hb1, hcnt, nhall, dt0, dt1, hbx, N);
+                  d0s[sI] |= dt0 & z; d1s[sI] |= dt1 & z;
+                }
+              }
+            }
             }
             FST(3);
             if (SR_TSUMS && pack && pend - p0 >= SR_TSUMS) {
@@ -2898,7 +2962,16 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 u[sI] = (uint32_t)(d0s[sI] + N) | ((uint32_t)(d1s[sI] + N) << 16);
                 u[16 + sI] = (uint32_t)((d0s[sI] | d1s[sI]) != 0) | ((uint32_t)(d0s[sI] != 0) << 16);
               }
-              const uint32_t v = wave_sum32_t(u, lane);
+              uint32_t v = wave_sum32_t(u, lane);
+              if (SR_DOUBLE == 2) {
+                const uint32_t z = (uint32_t)sr_opaque_zero();
+#pragma unroll
+                for (int sI = 0; sI < 16; ++sI) {
+                  u[sI] = (uint32_t)(d0s[sI] + N) | ((uint32_t)(d1s[sI] + N) << 16) | z;
+                  u[16 + sI] = ((uint32_t)((d0s[sI] | d1s[sI]) != 0) | ((uint32_t)(d0s[sI] != 0) << 16)) + z;
+                }
+                v |= wave_sum32_t(u, lane) & z;
+              }
               const int sl = (((lane >> 1) & 1) << 3) | (((lane >> 2) & 1) << 2) | (((lane >> 3) & 1) << 1) | ((lane >> 4) & 1);
               const uint32_t pk = (uint32_t)__builtin_amdgcn_ds_bpermute(sl << 2, vpk);   /* slot sl's record */
               if (lane < 32) {
@@ -2915,9 +2988,10 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 int *o = pw + (sl * NWV + wave) * 8 + 2 * (lane & 1);
                 o[0] = w0; o[1] = w1;
               }
-            } else if (SR_TSUMS && !pack && pend - p0 >= SR_TSUMS) {
+            } else if (SR_TSUMS && !pack && !GM && pend - p0 >= SR_TSUMS) {
               /* N >= 512 (the packed fields would overflow): two transposed reductions of 32 plain sums each,
-                 (X0, X1) and (|dt0|, |dt1|) -- the per-slot path's exact Y */
+                 (X0, X1) and (|dt0|, |dt1|) -- the per-slot path's exact Y.  Not in the HBM-column kernels: at
+                 1024 threads (128 VGPRs) the 32 live sums spill and config 5 ran 5 % slower (r05f) */
               uint32_t u[32];
 #pragma unroll
               for (int sI = 0; sI < 16; ++sI) { u[sI] = (uint32_t)d0s[sI]; u[16 + sI] = (uint32_t)d1s[sI]; }
@@ -3144,14 +3218,57 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           const int16_t *nhp = nhall + q.r0;   /* pi3: the non-hard positions of [i, j] in order */
           for (int m = (PR && hf) ? M : olo + tx; m < ohi; m += TXS) {   /* PR: the even lane of each pair; SP: own taxa */
             uint32_t *Pm = P + m;
+            uint16_t *prem = pre + m;
             const int a = sab[m], b = sab[M + m];
             int dt0, dt1;
-            taxon_dt(kind, q, a, b, Pm, pre + m, M, kind == PK_PI3 ? hard_bits_col<HM>(Pm, M, hl, nh) : (HM)0, hcnt, nhall, dt0, dt1,
+            taxon_dt(kind, q, a, b, Pm, prem, M, kind == PK_PI3 ? hard_bits_col<HM>(Pm, M, hl, nh) : (HM)0, hcnt, nhall, dt0, dt1,
                      hbx, N);
-            scnt[m] += dt0; scnt[M + m] -= dt0; scnt[2 * M + m] += dt1; scnt[3 * M + m] -= dt1;
+            /* every read of the taxon's state before its first write (the compiler cannot tell the LDS / HBM
+               arrays apart, so a read after a write waits for it: one round trip instead of one per access) */
+            const int k0 = scnt[m], k1 = scnt[M + m], k2 = scnt[2 * M + m], k3 = scnt[3 * M + m];
+            const int lo = min(i, j), hi = max(i, j), wl = lo >> 5, wh = hi >> 5;
+            /* pi1 over at most 8 words (always at N <= 256): the words [wl - 1, wh + 1], the moved bit and the
+               prefix below word wl read now; the shifted words and their prefix entries computed in registers */
+            const bool reg1 = SR_APPLY_REG && kind == PK_PI1 && wh - wl < 8;
+            uint32_t wv[10];
+            uint32_t vb = 0u;
+            int sbase = 0;
+            if (reg1) {
+#pragma unroll
+              for (int t = 0; t < 10; ++t) {
+                const int w = wl - 1 + t;
+                wv[t] = (w >= 0 && w < NW && w <= wh + 1) ? Pm[w * M] : 0u;
+              }
+              vb = (Pm[(i >> 5) * M] >> (i & 31)) & 1u;
+              sbase = prem[wl * M];
+            }
+            scnt[m] = k0 + dt0; scnt[M + m] = k1 - dt0; scnt[2 * M + m] = k2 + dt1; scnt[3 * M + m] = k3 - dt1;
             int na_ = a, nb_ = b;   /* HBM columns: the new limits, stored below when they change */
             auto set_a = [&](int v) { if constexpr (GM) na_ = v; else sab[m] = v; };
             auto set_b = [&](int v) { if constexpr (GM) nb_ = v; else sab[M + m] = v; };
+            if (reg1) {                                            /* mcmc.c:1266-1297 */
+              if (i < j) {
+                if (ii < a && a <= jj + 1) set_a(a - 1);
+                if (ii < b && b <= jj + 1) set_b(b - 1);
+              } else {
+                if (ii <= a && a <= jj) set_a(a + 1);
+                if (ii <= b && b <= jj) set_b(b + 1);
+              }
+              int sacc = sbase;
+#pragma unroll
+              for (int t = 1; t < 10; ++t) {
+                const int w = wl - 1 + t;   /* words wl .. wh */
+                if (w <= wh) {
+                  const uint32_t old = wv[t];
+                  const uint32_t sh = (i < j) ? ((old >> 1) | (wv[t + 1 < 10 ? t + 1 : 9] << 31)) : ((old << 1) | (wv[t - 1] >> 31));
+                  const uint32_t m1 = (i < j) ? range_mask(w, i, j - 1) : range_mask(w, j + 1, i);
+                  uint32_t nw = (old & ~m1) | (sh & m1);
+                  if ((j >> 5) == w) nw = (nw & ~(1u << (j & 31))) | (vb << (j & 31));
+                  Pm[w * M] = nw;
+                  if (w < wh) { sacc += __popc(nw); prem[(w + 1) * M] = (uint16_t)sacc; }   /* prefix entries (lo/32, hi/32] */
+                }
+              }
+            } else {
             if (kind == PK_PI1) {                                  /* mcmc.c:1266-1297 */
               /* the shifted words read 8 at a time before they are rewritten (one memory round trip
                  per 8 words: the HBM-column kernels) */
@@ -3218,13 +3335,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 }
               }
             }
-            if constexpr (GM) {
-              if (na_ != a) sab[m] = na_;
-              if (nb_ != b) sab[M + m] = nb_;
-            }
             {   /* the move permutes positions [lo, hi] only: prefix entries (lo/32, hi/32] change */
-              const int lo = min(i, j), hi = max(i, j), rlo = (lo >> 5) + 1, rhi = hi >> 5;
-              uint16_t *prem = pre + m;
+              const int rlo = wl + 1, rhi = wh;
               int sacc = prem[(rlo - 1) * M];
               for (int r0 = rlo; r0 <= rhi; r0 += 8) {
                 uint32_t wv[8];
@@ -3234,6 +3346,11 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 for (int t = 0; t < 8; ++t)
                   if (r0 + t <= rhi) { sacc += __popc(wv[t]); prem[(r0 + t) * M] = (uint16_t)sacc; }
               }
+            }
+            }
+            if constexpr (GM) {
+              if (na_ != a) sab[m] = na_;
+              if (nb_ != b) sab[M + m] = nb_;
             }
           }
           FST(7);

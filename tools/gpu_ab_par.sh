@@ -8,6 +8,9 @@ export TMPDIR=/tmp
 OUT=gpurun_out/$1; shift
 mkdir -p "$OUT"
 V=seriation-in-paleontological-data-using-mcmc_amd/build/var
+timeout -k 10 300 python -m pytest ${PARITY:-tests/test_gpu_parity.py} -x -q -p no:cacheprovider > "$OUT/parity_default.log" 2>&1 ||
+  { tail -30 "$OUT/parity_default.log"; exit 1; }
+echo "default: $(tail -1 "$OUT/parity_default.log")"
 for v in "$@"; do
   SERIATION_LIB=$PWD/$V/$v/libseriation.so timeout -k 10 300 python -m pytest ${PARITY:-tests/test_gpu_parity.py} -x -q \
     -p no:cacheprovider > "$OUT/parity_$v.log" 2>&1 || { tail -30 "$OUT/parity_$v.log"; exit 1; }

@@ -119,7 +119,7 @@ __device__ __forceinline__ int sr_opaque_zero()
 }
 /* the swap drawn into one batch with proposals 1..15 (its acceptance, ~44 %, then wastes their terms) */
 #ifndef SR_MERGE_SWAP
-#define SR_MERGE_SWAP 0
+#define SR_MERGE_SWAP 1
 #endif
 /* at most this many proposals per batch (a smaller batch wastes fewer evaluations after an accepted proposal,
    at the cost of more batches) */

@@ -55,8 +55,9 @@ def test_manycd_several_taxa_per_thread():
 
 
 def test_manycd_session_records_and_checkpoint(tmp_path):
-    """Session API: fetch_cd_vectors equals the oracle's per-taxon records; a checkpoint (version 4, with the
-    per-taxon c, d) restores into a session that continues exactly; restoring it as manycd = 0 is refused."""
+    """Session API: fetch_cd_vectors equals the oracle's per-taxon records; a checkpoint (version 6: the per-taxon
+    c, d and the buffered records) restores into a session that holds the first 3 records and continues exactly;
+    restoring it as manycd = 0 is refused."""
     text = _text("g10s10.txt")
     ds = sa.Dataset.parse(text)
     seeds = [7, 8]
@@ -74,12 +75,13 @@ def test_manycd_session_records_and_checkpoint(tmp_path):
     ri2, rd2 = r.fetch_records()
     rv2 = r.fetch_cd_vectors()
     r.close()
-    np.testing.assert_array_equal(ri2, ri[:, 3:])
+    np.testing.assert_array_equal(ri2, ri)   # the checkpoint's 3 records, then the 3 continued ones
+    assert np.array_equal(rd2.view(np.uint64), rd.view(np.uint64))
     with sa.Session.restore(ds, ck, calls_per_launch=6, manycd=1) as r3:   # the state API: every taxon's c, d
         st = r3.state(1)
         assert np.array_equal(st["cv"].view(np.uint64), rv[1, 2, :ds.M].view(np.uint64))
         assert np.array_equal(st["dv"].view(np.uint64), rv[1, 2, ds.M:].view(np.uint64))
-    assert np.array_equal(rv2.view(np.uint64), rv[:, 3:].view(np.uint64))
+    assert np.array_equal(rv2.view(np.uint64), rv.view(np.uint64))
     for k, sd in enumerate(seeds):
         o = oracle_ref.run_chain(text, sd, 0, 6, manycd=1)
         np.testing.assert_array_equal(ri[k], o["rec_int"])

@@ -121,6 +121,9 @@ __device__ __forceinline__ int sr_opaque_zero()
 #ifndef SR_MERGE_SWAP
 #define SR_MERGE_SWAP 1
 #endif
+#ifndef SR_MERGE_SWAP_GM   /* ... also in the HBM-column kernels (their proposal terms cost far more) */
+#define SR_MERGE_SWAP_GM 0
+#endif
 /* at most this many proposals per batch (a smaller batch wastes fewer evaluations after an accepted proposal,
    at the cost of more batches) */
 #ifndef SR_BATCH_MAX
@@ -2329,7 +2332,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
          own copy as before (ptab_fill).  The previous sweep's readers are past the end-of-sweep barrier. */
       uint32_t tblk = 0u, toff = 0u;
       bool tvalid = false;
-      if constexpr (!MCD && SR_COOP_TABLES) {
+      if constexpr (!MCD && !GM && SR_COOP_TABLES) {   /* (GM: its registers spill 37 more VGPRs, r05l) */
         if (8 + 2 * M + SR_RNG_SLACK <= (SR_RING - 1) * SR_MT_N - (SR_MT_N - 1)) {
           rng_ensure(R, 8 + 2 * M + SR_RNG_SLACK, tid, TB);
           const uint32_t sp = R.off + 8u + 2u * (uint32_t)M;
@@ -2748,7 +2751,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           }
           /* (the swap in one batch with proposals 1..15 measured no faster at round 3: profiles/r03e_ab_phasec.json;
              SR_MERGE_SWAP re-tests it) */
-          if (p0 > 0 || (SR_MERGE_SWAP && pend == 1)) {
+          if (p0 > 0 || (SR_MERGE_SWAP && (!GM || SR_MERGE_SWAP_GM) && pend == 1)) {
             /* Lane-parallel draws: lane l evaluates "a pi1 / pi2 / pi3 proposal starting at word
                offset o" for o = l and o = l + 64 (words o..o+4) into ptab; the scan below then walks
                the batch's actual offsets reading those results.  ok = no GSL rejection and a nonzero
@@ -2951,7 +2954,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             }
             }
             FST(3);
-            if (SR_TSUMS && pack && pend - p0 >= SR_TSUMS) {
+            if (SR_TSUMS && !GM && pack && pend - p0 >= SR_TSUMS) {   /* (GM: see below) */
               /* all 16 slots' sums of one wave in one transposed reduction (wave_sum32_t): values 0-15 the packed
                  X = (dt0 + N) | (dt1 + N) << 16, values 16-31 the nonzero counts (dt0 | dt1 != 0) | (dt0 != 0) << 16;
                  lanes 0-31 then hold one (list, slot) total each and write it (slots outside the batch: zeros,
@@ -3229,7 +3232,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             const int lo = min(i, j), hi = max(i, j), wl = lo >> 5, wh = hi >> 5;
             /* pi1 over at most 8 words (always at N <= 256): the words [wl - 1, wh + 1], the moved bit and the
                prefix below word wl read now; the shifted words and their prefix entries computed in registers */
-            const bool reg1 = SR_APPLY_REG && kind == PK_PI1 && wh - wl < 8;
+            const bool reg1 = SR_APPLY_REG && !GM && kind == PK_PI1 && wh - wl < 8;   /* (GM: registers, r05l) */
             uint32_t wv[10];
             uint32_t vb = 0u;
             int sbase = 0;

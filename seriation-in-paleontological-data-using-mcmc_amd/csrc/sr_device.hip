@@ -107,7 +107,8 @@ struct KArgs {
 #endif
 /* diagnostic builds (tools/build_variant.sh): SR_DOUBLE = k does phase k's work twice, the second result folded
    in through an opaque zero (the chain is unchanged), so the time difference is the phase's marginal cost:
-   1 proposal terms, 2 proposal sums, 3 Gibbs draws, 7 the sweep's table fill */
+   1 proposal terms, 2 proposal sums, 3 Gibbs draws, 4 the c, d draws, 5 K and the step tables, 7 the sweep's
+   table fill, 8 the hard-site tables after a hard site moved */
 #ifndef SR_DOUBLE
 #define SR_DOUBLE 0
 #endif
@@ -123,6 +124,18 @@ __device__ __forceinline__ int sr_opaque_zero()
 #endif
 #ifndef SR_MERGE_SWAP_GM   /* ... also in the HBM-column kernels (their proposal terms cost far more) */
 #define SR_MERGE_SWAP_GM 0
+#endif
+/* the c, d draws' ziggurat steps read before the phase-A barrier (measured +0.5 %: off, r05q) */
+#ifndef SR_CD_PREFETCH
+#define SR_CD_PREFETCH 0
+#endif
+/* pi1's taxon change by one unsigned compare per limit */
+#ifndef SR_PI1_FAST
+#define SR_PI1_FAST 1
+#endif
+/* the per-lane "owns a taxon" test as a constant in shape-specialised kernels whose taxa fill the block */
+#ifndef SR_OWN_CONST
+#define SR_OWN_CONST 1
 #endif
 /* at most this many proposals per batch (a smaller batch wastes fewer evaluations after an accepted proposal,
    at the cost of more batches) */
@@ -581,31 +594,49 @@ __device__ __forceinline__ double readlane_f64(double v, int l)
  * four gammas took their two-word path and the 8 words are resident -- otherwise returns false
  * and the caller runs the sequential draws from the same cursor.  Wave-level: every wave of the
  * block computes it identically (no block synchronisation). */
+/* The part of draw_cd_fast that does not depend on the counts: lane g (& 3)'s two words from the cursor and its
+ * ziggurat step (x, and whether the word falls inside the box), read before the phase-A barrier so that the table
+ * lookups (global constant memory) overlap the wait.  ok = false: the words are not resident (no prefetch). */
+struct CDPre { uint32_t w1; double x; bool box, ok; };
+__device__ __forceinline__ CDPre cd_prefetch(const DRng &r, int lane)
+{
+  CDPre p{};
+  p.ok = r.blk + (r.off + 7) / SR_MT_N < r.gen;
+  if (!p.ok) return p;
+  const uint32_t base = (r.blk & (SR_RING - 1)) * SR_MT_N + r.off;
+  const int g = lane & 3;
+  uint32_t i0 = base + 2 * g, i1 = base + 2 * g + 1;
+  i0 = (i0 >= SR_RING * SR_MT_N) ? i0 - SR_RING * SR_MT_N : i0;
+  i1 = (i1 >= SR_RING * SR_MT_N) ? i1 - SR_RING * SR_MT_N : i1;
+  const uint32_t k = sr_mt_temper(r.ring[i0]);
+  p.w1 = sr_mt_temper(r.ring[i1]);
+  uint32_t i = k & 0xFF;
+  const uint32_t j = (k >> 8) & 0xFFFFFF;
+  const int sign = (i & 0x80) ? +1 : -1;
+  i &= 0x7f;
+  const double x = j * c_zig_w[i];
+  p.box = j < c_zig_k[i];
+  p.x = sign * 1.0 * x;
+  return p;
+}
+
 __device__ __forceinline__ bool draw_cd_fast(DRng &r, double &c, double &d, int f1, int t0, int f0, int t1,
-                                             const sr_mtab &tb, int lane)
+                                             const sr_mtab &tb, int lane, CDPre pf = CDPre{})
 {
 #ifdef SR_FORCE_EXACT   /* test build: the sequential GSL draws */
   return false;
 #endif
   if (r.blk + (r.off + 7) / SR_MT_N >= r.gen) return false;
   if ((f1 == 0 && t0 == 0) || (f0 == 0 && t1 == 0)) return false;   /* a Johnk beta: the sequential path */
-  const uint32_t base = (r.blk & (SR_RING - 1)) * SR_MT_N + r.off;
+  if (!pf.ok) pf = cd_prefetch(r, lane);
   const int g = lane & 3;
-  uint32_t i0 = base + 2 * g, i1 = base + 2 * g + 1;
-  i0 = (i0 >= SR_RING * SR_MT_N) ? i0 - SR_RING * SR_MT_N : i0;
-  i1 = (i1 >= SR_RING * SR_MT_N) ? i1 - SR_RING * SR_MT_N : i1;
-  const uint32_t k = sr_mt_temper(r.ring[i0]), w1 = sr_mt_temper(r.ring[i1]);
+  const uint32_t w1 = pf.w1;
   const int cnt = (g == 0) ? f1 : (g == 1) ? t0 : (g == 2) ? f0 : t1;
   const double a = 1. + (double)cnt;                   /* d_samplebeta: gamma(1. + a) */
   const double dd = a - 1.0 / 3.0;
   const double cc = (1.0 / 3.0) / __builtin_sqrt(dd);
-  uint32_t i = k & 0xFF;
-  const uint32_t j = (k >> 8) & 0xFFFFFF;
-  const int sign = (i & 0x80) ? +1 : -1;
-  i &= 0x7f;
-  double x = j * c_zig_w[i];
-  bool ok = j < c_zig_k[i];
-  x = sign * 1.0 * x;
+  const double x = pf.x;
+  bool ok = pf.box;
   double v = 1.0 + cc * x;
   ok = ok && v > 0 && w1 != 0u;
   v = v * v * v;
@@ -2010,6 +2041,14 @@ __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, 
     const int ii = q.ii, jj = q.jj;
     const int v = (Pm[(i >> 5) * M] >> (i & 31)) & 1;
     int sgn = 0;   /* +1: the moved site enters the taxon's range, -1: leaves it */
+#if SR_PI1_FAST
+    {   /* i < j: a, b tested against [ii + 1, jj + 1], sgn = ain - bin; i > j: against [ii, jj], sgn = bin - ain
+           (block-uniform bounds: one unsigned compare per limit) */
+      const int up = i < j ? 1 : 0, L = ii + up, span = jj - ii;
+      const int ain = (uint32_t)(a - L) <= (uint32_t)span, bin = (uint32_t)(b - L) <= (uint32_t)span;
+      sgn = up ? ain - bin : bin - ain;
+    }
+#else
     if (i < j) {
       const bool ain = (ii < a && a <= jj + 1), bin = (ii < b && b <= jj + 1);
       sgn = (ain && !bin) ? 1 : ((!ain && bin) ? -1 : 0);
@@ -2017,6 +2056,7 @@ __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, 
       const bool ain = (ii <= a && a <= jj), bin = (ii <= b && b <= jj);
       sgn = (!ain && bin) ? 1 : ((ain && !bin) ? -1 : 0);
     }
+#endif
     if (v) dt1 = sgn; else dt0 = -sgn;
   } else if (kind != PK_PI3) {
     const int ain = ininterval(a, i, j + 1, q.inc1, q.inc2);
@@ -2350,6 +2390,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           tvalid = true;
         }
       }
+      /* the c, d draws' ziggurat steps, before the phase-A barrier (their table loads overlap the wait) */
+      const CDPre cdpf = (SR_CD_PREFETCH && !MCD && !GM) ? cd_prefetch(R, lane) : CDPre{};
       FST(15);
       /* ============ phase A: totals and the c, d draws (mcmc.c:768-825) */
       {
@@ -2396,7 +2438,14 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           c = cv[0];
           d = cv[M];
           if (tid == 0) { misc[MS_ACC + 0] += M - 1; misc[MS_ACC + 1] += M - 1; }   /* samplec returns M (mcmc.c:785) */
-        } else if (!draw_cd_fast(R, c, d, s3, s0, s1, s2, tb, lane)) {
+        } else if (SR_DOUBLE == 4 && [&] {   /* (diagnostic: the fast draw once more on a copy of the cursor) */
+                     DRng R2 = R;
+                     double c2 = c, d2 = d;
+                     const int z = sr_opaque_zero();
+                     const bool ok2 = draw_cd_fast(R2, c2, d2, s3 + z, s0, s1, s2, tb, lane);
+                     c += (ok2 ? c2 : 1.0) * (double)z; d += d2 * (double)z;
+                     return false; }()) {
+        } else if (!draw_cd_fast(R, c, d, s3, s0, s1, s2, tb, lane, cdpf)) {
           if (tid == 0) misc[MS_CDSEQ]++;
           double cd2[2] = {c, d};
           for (int k = 0; k < 2; ++k)
@@ -2418,7 +2467,23 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       const double vA = (K.d - K.cc) * 1.4426950408889634;
       const double vB = (K.dd - K.c) * 1.4426950408889634;
       const double r2 = sr_exp_m(oddl ? K.c - K.dd : K.cc - K.d, &tb);
-      const double rA = readlane_f64(r2, 0), rB = readlane_f64(r2, 1);   /* 2^-vA, 2^-vB */
+      double rA = readlane_f64(r2, 0), rB = readlane_f64(r2, 1);   /* 2^-vA, 2^-vB */
+      if (SR_DOUBLE == 5) {   /* (diagnostic: K's logs and exps and the step tables once more) */
+        const double z = (double)sr_opaque_zero();
+        const double l1b = sr_log_m(1. - sr_exp_m((oddl ? d : c) + z, &tb), &tb);
+        const double r2b = sr_exp_m((oddl ? K.c - K.dd : K.cc - K.d) + z + l1b * z, &tb);
+        rA += readlane_f64(r2b, 0) * z; rB += readlane_f64(r2b, 1) * z;
+        if constexpr (NWM > 0 && !SH8) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int e = lane + 64 * q;
+            double pr = 1.0, sm = 0.0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) { sm = sm + pr; pr = pr * (((e >> k) & 1) ? rB : rA); }
+            *reinterpret_cast<double2 *>(T8w + 2 * e) = make_double2(sm, pr);
+          }
+        }
+      }
       /* PR: one shared copy of the tables, built by waves 0-4 (T8 quarters, T4), then a barrier */
       if ((!PR || wave == 4) && lane < 16) {   /* per-wave tables for 4 walk entries with bits = lane */
         double pr = 1.0, sm = 1.0;
@@ -2855,7 +2920,11 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           const bool one = NWM > 0 || (SP && TB == 1024) || (SP && ohi - olo <= TB) || M <= TXS;
           int a1 = 0, b1 = 0;
           const HM hb1 = hbc;
-          if (one && mt < ohi) { a1 = sab[mt]; b1 = sab[M + mt]; }
+          /* every thread owns a taxon when the shape is compiled in and fills the block (the bench kernel): the
+             ownership test is then a constant, not an exec mask re-set around every slot */
+          constexpr bool ALLOWN = SR_OWN_CONST && !SP && !PR && SR_FM > 0 && SR_FM >= TB;
+          const bool own = ALLOWN || mt < ohi;
+          if (one && own) { a1 = sab[mt]; b1 = sab[M + mt]; }
           FST(13);
 #if defined(SR_STAMP_DRAWS)
           STAMP(5);
@@ -2936,7 +3005,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               if (sI >= p0 && sI < pend && !vetoed(sI)) {
                 const Prop q = load_prop(sI);
                 int dt0 = 0, dt1 = 0;
-                if (mt < ohi) taxon_dt(prop_kind(sI), q, a1, b1, P + mt, pre + mt, M, hb1, hcnt, nhall, dt0, dt1, hbx, N);
+                if (own) taxon_dt(prop_kind(sI), q, a1, b1, P + mt, pre + mt, M, hb1, hcnt, nhall, dt0, dt1, hbx, N);
                 d0s[sI] = dt0; d1s[sI] = dt1;
               }
             }
@@ -3400,6 +3469,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           if (hmoved) {   /* (block-uniform: every wave holds the same hard positions) */
             wsync();
             build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane);
+            if (SR_DOUBLE == 8) { wsync(); build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane); }
             tvalid = false;
             if (SR_COOP_TABLES > 1 && p0 < 16) {
               /* the proposal tables depend on the hard positions: refilled here by all threads at the next

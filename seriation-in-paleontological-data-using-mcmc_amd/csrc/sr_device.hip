@@ -1406,7 +1406,8 @@ __device__ __forceinline__ int draw_fast_s(const uint32_t (&wk)[NWM], const uint
       ckr[k] = S;
 #pragma unroll
       for (int g = 0; g < 4; ++g) t[g] = tn[g];
-      __builtin_amdgcn_sched_barrier(0);   /* one word of reads ahead, no more (register pressure) */
+      __builtin_amdgcn_sched_barrier(0);   /* one word of reads ahead, no more (register pressure; two words
+                                              ahead: 10 -> 19 VGPR spills, +0.7 %, profiles/r05r_ab_gibbs_ahead.json) */
     }
     /* the partial byte (c8 entries) when its word lies in the window */
     const int nfull = (L + 1) >> 3, c8 = (L + 1) & 7, kb = nfull >> 2;
@@ -2730,6 +2731,9 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           /* one proposal drawn by block-uniform scalar code at word offset `off` (false: not enough
              resident words) */
           auto scalar_one = [&](int p) -> bool {
+#if defined(SR_STAMPS) && !defined(SR_STAMP_FINE)
+              if (tid == 0) misc[43] += 1;   /* proposals drawn by the scalar path */
+#endif
               need_vw();
               const int kind = prop_kind(p);
               bool bad = false;
@@ -2827,6 +2831,9 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             if (!tvalid || delta < 0 || delta + 5 * (16 - p0) + 5 > 128) {
               delta = 0;
               tblk = rblk; toff = roff; tvalid = true;
+#if defined(SR_STAMPS) && !defined(SR_STAMP_FINE)
+              if (tid == 0) misc[42] += 1;   /* table refills in phase C */
+#endif
 #pragma unroll
               for (int h = 0; h < 2; ++h)
                 ptab_fill(ptab, ring, base, avail, lane + 64 * h, -1, N, nh, hcnt, nhall, mdN, mdN1, md2, mdH, mdH1);
@@ -2891,6 +2898,9 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             if (!scalar_one(p)) break;
           }
           pend = __builtin_amdgcn_readfirstlane(pend);
+#if defined(SR_STAMPS) && !defined(SR_STAMP_FINE)   /* batch statistics (slots 40-41 are the fine build's) */
+          if (tid == 0 && pend > p0) { misc[40] += 1; misc[41] += (unsigned long long)(pend - p0); }
+#endif
           FST(2);
           STAMP_D(4);
           if (pend == p0) {   /* not enough resident words for one proposal: make more, retry */
@@ -3528,6 +3538,9 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 #ifdef SR_STAMPS
   if (tid == 0) { A.dbg[blockIdx.x * 17 * 8 + 0] += misc[MS_NEXACT]; for (int q_ = 0; q_ < 4; ++q_) A.dbg[blockIdx.x * 17 * 8 + 1 + q_] += misc[MS_FBK + q_];
                   for (int q_ = 0; q_ < 3; ++q_) A.dbg[blockIdx.x * 17 * 8 + 5 + q_] += misc[40 + q_];
+#if !defined(SR_STAMP_FINE) && !defined(SR_STAMP_GIBBS)
+                  if (TB <= 512) A.dbg[(blockIdx.x * 17 + 9) * 8 + 0] += misc[43];   /* (row 9: no wave's stamps) */
+#endif
 #if defined(SR_STAMP_GIBBS) || defined(SR_STAMP_FINE)
                   for (int q_ = 0; q_ < 3; ++q_) A.dbg[blockIdx.x * 17 * 8 + 5 + q_] = misc[MS_FBK + 26 + q_];
                   A.dbg[blockIdx.x * 17 * 8 + 4] = misc[MS_FBK + 29];

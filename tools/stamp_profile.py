@@ -24,14 +24,24 @@ calls = int(sys.argv[3]) if len(sys.argv) > 3 else 10
 tbk = int(sys.argv[4]) if len(sys.argv) > 4 else 0
 ds = sa.Dataset.load(path, maxs=0)   # full lines (the bench loads synthetic data the same way)
 s = sa.Session(ds, list(range(1, C + 1)), calls_per_launch=calls, block_threads=tbk)
+warm = int(os.environ.get("SR_WARM", "0"))   # extra calls before the profiled ones (a chain's steady state)
 s.run(calls)
 s.sync()
+out0 = np.zeros((C, 17, 8), np.uint64)
+if warm:   # steady state: the counters of the profiled launch alone (they accumulate over launches)
+    s.run(warm)
+    s.sync()
+    sa.lib().sr_session_debug_counters(s.h, out0.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)))
+acc0 = np.array([s.accept_counts(c) for c in range(C)], np.float64)
 t0 = time.perf_counter()
 s.run(calls)
 s.sync()
 wall = time.perf_counter() - t0
+acc = (np.array([s.accept_counts(c) for c in range(C)], np.float64) - acc0).mean(0) / (calls * 10)
 out = np.zeros((C, 17, 8), np.uint64)
 sa.lib().sr_session_debug_counters(s.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)))
+if warm:   # x / 2 / sweeps below: the profiled launch's counters, doubled
+    out = (out - out0) * np.uint64(2)
 sweeps = calls * 10
 nw = s.block_threads // 64
 per = out[:, 1:1 + nw, :].astype(np.float64) / 2.0 / sweeps   # [chain, wave, phase] cycles per sweep
@@ -47,9 +57,11 @@ print("  total wave0 %.0f; exact-sum fallbacks/sweep %.3f; sampleab fallbacks/sw
     out[:, 0, 1].astype(np.float64).mean() / 2 / sweeps))
 print("  sampleab fallback reasons/sweep: prev %.3f here %.3f S0 %.3f (rest = no crossing in segment)" % tuple(
     out[:, 0, 2 + q].astype(np.float64).mean() / 2 / sweeps for q in range(3)))
-ev = out[:, 0, 5:8].astype(np.float64).mean(0) / 2 / sweeps
-print("  term evaluations/sweep: pi1 %.2f pi2/swap %.2f pi3 %.2f" % tuple(ev))
-print("  cycles per evaluation (wave-mean): pi1 %.0f pi2/swap %.0f pi3 %.0f" % tuple(per[:, :, 4 + k].mean() / max(ev[k], 1e-9) for k in range(3)))
+if not os.environ.get("SR_FINE") and not os.environ.get("SR_GIBBS_STATS"):
+    bs = np.concatenate([out[:, 9, 0:1], out[:, 0, 5:8]], axis=1).astype(np.float64).mean(0) / 2 / sweeps   # coarse builds
+    print("  phase-C batches/sweep %.3f; proposals drawn into batches/sweep %.2f (16 needed); proposal-table refills/sweep "
+          "%.3f; scalar-path proposals/sweep %.3f" % (bs[1], bs[2], bs[3], bs[0]))
+print("  accepted per sweep (profiled launch, chain mean): pi1 %.3f pi2 %.3f swap %.3f pi3 %.3f" % tuple(acc[3:7]))
 if os.environ.get("SR_GIBBS_STATS"):
     h = out[:, 0, :].astype(np.float64).sum(0)
     nd = max(h[4], 1)

@@ -95,6 +95,13 @@ struct KArgs {
 #ifndef SR_CKG
 #define SR_CKG 4
 #endif
+/* split-chain kernels (SP): the Gibbs checkpoints in LDS ((N/32)/SR_CKG + 1 slots per thread) instead of HBM
+   scratch, room made by one block-shared copy of the hard-site and 4-step tables instead of one per wave
+   (16 waves: 66 KB + 20 KB at N = 1024).  The checkpoints were a quarter of config 5's HBM traffic (all of its
+   writes) and two dependent memory round trips of every walk's pass 2 (0 = HBM scratch, round 4's form) */
+#ifndef SR_SP_LCK
+#define SR_SP_LCK 1
+#endif
 /* the sweep's proposal tables filled by all threads before the phase-A barrier, and the swap drawn from them
    (round 5; 0 = each wave fills its own at the start of phase C and the swap takes the scalar path) */
 #ifndef SR_COOP_TABLES
@@ -196,14 +203,18 @@ __host__ __device__ static constexpr inline int sr_ckstride(int M, int TB) { ret
  * owner-thread access, L2/MALL-resident) and get no LDS slot */
 /* taxa per exact-delta chunk (one wave's taxa): 64, or 32 in the pair kernels (two lanes per taxon) */
 __host__ __device__ static constexpr inline int sr_chunk(bool pr) { return pr ? 32 : 64; }
-__host__ __device__ static constexpr inline Lay sr_layout(int N, int M, int NW, int TB, bool gm, bool pr = false, int nh = 0)
+/* lck (split-chain kernels, SR_SP_LCK): shared hard-site and 4-step tables, Gibbs checkpoints in LDS */
+__host__ __device__ static constexpr inline int sr_lck_slots(int N) { return (N >> 5) / SR_CKG + 1; }
+__host__ __device__ static constexpr inline Lay sr_layout(int N, int M, int NW, int TB, bool gm, bool pr = false, int nh = 0,
+                                                          bool lck = false)
 {
   Lay L{};
   size_t o = 0;
   const int CH = sr_chunk(pr), KT = (M + CH - 1) / CH, NWV = TB / 64;
   const size_t g = gm ? 0 : 1;
+  lck = lck && gm;
   /* step tables: one copy per wave, or one shared copy behind a barrier (pair kernels: 16 waves) */
-  const size_t NT = pr ? 1 : NWV;
+  const size_t NT = (pr || lck) ? 1 : NWV;
   L.tab = o;   o = sr_al16(o + 512 * sizeof(double));   /* glibc exp/log tables */
   L.cbuf = o;  o = sr_al16(o + g * 2 * KT * CH * sizeof(double));       /* [2][KT*CH] by proposal parity */
   L.lbuf = o;  o = sr_al16(o + g * M * sizeof(double));
@@ -211,9 +222,10 @@ __host__ __device__ static constexpr inline Lay sr_layout(int N, int M, int NW, 
   L.P = o;     o = sr_al16(o + g * NW * M * 4);
   L.rpi0 = o;  o = sr_al16(o + (size_t)N * 4);
   L.rpi1 = o;  o = sr_al16(o + (size_t)N * 4);
-  L.ht = o;    o = sr_al16(o + (size_t)NWV * (2 * N + 2) * 2);           /* per wave: hcnt[N+1], nhall[N] (int16) */
+  L.ht = o;    o = sr_al16(o + (lck ? 1 : (size_t)NWV) * (2 * N + 2) * 2);   /* per wave (lck: shared): hcnt[N+1], nhall[N] (int16) */
   const size_t rw = (pr || sr_regwalk(N, M, TB, gm, nh)) ? 1 : 0;   /* register walks (pair kernels too): byte tables instead of LDS checkpoints */
-  L.ck = o;    o = sr_al16(o + g * (1 - rw) * ((N >> 5) + 1) * sr_ckstride(M, TB) * sizeof(double));
+  L.ck = o;    o = sr_al16(o + g * (1 - rw) * ((N >> 5) + 1) * sr_ckstride(M, TB) * sizeof(double) +
+                           (lck ? (size_t)sr_lck_slots(N) * TB * sizeof(double) : 0));
   L.ccnt = o;  o = sr_al16(o + (size_t)2 * KT * 4);
   L.sab = o;   o = sr_al16(o + g * 2 * M * 4);
   L.scnt = o;  o = sr_al16(o + g * 4 * M * 4);
@@ -1918,8 +1930,9 @@ struct Prop { int i, j, ii, jj, inc1, inc2, Kn, r0; };   /* r0: non-hard rank of
 
 /* Per-wave hard-site tables (hard positions hp[] ascending): hcnt[x] = #hard positions < x
  * (x = 0..N), nhall[r] = position of the r-th non-hard position.  Rebuilt whenever hp moves. */
+/* wt: this wave writes hcnt / nhall (false: another wave writes the block's shared copy; hbw is always the wave's) */
 __device__ __forceinline__ void build_hard_tables(const int *hp, int nh, int N, int NW, uint32_t *hbw, int16_t *hcnt,
-                                                  int16_t *nhall, int lane)
+                                                  int16_t *nhall, int lane, bool wt = true)
 {
   /* hard bitmap (hbw: this wave's NW words, NW <= 64), then ranks by ballot over positions */
   for (int w = lane; w < NW; w += 64) hbw[w] = 0u;
@@ -1932,8 +1945,8 @@ __device__ __forceinline__ void build_hard_tables(const int *hp, int nh, int N, 
     const bool h = (x < N) && ((hbw[min(x, N - 1) >> 5] >> (x & 31)) & 1u);
     const uint64_t msk = __ballot(h && x < N);
     const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(msk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msk, 0u));
-    if (x <= N) hcnt[x] = (int16_t)(base + below);
-    if (x < N && !h) nhall[x - (base + below)] = (int16_t)x;
+    if (wt && x <= N) hcnt[x] = (int16_t)(base + below);
+    if (wt && x < N && !h) nhall[x - (base + below)] = (int16_t)x;
     base += __popcll(msk);
   }
   wsync();
@@ -2237,7 +2250,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   const int olo = SP ? half * sr_sp_half(M) : 0, ohi = SP ? min(M, olo + sr_sp_half(M)) : M;   /* own taxa */
   const int mt = olo + tx;   /* own taxon, one-taxon-per-thread kernels */
   const int KTC = (M + sr_chunk(PR) - 1) / sr_chunk(PR);   /* exact-delta chunks */
-  const Lay L = sr_layout(N, M, NW, TB, GM, PR, nh);
+  constexpr bool LCK = SP && SR_SP_LCK;   /* shared hard-site / 4-step tables, Gibbs checkpoints in LDS */
+  const Lay L = sr_layout(N, M, NW, TB, GM, PR, nh, LCK);
   double *tabs = (double *)(smem + L.tab);
   /* GM: the per-taxon arrays are the chain's HBM state itself (P, a/b, counts: updated in
      place) or its HBM scratch; otherwise LDS copies loaded here and stored at the end */
@@ -2248,12 +2262,12 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   int32_t *rpiA = (int32_t *)(smem + L.rpi0);
   int32_t *rpiB = (int32_t *)(smem + L.rpi1);
   uint16_t *pre = GM ? A.gpre + (size_t)chain * sr_gm_pre(M, NW) : (uint16_t *)(smem + L.pre);   /* column prefix ones */
-  int16_t *hcnt = (int16_t *)(smem + L.ht) + wave * (2 * N + 2);    /* this wave's hard-site tables */
+  int16_t *hcnt = (int16_t *)(smem + L.ht) + (LCK ? 0 : wave) * (2 * N + 2);    /* this wave's (LCK: the block's) hard-site tables */
   int16_t *nhall = hcnt + N + 1;
-  const int CKS = SP ? 2 * TB : sr_ckstride(M, TB);   /* SP: slots [half TB + tid] */
+  const int CKS = LCK ? TB : SP ? 2 * TB : sr_ckstride(M, TB);   /* SP: slots [half TB + tid] (LCK: [tid] in LDS) */
   using CKT = typename std::conditional<GM && SR_CK32, float, double>::type;   /* Gibbs checkpoints: f32 in HBM scratch, f64 in LDS */
-  CKT *ckb = GM ? (CKT *)A.gck + (size_t)chain * (SP ? sr_sp_ck(N, TB) : sr_gm_ck(N, M, TB)) : (CKT *)(void *)(smem + L.ck);
-  const int ckslot = SP ? half * TB + tid : tid;   /* this thread's Gibbs checkpoint slots */
+  CKT *ckb = (GM && !LCK) ? (CKT *)A.gck + (size_t)chain * (SP ? sr_sp_ck(N, TB) : sr_gm_ck(N, M, TB)) : (CKT *)(void *)(smem + L.ck);
+  const int ckslot = (SP && !LCK) ? half * TB + tid : tid;   /* this thread's Gibbs checkpoint slots */
   int *ccnt = (int *)(smem + L.ccnt);
   int32_t *sab = GM ? A.ab + (size_t)chain * 2 * M : (int32_t *)(smem + L.sab);     /* a[M], b[M] */
   int32_t *scnt = GM ? A.cnt + (size_t)chain * 4 * M : (int32_t *)(smem + L.scnt);  /* t0[M], f0[M], t1[M], f1[M] */
@@ -2261,7 +2275,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   int *hp = (int *)(smem + L.hpw) + wave * NHC;   /* this wave's copy of the hard positions */
   uint32_t *hbw = (uint32_t *)(smem + L.hbw) + wave * NW;   /* this wave's hard bitmap */
   const uint32_t *hbx = nh > SR_NHMAX ? hbw : nullptr;   /* many hard sites: hard ones from the bitmap */
-  double *T4w = (double *)(smem + L.t4) + (PR ? 0 : wave) * T4STRIDE;   /* this wave's (PR: the block's) 4-step tables */
+  double *T4w = (double *)(smem + L.t4) + ((PR || LCK) ? 0 : wave) * T4STRIDE;   /* this wave's (PR, LCK: the block's) 4-step tables */
   constexpr bool SH8 = PR || GM;   /* one shared copy of the 8-step tables (built by waves 0-3, then a barrier) */
   double *T8w = (double *)(smem + L.t8) + (SH8 ? 0 : wave) * T8STRIDE;   /* this wave's (SH8: the block's) 8-step tables */
   int *part = (int *)(smem + L.part);
@@ -2350,7 +2364,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   int xpar = 0;     /* parity of the double-buffered exact-delta term lists */
   __syncthreads();
 
-  build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane);
+  build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane, !LCK || wave == 0);   /* (LCK: read after the phase-A barrier) */
   for (int m = olo + tid; m < ohi; m += TB) col_pre_build(pre + m, P + m, M, NW);   /* own columns */
   {
     const int hl0 = (lane < nh) ? hp[lane] : 0;   /* loaded with every lane active */
@@ -2486,7 +2500,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         }
       }
       /* PR: one shared copy of the tables, built by waves 0-4 (T8 quarters, T4), then a barrier */
-      if ((!PR || wave == 4) && lane < 16) {   /* per-wave tables for 4 walk entries with bits = lane */
+      if (((!PR && !LCK) || wave == 4) && lane < 16) {   /* per-wave (PR, LCK: shared) tables for 4 walk entries with bits = lane */
         double pr = 1.0, sm = 1.0;
         double sc[5];
         sc[0] = 0.0;
@@ -3477,9 +3491,10 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           FST(10);
           /* the hard tables only when a hard site moved (the columns' hard-site bits never change) */
           if (hmoved) {   /* (block-uniform: every wave holds the same hard positions) */
-            wsync();
-            build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane);
-            if (SR_DOUBLE == 8) { wsync(); build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane); }
+            if constexpr (LCK) __syncthreads(); else wsync();   /* LCK: every wave is past its reads of the shared tables */
+            build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane, !LCK || wave == 0);
+            if constexpr (LCK) __syncthreads();                 /* ... and the next batch reads the new ones */
+            if (SR_DOUBLE == 8 && !LCK) { wsync(); build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane); }
             tvalid = false;
             if (SR_COOP_TABLES > 1 && p0 < 16) {
               /* the proposal tables depend on the hard positions: refilled here by all threads at the next
@@ -3870,6 +3885,9 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
     const int want = e ? atoi(e) : -1;
     const int Mh = sr_sp_half(st->M);
     sr_kfn ks = sr_pick_kernel(TB, st->N, st->M, true, false, st->nh, true);
+    /* the split kernels' own layout (SR_SP_LCK: checkpoints in LDS, shared tables): they must fit it */
+    const size_t lds_sp = sr_layout(st->N, st->M, st->NW, TB, true, false, st->nh, SR_SP_LCK != 0).total;
+    if (lds_sp > 160 * 1024) ks = nullptr;
     /* SR_SPLIT=2 (experiment, opt-in only): 512-thread halves of up to two blocks' taxa, several taxa per
        thread (256 VGPRs, 8 waves per CU; measured slower) -- never chosen without it */
     if (want != 0 && !d->mcd && d->gm && ks && ((TB == 1024 && Mh <= TB) || (want == 2 && TB == 512 && Mh <= 2 * TB)) &&
@@ -3879,11 +3897,12 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
       const int grid = 16 * ((st->nchains + 7) / 8);
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
           hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device) == hipSuccess && coop &&
-          hipFuncSetAttribute((const void *)ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d->lds) == hipSuccess &&
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)ks, TB, d->lds) == hipSuccess &&
+          hipFuncSetAttribute((const void *)ks, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sp) == hipSuccess &&
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)ks, TB, lds_sp) == hipSuccess &&
           grid <= occ * cus) {
         d->sp = 1;
         d->grid = grid;
+        d->lds = lds_sp;
         /* SR_COOP=0: an ordinary launch of the same grid (rocprofv3's kernel tracer crashes at
            process exit after cooperative launches; on an otherwise idle GPU the grid is resident
            anyway, and a wait that times out fails the session instead of hanging) */

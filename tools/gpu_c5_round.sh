@@ -3,6 +3,7 @@
 # same command and separate FETCH / WRITE / SQ --pmc passes.  The profiled runs launch the split
 # grid without the cooperative API (SR_COOP=0: rocprofv3's tracer crashes at exit after cooperative
 # launches, gpurun_out/r03w/c5_prof.log); the bench line itself is the default (cooperative) launch.
+# plus an L2 hit / miss pass (TCC_HIT_sum, TCC_MISS_sum).
 #   tools/gpu_c5_round.sh NAME  ->  tools/pmc_summary.py gpurun_out/NAME profiles/NAME_config5 --tag c5_
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -18,7 +19,8 @@ SR_COOP=0 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv
 SR_COOP=0 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/c5_fetch" -o f -- python3 $C5 > "$OUT/c5_fetch.log" 2>&1 &&
 SR_COOP=0 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/c5_write" -o w -- python3 $C5 > "$OUT/c5_write.log" 2>&1 &&
 SR_COOP=0 timeout -s KILL 180 rocprofv3 --pmc $SQA --output-format csv -d "$OUT/c5_sq" -o s -- python3 $C5 > "$OUT/c5_sq.log" 2>&1 &&
-SR_COOP=0 timeout -s KILL 180 rocprofv3 --pmc $SQB --output-format csv -d "$OUT/c5_sq_b" -o s -- python3 $C5 > "$OUT/c5_sq_b.log" 2>&1
+SR_COOP=0 timeout -s KILL 180 rocprofv3 --pmc $SQB --output-format csv -d "$OUT/c5_sq_b" -o s -- python3 $C5 > "$OUT/c5_sq_b.log" 2>&1 &&
+SR_COOP=0 timeout -s KILL 180 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/c5_l2" -o l -- python3 $C5 > "$OUT/c5_l2.log" 2>&1
 rc=$?
 echo "exit $rc"
 exit $rc

@@ -2,7 +2,8 @@
 # One full GPU-box pass for the round record: smoke, GPU test suite, the default bench (CPU
 # baseline included), rocprofv3 --kernel-trace --stats of that SAME bench command, separate --pmc
 # passes over it (HBM FETCH_SIZE / WRITE_SIZE; SQ issue / park split, instruction mix, LDS), then
-# config 5 (1024 x 2048, HBM columns) with its own bench line, kernel trace and FETCH / WRITE / SQ
+# config 5 (1024 x 2048, HBM columns) with its own bench line (after 3 warm-up launches, and after 100 = 2000
+# sweeps: c5_bench_ss, nearer the steady state of the headline's 1000 warm-up calls), kernel trace and FETCH / WRITE / SQ
 # passes.  Every GPU step has its own time limit; the chain stops at the first failure.
 #   tools/gpu_round.sh NAME [skip-tests]  ->  tools/pmc_summary.py gpurun_out/NAME profiles/NAME
 #                                            tools/pmc_summary.py gpurun_out/NAME profiles/NAME_config5 --tag c5_
@@ -29,7 +30,8 @@ timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o w -- python3 $P > "$OUT/pmc_write.log" 2>&1 &&
 timeout -s KILL 180 rocprofv3 --pmc $SQA --output-format csv -d "$OUT/pmc_sq" -o s -- python3 $P > "$OUT/pmc_sq.log" 2>&1 &&
 timeout -s KILL 180 rocprofv3 --pmc $SQB --output-format csv -d "$OUT/pmc_sq_b" -o s -- python3 $P > "$OUT/pmc_sq_b.log" 2>&1 &&
-timeout -k 10 200 python $C5B > "$OUT/c5_bench.json" 2> "$OUT/c5_bench.err" && export SR_COOP=0 &&   # (rocprofv3 + cooperative launch: see tools/gpu_c5_round.sh)
+timeout -k 10 200 python $C5B > "$OUT/c5_bench.json" 2> "$OUT/c5_bench.err" &&
+timeout -k 10 300 python ${C5B/--warmup 3/--warmup 100} > "$OUT/c5_bench_ss.json" 2> "$OUT/c5_bench_ss.err" && export SR_COOP=0 &&   # (rocprofv3 + cooperative launch: see tools/gpu_c5_round.sh)
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c5_prof" -o c5 -- python3 $C5 > "$OUT/c5_prof.log" 2>&1 &&
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/c5_fetch" -o f -- python3 $C5 > "$OUT/c5_fetch.log" 2>&1 &&
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/c5_write" -o w -- python3 $C5 > "$OUT/c5_write.log" 2>&1 &&

@@ -72,7 +72,8 @@ struct KArgs {
   unsigned long long *dbg;   /* SR_STAMPS builds: [chain][16] cycles per phase */
   uint16_t *gpre;            /* gm variant scratch, per chain: column prefix tables */
   uint32_t *pkey;            /* [chain][2] Philox keys (SR_F_RNG_PHILOX), else null: MT19937 */
-  void *gck;                     /* gm variant scratch: Gibbs checkpoints (SR_CK32: f32, half the bytes of the scratch stream) */
+  void *gck;                     /* gm variant scratch: Gibbs checkpoints (SR_CK32: f32, half the bytes of the scratch stream;
+                                    unused by the split kernels, whose checkpoints are in LDS: SR_SP_LCK) */
   double *glbuf, *gcbuf;         /* gm variant scratch: logl terms, exact-delta terms */
   int *xflag, *xbuf, *xerr;      /* split chains (SP kernels): [chain][2] progress flags, exchange slots, timeout flag */
   double *cdv, *cdx;   /* manycd (MCD kernels): [chain][2M] per-taxon c, d (state); [chain][2M] their cc, dd (scratch) */
@@ -3934,7 +3935,9 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
     rc |= dev_alloc_copy(d, &A.gpre, (const uint16_t *)nullptr, C * sr_gm_pre(st->M, st->NW));
     using CKT = typename std::conditional<SR_CK32 != 0, float, double>::type;
     CKT *gck = nullptr;
-    rc |= dev_alloc_copy(d, &gck, (const CKT *)nullptr, C * (d->sp ? sr_sp_ck(st->N, TB) : sr_gm_ck(st->N, st->M, TB)));
+    /* (split kernels with SR_SP_LCK keep their checkpoints in LDS: no HBM scratch) */
+    rc |= dev_alloc_copy(d, &gck, (const CKT *)nullptr,
+                         C * (d->sp ? (SR_SP_LCK ? 0 : sr_sp_ck(st->N, TB)) : sr_gm_ck(st->N, st->M, TB)));
     A.gck = gck;
     rc |= dev_alloc_copy(d, &A.glbuf, (const double *)nullptr, C * st->M);
     rc |= dev_alloc_copy(d, &A.gcbuf, (const double *)nullptr, C * sr_gm_cbuf(st->M));

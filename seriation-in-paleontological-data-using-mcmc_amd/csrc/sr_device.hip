@@ -103,6 +103,11 @@ struct KArgs {
 #ifndef SR_SP_LCK
 #define SR_SP_LCK 1
 #endif
+/* HBM-column kernels: one block-shared copy of the hard-site and 4-step tables (16 waves at 1024 threads held 64 N
+   bytes of per-wave hard tables: at N ~ 1250 the layout passed 160 KB; shared, N reaches 4095 at 1024 threads) */
+#ifndef SR_GM_SHARED
+#define SR_GM_SHARED 1
+#endif
 /* the sweep's proposal tables filled by all threads before the phase-A barrier, and the swap drawn from them
    (round 5; 0 = each wave fills its own at the start of phase C and the swap takes the scalar path) */
 #ifndef SR_COOP_TABLES
@@ -204,7 +209,7 @@ __host__ __device__ static constexpr inline int sr_ckstride(int M, int TB) { ret
  * owner-thread access, L2/MALL-resident) and get no LDS slot */
 /* taxa per exact-delta chunk (one wave's taxa): 64, or 32 in the pair kernels (two lanes per taxon) */
 __host__ __device__ static constexpr inline int sr_chunk(bool pr) { return pr ? 32 : 64; }
-/* lck (split-chain kernels, SR_SP_LCK): shared hard-site and 4-step tables, Gibbs checkpoints in LDS */
+/* gm (SR_GM_SHARED): shared hard-site and 4-step tables; lck (split-chain kernels, SR_SP_LCK): Gibbs checkpoints in LDS */
 __host__ __device__ static constexpr inline int sr_lck_slots(int N) { return (N >> 5) / SR_CKG + 1; }
 __host__ __device__ static constexpr inline Lay sr_layout(int N, int M, int NW, int TB, bool gm, bool pr = false, int nh = 0,
                                                           bool lck = false)
@@ -214,8 +219,9 @@ __host__ __device__ static constexpr inline Lay sr_layout(int N, int M, int NW, 
   const int CH = sr_chunk(pr), KT = (M + CH - 1) / CH, NWV = TB / 64;
   const size_t g = gm ? 0 : 1;
   lck = lck && gm;
+  const bool sht = gm && SR_GM_SHARED;
   /* step tables: one copy per wave, or one shared copy behind a barrier (pair kernels: 16 waves) */
-  const size_t NT = (pr || lck) ? 1 : NWV;
+  const size_t NT = (pr || sht) ? 1 : NWV;
   L.tab = o;   o = sr_al16(o + 512 * sizeof(double));   /* glibc exp/log tables */
   L.cbuf = o;  o = sr_al16(o + g * 2 * KT * CH * sizeof(double));       /* [2][KT*CH] by proposal parity */
   L.lbuf = o;  o = sr_al16(o + g * M * sizeof(double));
@@ -223,7 +229,7 @@ __host__ __device__ static constexpr inline Lay sr_layout(int N, int M, int NW, 
   L.P = o;     o = sr_al16(o + g * NW * M * 4);
   L.rpi0 = o;  o = sr_al16(o + (size_t)N * 4);
   L.rpi1 = o;  o = sr_al16(o + (size_t)N * 4);
-  L.ht = o;    o = sr_al16(o + (lck ? 1 : (size_t)NWV) * (2 * N + 2) * 2);   /* per wave (lck: shared): hcnt[N+1], nhall[N] (int16) */
+  L.ht = o;    o = sr_al16(o + (sht ? 1 : (size_t)NWV) * (2 * N + 2) * 2);   /* per wave (gm: shared): hcnt[N+1], nhall[N] (int16) */
   const size_t rw = (pr || sr_regwalk(N, M, TB, gm, nh)) ? 1 : 0;   /* register walks (pair kernels too): byte tables instead of LDS checkpoints */
   L.ck = o;    o = sr_al16(o + g * (1 - rw) * ((N >> 5) + 1) * sr_ckstride(M, TB) * sizeof(double) +
                            (lck ? (size_t)sr_lck_slots(N) * TB * sizeof(double) : 0));
@@ -2251,7 +2257,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   const int olo = SP ? half * sr_sp_half(M) : 0, ohi = SP ? min(M, olo + sr_sp_half(M)) : M;   /* own taxa */
   const int mt = olo + tx;   /* own taxon, one-taxon-per-thread kernels */
   const int KTC = (M + sr_chunk(PR) - 1) / sr_chunk(PR);   /* exact-delta chunks */
-  constexpr bool LCK = SP && SR_SP_LCK;   /* shared hard-site / 4-step tables, Gibbs checkpoints in LDS */
+  constexpr bool LCK = SP && SR_SP_LCK;   /* Gibbs checkpoints in LDS */
+  constexpr bool SHT = GM && SR_GM_SHARED;   /* block-shared hard-site / 4-step tables */
   const Lay L = sr_layout(N, M, NW, TB, GM, PR, nh, LCK);
   double *tabs = (double *)(smem + L.tab);
   /* GM: the per-taxon arrays are the chain's HBM state itself (P, a/b, counts: updated in
@@ -2263,7 +2270,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   int32_t *rpiA = (int32_t *)(smem + L.rpi0);
   int32_t *rpiB = (int32_t *)(smem + L.rpi1);
   uint16_t *pre = GM ? A.gpre + (size_t)chain * sr_gm_pre(M, NW) : (uint16_t *)(smem + L.pre);   /* column prefix ones */
-  int16_t *hcnt = (int16_t *)(smem + L.ht) + (LCK ? 0 : wave) * (2 * N + 2);    /* this wave's (LCK: the block's) hard-site tables */
+  int16_t *hcnt = (int16_t *)(smem + L.ht) + (SHT ? 0 : wave) * (2 * N + 2);    /* this wave's (SHT: the block's) hard-site tables */
   int16_t *nhall = hcnt + N + 1;
   const int CKS = LCK ? TB : SP ? 2 * TB : sr_ckstride(M, TB);   /* SP: slots [half TB + tid] (LCK: [tid] in LDS) */
   using CKT = typename std::conditional<GM && SR_CK32, float, double>::type;   /* Gibbs checkpoints: f32 in HBM scratch, f64 in LDS */
@@ -2276,7 +2283,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   int *hp = (int *)(smem + L.hpw) + wave * NHC;   /* this wave's copy of the hard positions */
   uint32_t *hbw = (uint32_t *)(smem + L.hbw) + wave * NW;   /* this wave's hard bitmap */
   const uint32_t *hbx = nh > SR_NHMAX ? hbw : nullptr;   /* many hard sites: hard ones from the bitmap */
-  double *T4w = (double *)(smem + L.t4) + ((PR || LCK) ? 0 : wave) * T4STRIDE;   /* this wave's (PR, LCK: the block's) 4-step tables */
+  double *T4w = (double *)(smem + L.t4) + ((PR || SHT) ? 0 : wave) * T4STRIDE;   /* this wave's (PR, SHT: the block's) 4-step tables */
   constexpr bool SH8 = PR || GM;   /* one shared copy of the 8-step tables (built by waves 0-3, then a barrier) */
   double *T8w = (double *)(smem + L.t8) + (SH8 ? 0 : wave) * T8STRIDE;   /* this wave's (SH8: the block's) 8-step tables */
   int *part = (int *)(smem + L.part);
@@ -2365,7 +2372,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   int xpar = 0;     /* parity of the double-buffered exact-delta term lists */
   __syncthreads();
 
-  build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane, !LCK || wave == 0);   /* (LCK: read after the phase-A barrier) */
+  build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane, !SHT || wave == 0);   /* (SHT: read after the phase-A barrier) */
   for (int m = olo + tid; m < ohi; m += TB) col_pre_build(pre + m, P + m, M, NW);   /* own columns */
   {
     const int hl0 = (lane < nh) ? hp[lane] : 0;   /* loaded with every lane active */
@@ -2501,7 +2508,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         }
       }
       /* PR: one shared copy of the tables, built by waves 0-4 (T8 quarters, T4), then a barrier */
-      if (((!PR && !LCK) || wave == 4) && lane < 16) {   /* per-wave (PR, LCK: shared) tables for 4 walk entries with bits = lane */
+      if ((PR ? wave == 4 : (!SHT || wave == NWV - 1)) && lane < 16) {   /* per-wave (PR, SHT: shared) tables for 4 walk entries with bits = lane */
         double pr = 1.0, sm = 1.0;
         double sc[5];
         sc[0] = 0.0;
@@ -3492,10 +3499,10 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           FST(10);
           /* the hard tables only when a hard site moved (the columns' hard-site bits never change) */
           if (hmoved) {   /* (block-uniform: every wave holds the same hard positions) */
-            if constexpr (LCK) __syncthreads(); else wsync();   /* LCK: every wave is past its reads of the shared tables */
-            build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane, !LCK || wave == 0);
-            if constexpr (LCK) __syncthreads();                 /* ... and the next batch reads the new ones */
-            if (SR_DOUBLE == 8 && !LCK) { wsync(); build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane); }
+            if constexpr (SHT) __syncthreads(); else wsync();   /* SHT: every wave is past its reads of the shared tables */
+            build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane, !SHT || wave == 0);
+            if constexpr (SHT) __syncthreads();                 /* ... and the next batch reads the new ones */
+            if (SR_DOUBLE == 8 && !SHT) { wsync(); build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane); }
             tvalid = false;
             if (SR_COOP_TABLES > 1 && p0 < 16) {
               /* the proposal tables depend on the hard positions: refilled here by all threads at the next

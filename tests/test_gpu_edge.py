@@ -124,7 +124,8 @@ def test_steep_walks(N, M, noise, seeds, burnin):
 # Split chains (two workgroups per chain exchanging sums through HBM flags), forced on small HBM-column
 # cases at 1024 threads (SR_SPLIT=1; by default only chains of 1025..2048 taxa split).
 SPLIT_CASES = [("m700", 64, 700, 4), ("m1100", 64, 1100, 6), ("nh64", 150, 1200, 64), ("lds-walk", 600, 1300, 7),
-               ("many-hard", 60, 1500, 30)]
+               ("many-hard", 60, 1500, 30), ("n1300", 1300, 1100, 8)]   # n1300: 11 LDS checkpoint slots per thread,
+# the largest split layout of round 5 (the per-wave hard tables of round 4's layout did not fit 160 KB there)
 
 
 @pytest.mark.parametrize("name,N,M,nh", SPLIT_CASES, ids=["split-" + c[0] for c in SPLIT_CASES])
@@ -152,6 +153,31 @@ def test_split_chain_parity(monkeypatch, name, N, M, nh):
             s.run(5)
             counts[mode] = [np.concatenate([s.accept_counts(k), s.fallback_counts(k)]) for k in range(len(seeds))]
     np.testing.assert_array_equal(np.array(counts["1"]), np.array(counts["0"]))
+
+
+@pytest.mark.parametrize("N,M,nh", [(3000, 1100, 9), (1700, 1500, 70)], ids=["n3000", "n1700-nh70"])
+def test_hbm_columns_1024_threads_long_columns(monkeypatch, N, M, nh):
+    """HBM columns at 1024 threads with long columns (round 5: one block-shared copy of the hard-site and 4-step
+    tables; the per-wave copies of 16 waves passed 160 KB of LDS at N ~ 1250, so these shapes had no kernel).
+    One-workgroup kernel (SR_SPLIT=0) and, where its layout fits, the split kernel, both against the oracle."""
+    text = make_text(N, M, nh, seed=N * 7 + M)
+    ds = sa.Dataset.parse(text, maxs=0)
+    seeds = [3, 11]
+    orc = [oracle_ref.run_chain(text, s, 2, 3, maxs=0) for s in seeds]
+    for mode in ("0", "1"):
+        monkeypatch.setenv("SR_SPLIT", mode)
+        with sa.Session(ds, seeds, block_threads=1024, columns="hbm") as s:
+            assert s.variant == "hbm"
+            kern = s.kernel
+        if mode == "1" and kern != "split":
+            continue   # (the split layout, LDS checkpoints included, does not fit at this N)
+        summ, (ri, rd) = sa.run_chains(ds, seeds, burnin_calls=2, sample_calls=3, keep_records=True,
+                                       block_threads=1024, columns="hbm")
+        for k, o in enumerate(orc):
+            assert o["rc"] == 0
+            np.testing.assert_array_equal(ri[k], o["rec_int"], err_msg="N %d mode %s seed %d" % (N, mode, seeds[k]))
+            assert np.array_equal(rd[k].view(np.uint64), o["rec_dbl"].view(np.uint64)), (N, mode, seeds[k])
+            assert summ[k]["consistent"] == 0
 
 
 @pytest.mark.parametrize("name,N,M,nh", [("m1100", 64, 1100, 6), ("many-hard", 60, 1500, 30)], ids=["split512-m1100",

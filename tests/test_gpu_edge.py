@@ -155,7 +155,8 @@ def test_split_chain_parity(monkeypatch, name, N, M, nh):
     np.testing.assert_array_equal(np.array(counts["1"]), np.array(counts["0"]))
 
 
-@pytest.mark.parametrize("N,M,nh", [(3000, 1100, 9), (1700, 1500, 70)], ids=["n3000", "n1700-nh70"])
+@pytest.mark.parametrize("N,M,nh", [(3000, 1100, 9), (1700, 1500, 70), (1024, 3000, 200)],
+                         ids=["n3000", "n1700-nh70", "n1024-nh200"])
 def test_hbm_columns_1024_threads_long_columns(monkeypatch, N, M, nh):
     """HBM columns at 1024 threads with long columns (round 5: one block-shared copy of the hard-site and 4-step
     tables; the per-wave copies of 16 waves passed 160 KB of LDS at N ~ 1250, so these shapes had no kernel).

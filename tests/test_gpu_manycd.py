@@ -47,6 +47,11 @@ def test_manycd_hbm_columns():
     _check(make_text(90, 300, 6, seed=90300), [3, 4], tb=1, ts=3, columns="hbm")
 
 
+def test_manycd_long_columns():
+    """N = 1400 (HBM columns at 1024 threads: a layout that exists since round 5's block-shared hard-site tables)."""
+    _check(make_text(1400, 150, 9, seed=1400150), [6], tb=1, ts=2)
+
+
 def test_manycd_several_taxa_per_thread():
     """M > 1024: two taxa per thread (HBM columns, the one-workgroup kernel; no split chains for manycd)."""
     ds = _check(make_text(48, 1300, 4, seed=481300), [5], tb=1, ts=2)

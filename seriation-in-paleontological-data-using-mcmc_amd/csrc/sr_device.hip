@@ -2234,7 +2234,7 @@ __device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const i
  * 1 + t0_m) / Beta(1 + f0_m, 1 + t1_m), every Gibbs draw, logl term and proposal delta with its taxon's own
  * coefficients -- the exact paths throughout (per-taxon step ratios leave nothing to share or certify by
  * integer sums).  One taxon or more per thread, one workgroup per chain, LDS or HBM columns. */
-template <int TB, int NWM, bool GM, bool PR = false, bool SP = false, bool MCD = false>
+template <int TB, int NWM, bool GM, bool PR = false, bool SP = false, bool MCD = false, bool LK = false>
 __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 {
   static_assert(!SP || (GM && !PR && NWM == 0), "split chains: HBM-column kernels only");
@@ -2257,7 +2257,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   const int olo = SP ? half * sr_sp_half(M) : 0, ohi = SP ? min(M, olo + sr_sp_half(M)) : M;   /* own taxa */
   const int mt = olo + tx;   /* own taxon, one-taxon-per-thread kernels */
   const int KTC = (M + sr_chunk(PR) - 1) / sr_chunk(PR);   /* exact-delta chunks */
-  constexpr bool LCK = SP && SR_SP_LCK;   /* Gibbs checkpoints in LDS */
+  constexpr bool LCK = SP && LK;   /* Gibbs checkpoints in LDS (split kernels whose layout fits them, SR_SP_LCK) */
   constexpr bool SHT = GM && SR_GM_SHARED;   /* block-shared hard-site / 4-step tables */
   const Lay L = sr_layout(N, M, NW, TB, GM, PR, nh, LCK);
   double *tabs = (double *)(smem + L.tab);
@@ -3626,6 +3626,7 @@ __constant__ unsigned long long sr_spec_abi[4] = {
 
 struct srk_dev {
   int device, N, M, NW, nh, nchains, TB, TPT, rec_cap, gm, pr, sp, grid, coop;
+  int lck;                 /* split kernels: Gibbs checkpoints in LDS (LK kernels) */
   int mcd;                 /* manycd: per-taxon c, d (MCD kernels) */
   int jit;                 /* the launch uses the shape-specialised kernel (srk_spec_load) */
   int jemb;                /* ... and its code object is the one embedded in the library */
@@ -3660,7 +3661,8 @@ static bool sr_pair_ok(int N, int M)
   return sr_nwm(N) == 9 && M > 256 && M <= 512;
 }
 
-static sr_kfn sr_pick_kernel(int TB, int N, int M, bool gm, bool pr, int nh, bool sp = false, bool mcd = false)
+static sr_kfn sr_pick_kernel(int TB, int N, int M, bool gm, bool pr, int nh, bool sp = false, bool mcd = false,
+                             bool lk = false)
 {
   if (mcd) {   /* manycd: the generic one-workgroup kernels at 1024 threads */
     if (TB != 1024 || pr || sp) return nullptr;
@@ -3669,8 +3671,14 @@ static sr_kfn sr_pick_kernel(int TB, int N, int M, bool gm, bool pr, int nh, boo
   }
   if (pr) return (TB == 1024 && !gm) ? (sr_kfn)sr_sweep_kernel<1024, 9, false, true> : nullptr;
 #ifndef SR_STAMPS
-  if (sp) return !gm ? nullptr : TB == 1024 ? (sr_kfn)sr_sweep_kernel<1024, 0, true, false, true>
-                 : TB == 512 ? (sr_kfn)sr_sweep_kernel<512, 0, true, false, true> : nullptr;
+  if (sp) {   /* LK: checkpoints in LDS (where the layout fits them), else in HBM scratch */
+    if (!gm) return nullptr;
+    if (TB == 1024) return lk ? (sr_kfn)sr_sweep_kernel<1024, 0, true, false, true, false, true>
+                              : (sr_kfn)sr_sweep_kernel<1024, 0, true, false, true>;
+    if (TB == 512) return lk ? (sr_kfn)sr_sweep_kernel<512, 0, true, false, true, false, true>
+                             : (sr_kfn)sr_sweep_kernel<512, 0, true, false, true>;
+    return nullptr;
+  }
 #else
   if (sp) return nullptr;   /* (stamp builds index their counters by block) */
 #endif
@@ -3783,7 +3791,7 @@ static int srk_spec_load(srk_dev *d, const srk_spec_src *src)
   const sr_spec_shape &s = src->s;
   char log[4700];
   char name[128];
-  snprintf(name, sizeof name, "_Z15sr_sweep_kernelILi%dELi%dELb0ELb0ELb0ELb0EEv5KArgs", s.TB, s.NWM);
+  snprintf(name, sizeof name, "_Z15sr_sweep_kernelILi%dELi%dELb0ELb0ELb0ELb0ELb0EEv5KArgs", s.TB, s.NWM);
   unsigned long long abi[4] = {0, 0, 0, 0};
   const unsigned long long want[4] = {
       sizeof(KArgs), (unsigned long long)s.TB | ((unsigned long long)s.NWM << 16),
@@ -3892,9 +3900,12 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
     const char *e = getenv("SR_SPLIT");
     const int want = e ? atoi(e) : -1;
     const int Mh = sr_sp_half(st->M);
-    sr_kfn ks = sr_pick_kernel(TB, st->N, st->M, true, false, st->nh, true);
-    /* the split kernels' own layout (SR_SP_LCK: checkpoints in LDS, shared tables): they must fit it */
-    const size_t lds_sp = sr_layout(st->N, st->M, st->NW, TB, true, false, st->nh, SR_SP_LCK != 0).total;
+    /* the split kernels' own layout: Gibbs checkpoints in LDS where they fit (SR_SP_LCK; up to N ~ 1300 at 1024
+       threads), else in HBM scratch (round 4's form; any N) */
+    const size_t lds_lk = sr_layout(st->N, st->M, st->NW, TB, true, false, st->nh, true).total;
+    const bool lk = SR_SP_LCK && lds_lk <= 160 * 1024;
+    const size_t lds_sp = lk ? lds_lk : sr_layout(st->N, st->M, st->NW, TB, true, false, st->nh, false).total;
+    sr_kfn ks = sr_pick_kernel(TB, st->N, st->M, true, false, st->nh, true, false, lk);
     if (lds_sp > 160 * 1024) ks = nullptr;
     /* SR_SPLIT=2 (experiment, opt-in only): 512-thread halves of up to two blocks' taxa, several taxa per
        thread (256 VGPRs, 8 waves per CU; measured slower) -- never chosen without it */
@@ -3909,6 +3920,7 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
           hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)ks, TB, lds_sp) == hipSuccess &&
           grid <= occ * cus) {
         d->sp = 1;
+        d->lck = lk ? 1 : 0;
         d->grid = grid;
         d->lds = lds_sp;
         /* SR_COOP=0: an ordinary launch of the same grid (rocprofv3's kernel tracer crashes at
@@ -3942,9 +3954,9 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
     rc |= dev_alloc_copy(d, &A.gpre, (const uint16_t *)nullptr, C * sr_gm_pre(st->M, st->NW));
     using CKT = typename std::conditional<SR_CK32 != 0, float, double>::type;
     CKT *gck = nullptr;
-    /* (split kernels with SR_SP_LCK keep their checkpoints in LDS: no HBM scratch) */
+    /* (split kernels with their checkpoints in LDS: no HBM scratch) */
     rc |= dev_alloc_copy(d, &gck, (const CKT *)nullptr,
-                         C * (d->sp ? (SR_SP_LCK ? 0 : sr_sp_ck(st->N, TB)) : sr_gm_ck(st->N, st->M, TB)));
+                         C * (d->sp ? (d->lck ? 0 : sr_sp_ck(st->N, TB)) : sr_gm_ck(st->N, st->M, TB)));
     A.gck = gck;
     rc |= dev_alloc_copy(d, &A.glbuf, (const double *)nullptr, C * st->M);
     rc |= dev_alloc_copy(d, &A.gcbuf, (const double *)nullptr, C * sr_gm_cbuf(st->M));
@@ -3960,7 +3972,7 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
     rc |= dev_alloc_copy(d, &A.xerr, (const int *)nullptr, 1);
   }
   if (rc) { srk_destroy(d); return -5; }
-  sr_kfn k = sr_pick_kernel(TB, st->N, st->M, d->gm != 0, d->pr != 0, st->nh, d->sp != 0, d->mcd != 0);
+  sr_kfn k = sr_pick_kernel(TB, st->N, st->M, d->gm != 0, d->pr != 0, st->nh, d->sp != 0, d->mcd != 0, d->lck != 0);
   if (hipFuncSetAttribute((const void *)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)d->lds) != hipSuccess) {
     srk_destroy(d);
     return -5;
@@ -3991,7 +4003,7 @@ extern "C" int srk_run(srk_dev *d, int calls, int spc, int save, int rec_base)
   HIPCHK(hipSetDevice(d->device));
   KArgs A = d->args;
   A.calls = calls; A.spc = spc; A.save = save; A.rec_base = rec_base;
-  sr_kfn k = sr_pick_kernel(d->TB, d->N, d->M, d->gm != 0, d->pr != 0, d->nh, d->sp != 0, d->mcd != 0);
+  sr_kfn k = sr_pick_kernel(d->TB, d->N, d->M, d->gm != 0, d->pr != 0, d->nh, d->sp != 0, d->mcd != 0, d->lck != 0);
   if (d->sp) HIPCHK(hipMemsetAsync(A.xflag, 0, (size_t)d->nchains * 2 * sizeof(int), d->stream));   /* exchange sequence restarts */
   if (d->have_events) HIPCHK(hipEventRecord(d->ev0, d->stream));
   if (d->jit) {   /* the run-time specialised kernel (same arguments; LDS columns: one workgroup per chain) */

@@ -33,7 +33,7 @@ def _subject():
 
 SUBJECT = _subject()
 HIPCC = "/opt/rocm/bin/hipcc"
-BENCH_KERNEL = b"_Z15sr_sweep_kernelILi512ELi9ELb0ELb0ELb0ELb0EEv5KArgs"
+BENCH_KERNEL = b"_Z15sr_sweep_kernelILi512ELi9ELb0ELb0ELb0ELb0ELb0EEv5KArgs"
 
 needs_hipcc = pytest.mark.skipif(not os.access(HIPCC, os.X_OK), reason="no hipcc")
 

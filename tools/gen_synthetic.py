@@ -9,6 +9,7 @@ floor((k+0.5) N/12).  Lines are "0 1 0 ... *" like Dataset/*.txt.
   python tools/gen_synthetic.py N M SEED OUT
 """
 import hashlib
+import os
 import sys
 
 import numpy as np
@@ -45,8 +46,12 @@ def to_text(X, hard):
 def write(N, M, seed, out):
     X, hard = make(N, M, seed)
     txt = to_text(X, hard)
-    with open(out, "w") as fh:
+    # written under a private name and renamed: ranks of one box that generate the same file concurrently
+    # (bench.py --gpus N --sites .. --taxa ..) never read a partial one
+    tmp = "%s.%d.tmp" % (out, os.getpid())
+    with open(tmp, "w") as fh:
         fh.write(txt)
+    os.replace(tmp, out)
     return hashlib.sha256(txt.encode()).hexdigest()
 
 

@@ -1,6 +1,6 @@
 """Parity fuzz over random shapes (GPU): random N, M, hard sites, block size, column placement and c/d mode, each run against
 the CPU oracle (2 burn-in + 3 saved calls, 2 seeds).  Prints one line per shape and exits 1 on the first mismatch.
-    python tools/fuzz_shapes.py [count] [seed]"""
+    python tools/fuzz_shapes.py [count] [seed] [--lds]"""
 import os
 import sys
 
@@ -15,14 +15,16 @@ from test_gpu_edge import make_text    # noqa: E402
 
 
 def main():
-    count = int(sys.argv[1]) if len(sys.argv) > 1 else 12
-    rng = np.random.default_rng(int(sys.argv[2]) if len(sys.argv) > 2 else 2026)
+    lds = "--lds" in sys.argv   # LDS-column shapes (register and LDS walks; with SR_JIT unset, specialised kernels)
+    argv = [a for a in sys.argv[1:] if a != "--lds"]
+    count = int(argv[0]) if argv else 12
+    rng = np.random.default_rng(int(argv[1]) if len(argv) > 1 else 2026)
     for t in range(count):
-        N = int(rng.integers(8, 1500))
-        M = int(rng.integers(2, 2600))
+        N = int(rng.integers(8, 544 if lds else 1500))
+        M = int(rng.integers(2, 1025 if lds else 2600))
         nh = int(min(N - 2, rng.choice([0, 3, 12, 40, 70])))
         tb = int(rng.choice([0, 256, 512, 1024]))
-        cols = str(rng.choice(["auto", "hbm"]))
+        cols = "auto" if lds else str(rng.choice(["auto", "hbm"]))
         mcd = int(rng.random() < 0.2)   # manycd: per-taxon c, d (1024 threads)
         if mcd:
             tb = int(rng.choice([0, 1024]))

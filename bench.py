@@ -1,15 +1,24 @@
 #!/usr/bin/env python3
 """Benchmark: chain-iterations/s of the MCMC seriation sweep on MI355X.
 
-Workload (BASELINE.json configs[2]/[3]): synthetic 256 sites x 512 taxa
-(tools/gen_synthetic.py, seed 20261015), 100 chains per GPU (weak scaling: 100*N chains on
-N GPUs, 800 on 8 = config 4).  One step = one kernel launch that runs
-`--calls-per-step` reference mcmc_sample calls (10 sweeps each, mcmc.c:225) for every
-chain of the rank and saves one record per call (a, b, pi, c, d, loglik -- the
-mcmc_save_chain payload) to HBM, as the reference's sampling phase does.  Chain state,
-dataset and records stay resident in HBM; host formatting of records is not timed.
-At the end of the timed region ranks all-gather their per-chain loglik over RCCL (the
-one-sigma selection input) -- the only collective.
+Headline (BASELINE.json metric, configs[2]): synthetic 256 sites x 512 taxa (tools/gen_synthetic.py,
+seed 20261015), 100 chains in total, sharded contiguously over the N GPUs (ragged shards from
+dist.shard: 13/13/13/13/12/12/12/12 at N = 8; `--total-chains 800` is config 4, `--chains-per-gpu C`
+the weak-scaling form).  One step = one kernel launch that runs `--calls-per-step` reference
+mcmc_sample calls (10 sweeps each, mcmc.c:225) for every chain of the rank and saves one record per
+call (a, b, pi, c, d, loglik -- the mcmc_save_chain payload) to HBM, as the reference's sampling phase
+does.  Chain state, dataset and records stay resident in HBM; host formatting of records is not timed.
+At the end of the timed region ranks all-gather their per-chain summaries over RCCL (the one-sigma
+selection input) and the selected chains' records -- the only collectives.
+
+At N = 1 the same line also carries (`--legs`, default both):
+  config2 -- the reference's own published workload (Report p.6 s5.1: g10s10, 100 chains x 2000
+             mcmc_sample calls in 15-20 min): script.py:48-67 end to end through the drop-in launcher,
+             Chains/chain_NN files written, beside the CPU oracle CLI running the same protocol, whose
+             files must be byte-identical;
+  config5 -- 1024 x 2048 (HBM columns, split chains), 100 chains from init over the reference protocol
+             (1000 burn-in + 1000 saved calls), with the steady-state rate of the saved window and its
+             records checked against the committed oracle digests (tests/golden/config5.json).
 
 1 chain-iteration = 1 sweep = body of mcmc.c:225-244.
 
@@ -30,6 +39,8 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 SYNTH = os.path.join(ROOT, "tests", "golden", "datasets", "synth_256x512.txt")
+G10S10 = os.path.join(ROOT, "tests", "golden", "datasets", "g10s10.txt")
+C5_GOLDEN = os.path.join(ROOT, "tests", "golden", "config5.json")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 CHAINS_SELECTED = 8    # choose_chains(8) as in Report Table 1 for g10s10
 
@@ -45,6 +56,33 @@ def launch_ranks(n):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
     return subprocess.call(cmd)
+
+
+def visible_gpu_count(base="/sys/class/kfd/kfd/topology/nodes"):
+    """GPUs this process could use, counted without initialising HIP (torch.cuda.device_count() may fall back to
+    hipGetDeviceCount, and this process must not touch the GPU before it starts the ranks): the KFD topology's
+    nodes with SIMDs, narrowed by ROCR / HIP / CUDA_VISIBLE_DEVICES.  None when the topology cannot be read
+    (then the ranks report a missing device themselves)."""
+    try:
+        nodes = os.listdir(base)
+    except OSError:
+        return None
+    n = 0
+    for node in nodes:
+        try:
+            with open(os.path.join(base, node, "properties")) as fh:
+                for line in fh:
+                    k, _, v = line.partition(" ")
+                    if k == "simd_count" and int(v) > 0:
+                        n += 1
+                        break
+        except (OSError, ValueError):
+            return None
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None and v.strip():
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
 
 
 def algorithmic_bytes_per_iter(N, M):
@@ -78,13 +116,12 @@ def measured_traffic(N, M, chains, sweeps_per_step):
 
 
 def _cpu_worker(args):
-    text, seed, calls, variant = args
+    text, seed, burnin, calls, variant = args
     import oracle_ref
     if variant != "O2":
         oracle_ref.use_variant(variant)
-    t0 = time.perf_counter()
-    o = oracle_ref.run_chain(text, seed, 0, calls, sweeps=10)
-    return time.perf_counter() - t0, o["rc"]
+    o = oracle_ref.run_chain(text, seed, burnin, calls, sweeps=10)
+    return o["burnin_s"], o["sample_s"], o["rc"]
 
 
 def cpu_share():
@@ -106,11 +143,13 @@ def cpu_share():
     return n, nproc
 
 
-def cpu_baseline(path, calls, workers, variant="O2"):
-    """The CPU oracle (C restatement of mcmc.c; recount after every accepted proposal as the
-    reference) on `workers` processes, one chain each, `calls` mcmc_sample calls per chain:
-    aggregate chain-iterations/s.  variant "O2" (gcc -O2) or "O0" (reference-like: the shipped
-    binary was built at -O0)."""
+def cpu_baseline(path, burnin, calls, workers, variant="O2"):
+    """The CPU oracle (C restatement of mcmc.c; recount after every accepted proposal as the reference) on
+    `workers` processes, one chain each: `burnin` untimed mcmc_sample calls from chain birth -- the calls the
+    GPU's warm-up runs, so both sides time chains of the same age (mcmc.c:140-185) -- then `calls` timed calls.
+    value = the sum of the workers' rates over the timed window (one chain per core); "from_birth" = the same
+    over the burn-in window (young chains accept far more moves, each paid with an O(N*M) recount).
+    variant "O2" (gcc -O2) or "O0" (reference-like: the shipped binary was built at -O0)."""
     import multiprocessing as mp
     with open(path, "rb") as fh:
         text = fh.read()
@@ -120,22 +159,158 @@ def cpu_baseline(path, calls, workers, variant="O2"):
     t0 = time.perf_counter()
     pool = ctx.Pool(workers)
     try:
-        res = pool.map(_cpu_worker, [(text, s + 1, calls, variant) for s in range(workers)])
+        res = pool.map(_cpu_worker, [(text, s + 1, burnin, calls, variant) for s in range(workers)])
     finally:
         # close + join: the workers exit on their own (a Pool context exit terminate()s them with
         # SIGTERM, which a profiler's signal handler reports as an abort)
         pool.close()
         pool.join()
     wall = time.perf_counter() - t0
-    assert all(rc == 0 for _, rc in res)
-    iters = workers * calls * 10
+    assert all(rc == 0 for _, _, rc in res)
     share, nproc = cpu_share()
-    return {"value": iters / wall, "unit": "chain-iterations/s", "cores": workers, "kind": "port",
-            "nproc": nproc, "cpu_share": share,
-            "sample": "%d chains x %d mcmc_sample calls (%d sweeps each) of the bench workload, oracle/ "
-                      "(C restatement of mcmc.c, gcc -%s, recount after accept as the reference) on %d "
-                      "processes (one per core of this process's CPU share; nproc %d), wall %.1f s"
-                      % (workers, calls, 10, variant, workers, nproc, wall)}
+    value = sum(calls * 10 / ts for _, ts, _ in res)
+    out = {"value": value, "unit": "chain-iterations/s", "cores": workers, "kind": "port",
+           "nproc": nproc, "cpu_share": share,
+           "sample": "%d chains, each %d untimed mcmc_sample calls from birth (the GPU's warm-up calls) then %d timed "
+                     "calls (%d sweeps each) of the bench workload; oracle/ (C restatement of mcmc.c, gcc -%s, recount "
+                     "after accept as the reference) on %d processes (one per core of this process's CPU share; nproc "
+                     "%d); value = sum of the per-chain rates over the timed window; wall %.1f s"
+                     % (workers, burnin, calls, 10, variant, workers, nproc, wall)}
+    if burnin:
+        out["from_birth"] = {"value": sum(burnin * 10 / tb for tb, _, _ in res), "unit": "chain-iterations/s",
+                             "sample": "the same chains over their first %d calls (from birth: the regime a fresh "
+                                       "chain runs in, not the GPU's timed window)" % burnin}
+    return out
+
+
+def leg_config2_cpu(workers, tmp):
+    """config2's CPU side, before the GPU is touched: the oracle CLI (oracle/build/mcmc_oracle, the reference
+    main() restated, mcmc.c:102-210) as script.py:25-45 starts it -- `mcmc k` with GSL_RNG_SEED = k + 1 in its own
+    directory -- for chains 0..workers-1 of the 100, one process per core, full protocol (1000 burn-in + 1000 saved
+    calls), files written.  Their Chains/ files are the parity reference of the GPU run."""
+    import subprocess
+    cli = os.path.join(ROOT, "oracle", "build", "mcmc_oracle")
+    if not os.path.exists(cli):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    procs = []
+    t0 = time.perf_counter()
+    for k in range(workers):
+        d = os.path.join(tmp, "cpu%02d" % k)
+        os.makedirs(os.path.join(d, "Chains", "chain_%02d" % k))
+        with open(G10S10, "rb") as fin:
+            procs.append(subprocess.Popen([cli, str(k)], cwd=d, stdin=fin, stdout=subprocess.DEVNULL,
+                                          stderr=subprocess.DEVNULL, env=dict(os.environ, GSL_RNG_SEED=str(k + 1))))
+    rcs = [p.wait() for p in procs]
+    wall = time.perf_counter() - t0
+    assert all(rc == 0 for rc in rcs), rcs
+    rate = workers * 2000 * 10 / wall
+    return {"chains": workers, "cores": workers, "wall_s": wall, "chain_iterations_per_s": rate,
+            "projected_100_chain_wall_s": 100 * 2000 * 10 / rate, "kind": "port (oracle CLI, gcc -O2)",
+            "sample": "chains 0..%d of the 100 (seeds 1..%d), the full protocol each, one process per core, files "
+                      "written; 100-chain wall projected at the same rate" % (workers - 1, workers)}
+
+
+def leg_config2_gpu(device, tmp, cpu):
+    """config2 on the GPU: launcher.run_all_chains (script.py:48-67) over g10s10 with seeds 1..100 -- dataset load,
+    init, 1000 burn-in + 1000 saved calls per chain, the five Chains/chain_NN files per chain, the closing
+    mcmc_consistent -- timed end to end; then the files of the chains the CPU ran compared byte for byte."""
+    from seriation_amd import launcher
+    root = os.path.join(tmp, "gpu")
+    t0 = time.perf_counter()
+    summ = launcher.run_all_chains(G10S10, n_chains=100, seeds=list(range(1, 101)), devices=[device], root=root,
+                                   verbose=False)
+    wall = time.perf_counter() - t0
+    files = ("chain_data.csv", "exp_data.csv", "taxa.csv", "sites.csv", "hard_sites.csv")
+    bad = []
+    nchk = cpu["chains"] if cpu else 0
+    for k in range(nchk):
+        for f in files:
+            with open(os.path.join(tmp, "cpu%02d" % k, "Chains", "chain_%02d" % k, f), "rb") as fa, \
+                    open(os.path.join(root, "Chains", "chain_%02d" % k, f), "rb") as fb:
+                if fa.read() != fb.read():
+                    bad.append("chain_%02d/%s" % (k, f))
+    out = {"workload": "Dataset/g10s10.txt (124 sites x 139 taxa), 100 chains (seeds 1..100), 1000 burn-in + 1000 "
+                       "saved mcmc_sample calls each (script.py:48-67 -> mcmc.c:102-210), Chains/chain_NN/*.csv written",
+           "gpu_wall_s": wall, "chain_iterations_per_s": 100 * 2000 * 10 / wall,
+           "consistent": all(s["consistent"] == 0 for s in summ),
+           "timed": "launcher.run_all_chains end to end: Dataset.load, init, sampling, file output, closing "
+                    "mcmc_consistent",
+           "reference_published": {"wall_s": [900, 1200], "source": "Docs/Report.pdf p.6 s5.1: 100 chains x 2000 "
+                                   "mcmc_sample calls in 15-20 min (6 processes)"},
+           "speedup_vs_published": [900 / wall, 1200 / wall],
+           "cpu": cpu}
+    if cpu:
+        out["parity"] = {"chains": list(range(nchk)), "files": list(files), "match": not bad, "mismatch": bad,
+                         "note": "the GPU run's Chains/chain_NN files byte-identical to the oracle CLI's"}
+        out["speedup_vs_cpu_oracle"] = cpu["projected_100_chain_wall_s"] / wall
+    return out
+
+
+def leg_config5(device, calls_per_launch=50):
+    """config5 (BASELINE configs[4]): synthetic 1024 x 2048 (gen_synthetic seed 20261016), 100 chains (seeds
+    1..100) from init over the reference protocol, 1000 burn-in + 1000 saved calls (mcmc.c:140-185), launches of
+    `calls_per_launch` calls.  Timed: the whole protocol from session creation (host init, upload) to the last
+    record, and the saved window alone (the steady-state rate).  Parity: chains 0..3 against the committed
+    oracle digests of tests/golden/config5.json (every saved record, exp_data)."""
+    import hashlib as hl
+    import numpy as np
+    import gen_synthetic
+    import seriation_amd as sa
+    X, hard = gen_synthetic.make(1024, 2048, 20261016)
+    text = gen_synthetic.to_text(X, hard).encode()
+    ds = sa.Dataset.parse(text, maxs=0)
+    seeds = list(range(1, 101))
+    launches = 1000 // calls_per_launch
+    t0 = time.perf_counter()
+    sess = sa.Session(ds, seeds, device=device, calls_per_launch=1000)
+    for _ in range(launches):
+        sess.run(calls_per_launch, save=False)
+    sess.sync()
+    t1 = time.perf_counter()
+    for _ in range(launches):
+        sess.run(calls_per_launch, save=True)
+    sess.sync()
+    t2 = time.perf_counter()
+    rows = sess.summaries()
+    t3 = time.perf_counter()
+    kernel, variant = sess.kernel, sess.variant
+    launch = ("ordinary (SR_COOP=0)" if os.environ.get("SR_COOP") == "0" else "cooperative") if kernel == "split" \
+        else "ordinary"
+    parity = None
+    if os.path.exists(C5_GOLDEN):
+        with open(C5_GOLDEN) as fh:
+            g = json.load(fh)
+        bad = {}
+        if g["dataset_sha256"] != hl.sha256(text).hexdigest():
+            bad["dataset"] = "generated matrix differs from the fixture's"
+        for ch in g["chains"]:
+            k = ch["seed"] - 1
+            ab, cd = sess.fetch_chain_records(k)
+            dig = [hl.sha256(np.ascontiguousarray(r, dtype="<i4").tobytes()).hexdigest() for r in ab]
+            n = len(ch["sha256"])
+            if dig[:n] != ch["sha256"]:
+                bad[str(k)] = "integer state differs from saved call %d on" % next(
+                    i for i in range(n) if dig[i] != ch["sha256"][i])
+            elif [[float(v).hex() for v in r] for r in cd[:n]] != ch["cdl_hex"]:
+                bad[str(k)] = "c/d/loglik bits differ"
+            elif [float(v).hex() for v in rows[k, 1:4]] != ch["exp_hex"]:
+                bad[str(k)] = "exp_data differs"
+        parity = {"chains": [ch["seed"] - 1 for ch in g["chains"]], "seeds": [ch["seed"] for ch in g["chains"]],
+                  "burnin_calls": g["burnin_calls"], "saved_calls_compared": g["saved_calls"], "match": not bad,
+                  "mismatch": bad, "reference": "tests/golden/config5.json (oracle/om_mcmc.c digests, "
+                                                "tests/golden/make_golden_c5.py)"}
+    sess.close()
+    iters = 100 * 2000 * 10
+    return {"workload": "synthetic (tools/gen_synthetic.py seed 20261016) 1024 sites x 2048 taxa, 12 hard sites, 100 "
+                        "chains (seeds 1..100) from init, 1000 burn-in + 1000 saved mcmc_sample calls, %d-call launches"
+                        % calls_per_launch,
+            "columns": variant, "kernel": kernel, "launch": launch,
+            "protocol_wall_s": t3 - t0, "protocol_chain_iterations_per_s": iters / (t3 - t0),
+            "burnin_wall_s": t1 - t0, "saved_window_wall_s": t2 - t1,
+            "steady_state_chain_iterations_per_s": iters / 2 / (t2 - t1),
+            "timed": "protocol: session creation (host init + upload) to the exp_data summaries; steady state: the "
+                     "1000 saved calls (10 000 sweeps per chain after 10 000 of burn-in)",
+            "parity": parity}
 
 
 def main():
@@ -143,7 +318,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=20, help="untimed steps first (the clocks ramp over the first ~10 launches)")
-    ap.add_argument("--chains-per-gpu", type=int, default=100)
+    ap.add_argument("--total-chains", type=int, default=100, help="chains in the whole job, sharded contiguously over "
+                    "the N GPUs (ragged shards: dist.shard); the metric's 100 at every N (strong scaling); 800 = config 4")
+    ap.add_argument("--chains-per-gpu", type=int, default=0, help="weak scaling instead: this many chains per GPU "
+                    "(overrides --total-chains)")
     ap.add_argument("--calls-per-step", type=int, default=50,
                     help="mcmc_sample calls per step: 50 (500 sweeps) makes the driver's --steps 20 --warmup 5 time "
                          "SURVEY 8(d)'s 10 000 sweeps after 2 500 warm-up sweeps, saving 1000 records per chain")
@@ -176,15 +354,25 @@ def main():
                     "several ranks on one GPU, which RCCL does not allow)")
     ap.add_argument("--no-save", action="store_true", help="sample without saving records (SURVEY.md 8(d) "
                     "asks for both; the default saves one record per call, as the reference's sampling phase)")
+    ap.add_argument("--legs", default="auto", help="extra workloads in the same line at N = 1: comma-separated from "
+                    "config2, config5; none; auto = both unless --no-cpu-baseline or N > 1")
     args = ap.parse_args()
+    legs = set()
+    if args.legs == "auto":
+        if args.gpus == 1 and not args.no_cpu_baseline:
+            legs = {"config2", "config5"}
+    elif args.legs != "none":
+        legs = set(x.strip() for x in args.legs.split(",") if x.strip())
+        if not legs <= {"config2", "config5"}:
+            raise SystemExit("bench.py: --legs takes config2, config5, none or auto")
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # one process per GPU: launch the ranks as children (this process has not touched the
-        # GPU and never will) and exit with their status.  Counting devices does not initialise the GPU.
-        import torch
+        # GPU and never will: the devices are counted from the KFD topology, not through HIP) and exit with their
+        # status.
         need = max(int(x) for x in args.device_of_rank.split(",")) + 1 if args.device_of_rank else args.gpus
-        have = torch.cuda.device_count()
-        if have < need:
+        have = visible_gpu_count()
+        if have is not None and have < need:
             raise SystemExit("bench.py: --gpus %d needs %d visible GPU(s), %d visible" % (args.gpus, need, have))
         return launch_ranks(args.gpus)
 
@@ -205,13 +393,25 @@ def main():
         import gen_synthetic
         gen_synthetic.write(256, 512, 20261015, args.dataset)
 
-    # CPU baseline first, before this process touches the GPU (it forks workers).
-    cpu = cpu_o0 = None
+    total = args.chains_per_gpu * world if args.chains_per_gpu else args.total_chains
+    if total < world:
+        raise SystemExit("bench.py: %d chains cannot be sharded over %d GPUs" % (total, world))
+    scaling = "weak" if args.chains_per_gpu else "strong"
+
+    # CPU baseline and the CPU side of the extra legs first, before this process touches the GPU (they fork).
+    cpu = cpu_o0 = c2cpu = None
+    tmp = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        workers = args.cpu_workers or min(cpu_share()[0], args.chains_per_gpu)
-        cpu = cpu_baseline(args.dataset, args.cpu_calls, workers)
-        cpu_o0 = cpu_baseline(args.dataset, max(1, args.cpu_calls // 4), workers, "O0")
+        workers = args.cpu_workers or min(cpu_share()[0], total)
+        warm_calls = args.warmup * args.calls_per_step
+        cpu = cpu_baseline(args.dataset, warm_calls, args.cpu_calls, workers)
+        cpu_o0 = cpu_baseline(args.dataset, warm_calls, max(1, args.cpu_calls // 4), workers, "O0")
         cpu_o0["kind"] = "port (reference-like -O0 build)"
+    if rank == 0 and "config2" in legs:
+        import tempfile
+        tmp = tempfile.mkdtemp(prefix="sr_bench_c2_")
+        if not args.no_cpu_baseline:
+            c2cpu = leg_config2_cpu(args.cpu_workers or min(cpu_share()[0], 16), tmp)
 
     import numpy as np
     import torch
@@ -236,9 +436,10 @@ def main():
     # the session runs the sweep kernel compiled for this dataset's shape (the library's default for LDS
     # columns; cached, identical results) unless --generic
     ds = sa.Dataset.load(args.dataset, maxs=0)
-    C = args.chains_per_gpu
-    # weak scaling: C chains per rank, rank r owns chains [r*C, (r+1)*C) (sd.shard), seed = id + 1
-    chain_ids = list(sd.shard(C * world, world, rank))
+    # rank r owns the contiguous block sd.shard(total, world, r) (ragged when world does not divide total), seed = id + 1
+    chain_ids = list(sd.shard(total, world, rank))
+    C = len(chain_ids)
+    shards = [len(sd.shard(total, world, r)) for r in range(world)]
     seeds = [i + 1 for i in chain_ids]
     cps = args.calls_per_step
     # records of every timed step are kept (steps x calls-per-step saved samples per chain: 1000 at the
@@ -279,7 +480,7 @@ def main():
     t_summ = time.perf_counter()
     nrec = int(sess.fetch_cdl().shape[1]) if args.no_save else args.steps * cps
     if dist:
-        gathered = sd.gather_summaries(rows, C * world, device=coll_dev)
+        gathered = sd.gather_summaries(rows, total, device=coll_dev)
     else:
         gathered = rows
     selected = sd.select_chains(gathered, CHAINS_SELECTED)
@@ -288,7 +489,7 @@ def main():
     # the selected chains' records: device-to-device copies out of the session's record buffer on this stream,
     # then (N > 1) one all-gather per array over RCCL -- they never leave HBM inside the timed region
     dev_ab, dev_cd = sd.gather_selected_records_device(
-        selected, C * world, chain_ids, lambda j, pa, pc: sess.copy_chain_records(j, pa, pc, count=nrec), nrec, W,
+        selected, total, chain_ids, lambda j, pa, pc: sess.copy_chain_records(j, pa, pc, count=nrec), nrec, W,
         device=torch.device("cuda", device), ws=rec_ws if nrec == nrec_ws else None)
     t_fetch = t_sel
     torch.cuda.synchronize()
@@ -306,12 +507,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
-    assert len(gathered) == C * world and np.isfinite(gathered).all() and selected
+    assert len(gathered) == total and np.isfinite(gathered).all() and selected
     assert sel_ab.shape[0] == len(selected) and (sel_ab[:, :, 2 * ds.M:] >= 0).all()
 
-    total_chains = C * world
     sweeps_per_step = cps * 10
-    iters = total_chains * sweeps_per_step * args.steps
+    iters = total * sweeps_per_step * args.steps
     value = iters / elapsed
     B = algorithmic_bytes_per_iter(ds.N, ds.M)
     launch_bytes = C * sweeps_per_step * B
@@ -334,19 +534,22 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
         "config": {
-            "workload": ("%s %dx%d, %d chains per GPU, "
+            "workload": ("%s %dx%d, %d chains (%s), "
                          "%d mcmc_sample calls (%d sweeps) per chain per step, " +
                          ("no records saved" if args.no_save else "one saved record per call"))
                         % ("synthetic (tools/gen_synthetic.py seed %d)" % (20261015 if (ds.N, ds.M) == (256, 512)
                                                                           else 20261016)
                            if args.dataset == SYNTH or args.sites else os.path.basename(args.dataset),
-                           ds.N, ds.M, C, cps, sweeps_per_step),
-            "sites": ds.N, "taxa": ds.M, "chains": total_chains, "chains_per_gpu": C,
+                           ds.N, ds.M, total, ("%d per GPU" % C) if scaling == "weak" else
+                           "sharded over %d GPU(s): %s" % (world, "/".join(map(str, shards))), cps, sweeps_per_step),
+            "sites": ds.N, "taxa": ds.M, "chains": total, "chains_per_gpu": C, "chains_per_rank": shards,
+            "scaling_mode": "strong: %d chains in total at every N" % total if scaling == "strong" else
+                            "weak: %d chains per GPU" % C,
             "sweeps_per_step": sweeps_per_step, "block_threads": sess.block_threads, "columns": sess.variant,
             "kernel": sess.kernel,   # "split": two workgroups per chain (HBM columns)
             # split chains need both halves resident: hipLaunchCooperativeKernel (the product path), or an ordinary
@@ -424,8 +627,21 @@ def main():
             parity["calls_bound"] = ("--parity-calls %d" % pc if args.parity_calls > 0 else
                                      "auto: HBM-column session, the oracle takes ~0.4 s per call at this size")
     out["parity"] = parity
+    # the extra workloads of the same line (N = 1, rank 0, after the headline and its parity leg)
+    if rank == 0 and world == 1:
+        if "config2" in legs:
+            out["config2"] = leg_config2_gpu(device, tmp, c2cpu)
+        if "config5" in legs:
+            out["config5"] = leg_config5(device)
+    if tmp:
+        import shutil
+        shutil.rmtree(tmp, ignore_errors=True)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    for leg in ("config2", "config5"):
+        p = (out.get(leg) or {}).get("parity")
+        if p is not None and not p["match"]:
+            raise SystemExit("bench.py: %s differs from its oracle reference: %s" % (leg, p["mismatch"]))
     if parity is not None and not parity["match"]:
         raise SystemExit("bench.py: the timed records differ from the CPU oracle: %s" % parity["mismatch"])
 

@@ -111,9 +111,12 @@ void sr_default_opts(sr_run_opts *o);
  * "GSL_RNG_TYPE=mt19937" when set), then GSL_RNG_SEED (strtoul base 0, unset -> 0 = GSL's default 4357;
  * verbose: "GSL_RNG_SEED=<value>") into *seed.  Another GSL generator -> SR_EUNSUPPORTED (the sampler
  * implements MT19937's stream only), a name GSL does not know -> SR_EINVAL (verbose: GSL's "not recognized"
- * message and list of generator types).  Every session / run entry point applies the same GSL_RNG_TYPE
- * check (silently) and refuses with the same codes, so no run samples MT19937 where the environment named
- * another generator. */
+ * message and list of generator types).  Every session / run entry point that samples MT19937's stream
+ * applies the same GSL_RNG_TYPE check (silently) and refuses with the same codes, so no run samples MT19937
+ * where the environment named another generator; SR_F_RNG_PHILOX sessions sample no GSL stream and ignore it.
+ * Departure: for an unknown name GSL 2.6 prints the list, then its default error handler reports "unknown
+ * generator" and aborts (SIGABRT); here the caller gets SR_EINVAL and the CLIs exit 1 (parity unpinned: no GSL
+ * here to take the handler's exact line from). */
 int sr_rng_env_setup(uint64_t *seed, int32_t verbose);
 
 /* Run n_chains independent chains on one GPU (opts->device), burn-in then sampling;

@@ -21,6 +21,7 @@
 #include <stdlib.h>
 #include <stdint.h>
 #include <string.h>
+#include <time.h>
 #include "om_gsl.h"
 
 #define OM_MAXS 2000                              /* mcmc.h:25 */
@@ -291,28 +292,32 @@ static int om_sampled(om_model *x)
   return 1;
 }
 
-/* mcmc_randompick, mcmc.c:901-915 */
-static int om_randompick(om_model *mo, const double *p, int n)
+/* mcmc_randompick, mcmc.c:901-915, with the uniform given (om_pick_u) or drawn */
+static int om_pick_u(const double *p, int n, double u)
 {
   int i = 0;
-  double x = om_uniform(&mo->rng) - p[0];
+  double x = u - p[0];
   while (x > 0. && i < n - 1) x -= p[++i];
   return i;
 }
 
-/* mcmc_auxa, mcmc.c:828-898 */
-static void om_auxa(om_model *mo, const int *x, int b, double c, double d,
-                    int *a, int *t0, int *f0, int *t1, int *f1)
+static int om_randompick(om_model *mo, const double *p, int n)
+{
+  return om_pick_u(p, n, om_uniform(&mo->rng));
+}
+
+/* mcmc_auxa's weights (mcmc.c:828-897 up to the randompick): the count deltas dt0..df1[0..b] of moving the limit
+ * from *a to each entry and q[0..b] = the pick probabilities after mcmc_logtop */
+static void om_auxa_weights(const int *x, int b, int a, double c, double d, double *q, int *dt0, int *df0, int *dt1,
+                            int *df1)
 {
   int i;
   double cc, dd;
-  double *q = mo->q;
-  int *dt0 = mo->dt0, *df0 = mo->df0, *dt1 = mo->dt1, *df1 = mo->df1;
-  q[*a] = 0.;
-  dt0[*a] = df0[*a] = dt1[*a] = df1[*a] = 0;
+  q[a] = 0.;
+  dt0[a] = df0[a] = dt1[a] = df1[a] = 0;
   cc = om_log(1. - om_exp(c));
   dd = om_log(1. - om_exp(d));
-  for (i = *a - 1; i >= 0; i--) {
+  for (i = a - 1; i >= 0; i--) {
     if (x[i]) {
       dt0[i] = dt0[i + 1]; df0[i] = df0[i + 1];
       dt1[i] = dt1[i + 1] + 1; df1[i] = df1[i + 1] - 1;
@@ -321,7 +326,7 @@ static void om_auxa(om_model *mo, const int *x, int b, double c, double d,
       dt1[i] = dt1[i + 1]; df1[i] = df1[i + 1];
     }
   }
-  for (i = *a + 1; i <= b; i++) {
+  for (i = a + 1; i <= b; i++) {
     if (x[i - 1]) {
       dt0[i] = dt0[i - 1]; df0[i] = df0[i - 1];
       dt1[i] = dt1[i - 1] - 1; df1[i] = df1[i - 1] + 1;
@@ -333,6 +338,15 @@ static void om_auxa(om_model *mo, const int *x, int b, double c, double d,
   for (i = 0; i <= b; i++)
     q[i] = dt0[i] * cc + df0[i] * d + dt1[i] * dd + df1[i] * c;
   om_logtop(q, b + 1);
+}
+
+/* mcmc_auxa, mcmc.c:828-898 */
+static void om_auxa(om_model *mo, const int *x, int b, double c, double d,
+                    int *a, int *t0, int *f0, int *t1, int *f1)
+{
+  double *q = mo->q;
+  int *dt0 = mo->dt0, *df0 = mo->df0, *dt1 = mo->dt1, *df1 = mo->df1;
+  om_auxa_weights(x, b, *a, c, d, q, dt0, df0, dt1, df1);
   *a = om_randompick(mo, q, b + 1);
   *t0 += dt0[*a]; *f0 += df0[*a]; *t1 += dt1[*a]; *f1 += df1[*a];
 }
@@ -712,6 +726,17 @@ OM_API int oracle_parse(const char *text, long len, int maxs, int *N, int *M, in
 static int g_rng_philox = 0;
 OM_API void oracle_set_rng(int philox) { g_rng_philox = philox ? 1 : 0; }
 
+/* wall seconds of the last oracle_run_chain(_v) on this thread: [0] the tb burn-in calls, [1] the ts saved calls
+ * (bench.py's cpu_baseline times the calls after the GPU's warm-up window, mcmc.c:140-185's two loops) */
+static __thread double om_phase_s[2];
+static double om_now(void)
+{
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+OM_API void oracle_phase_seconds(double *out2) { out2[0] = om_phase_s[0]; out2[1] = om_phase_s[1]; }
+
 /* rec_cdv (optional, manycd runs): ts*2M doubles = every taxon's c then d per saved sample */
 OM_API int oracle_run_chain_v(const char *text, long len, int maxs, unsigned long seed, int manycd,
                               int tb, int ts, int sweeps, int check,
@@ -748,10 +773,12 @@ OM_API int oracle_run_chain_v(const char *text, long len, int maxs, unsigned lon
     for (int n = 0; n < N; n++) init_out[2 * M + n] = x.pi[n];
   }
   if (init_dbl) { init_dbl[0] = x.c[0]; init_dbl[1] = x.d[0]; init_dbl[2] = x.loglik; }
+  const double t0 = om_now();
   for (int i = 0; i < tb; i++) {
     om_sample(&x, sweeps);
     if (check && om_consistent(&x, 0, 1)) bad = 1;
   }
+  const double t1 = om_now();
   double ls = 0, cs = 0, ds = 0;
   for (int i = 0; i < ts; i++) {
     om_sample(&x, sweeps);
@@ -770,12 +797,83 @@ OM_API int oracle_run_chain_v(const char *text, long len, int maxs, unsigned lon
     cs += exp(x.c[0]);
     ds += exp(x.d[0]);
   }
+  om_phase_s[0] = t1 - t0;
+  om_phase_s[1] = om_now() - t1;
   if (exp_out) { exp_out[0] = ls / 1000; exp_out[1] = cs / 1000; exp_out[2] = ds / 1000; }
   if (acc_out) memcpy(acc_out, x.acc, sizeof(x.acc));
   if (rng_words) *rng_words = x.rng.ndraw;
   if (om_consistent(&x, 1, 1)) bad = 1;
   om_free(&x);
   return bad ? 1 : 0;
+}
+
+/* ---- references of the device certification self-tests (tests/test_gpu_cert.py) ----
+ * oracle_auxa_pick: mcmc_auxa + mcmc_logtop + mcmc_randompick (mcmc.c:828-915) over walk-order bits x[0..b) from
+ * limit a, with the uniform u given instead of drawn; returns the pick, p_out (optional, b + 1) the probabilities
+ * randompick subtracts.  oracle_auxa_boundary: the smallest u in [0, 1] whose pick exceeds entry i -- the
+ * reference's own CDF boundary, with its sequential subtractions -- by bisection over the ordered doubles of [0, 1]
+ * (each subtraction is monotone in its minuend, so the pick is monotone in u). */
+static int om_auxa_alloc(int b, double **q, int **dt)
+{
+  *q = (double *)malloc(sizeof(double) * (size_t)(b + 1));
+  *dt = (int *)malloc(sizeof(int) * 4 * (size_t)(b + 1));
+  return *q && *dt;
+}
+
+OM_API int oracle_auxa_pick(const int32_t *x, int b, int a, double c, double d, double u, double *p_out)
+{
+  double *q;
+  int *dt;
+  if (b < 0 || a < 0 || a > b || !om_auxa_alloc(b, &q, &dt)) return -1;
+  om_auxa_weights(x, b, a, c, d, q, dt, dt + b + 1, dt + 2 * (b + 1), dt + 3 * (b + 1));
+  const int r = om_pick_u(q, b + 1, u);
+  if (p_out) memcpy(p_out, q, sizeof(double) * (size_t)(b + 1));
+  free(q); free(dt);
+  return r;
+}
+
+OM_API double oracle_auxa_boundary(const int32_t *x, int b, int a, double c, double d, int i)
+{
+  double *q;
+  int *dt;
+  if (b < 0 || a < 0 || a > b || i < 0 || i >= b || !om_auxa_alloc(b, &q, &dt)) return -1.0;
+  om_auxa_weights(x, b, a, c, d, q, dt, dt + b + 1, dt + 2 * (b + 1), dt + 3 * (b + 1));
+  double one = 1.0;
+  uint64_t lo = 0, hi;
+  memcpy(&hi, &one, 8);
+  double r = 2.0;
+  if (om_pick_u(q, b + 1, 1.0) > i) {
+    while (lo < hi) {   /* invariant: pick(bits hi) > i */
+      const uint64_t mid = lo + (hi - lo) / 2;
+      double um;
+      memcpy(&um, &mid, 8);
+      if (om_pick_u(q, b + 1, um) > i) hi = mid; else lo = mid + 1;
+    }
+    memcpy(&r, &hi, 8);
+  }
+  free(q); free(dt);
+  return r;   /* 2.0: no u in [0, 1] picks beyond i */
+}
+
+/* a proposal's delta as the reference sums it (mcmc_samplepi1 / pi2 / pi3 / swap, e.g. mcmc.c:1300-1304): per
+ * taxon dt0 cc + df0 d + dt1 dd + df1 c with df0 = -dt0, df1 = -dt1 (cc = log(1 - e^c), dd = log(1 - e^d)), added
+ * in taxon order; and its acceptance (mcmc.c:492): 1 accepted without drawing u (delta >= 0), 2 accepted with the
+ * uniform_pos u drawn (delta > log u), 0 rejected */
+OM_API double oracle_delta_terms(const int32_t *dt0, const int32_t *dt1, long K, double c, double d)
+{
+  const double cc = om_log(1. - om_exp(c)), dd = om_log(1. - om_exp(d));
+  double delta = 0.;
+  for (long m = 0; m < K; m++) {
+    const int df0 = -dt0[m], df1 = -dt1[m];
+    delta += dt0[m] * cc + df0 * d + dt1[m] * dd + df1 * c;
+  }
+  return delta;
+}
+
+OM_API int oracle_mh_outcome(double delta, double u)
+{
+  if (delta >= 0.) return 1;
+  return delta > om_log(u) ? 2 : 0;
 }
 
 /* Philox4x32-10 block probe (known-answer tests) */

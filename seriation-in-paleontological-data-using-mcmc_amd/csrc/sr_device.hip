@@ -100,6 +100,14 @@ struct KArgs {
    scratch, room made by one block-shared copy of the hard-site and 4-step tables instead of one per wave
    (16 waves: 66 KB + 20 KB at N = 1024).  The checkpoints were a quarter of config 5's HBM traffic (all of its
    writes) and two dependent memory round trips of every walk's pass 2 (0 = HBM scratch, round 4's form) */
+/* test builds: every certification margin -- the Gibbs picks' REL / ABS (draw_fast, walk_pick_s, draw_pair9) and
+   phase C's Eb (pc_classify) -- scaled by 2^-SR_CERT_SHIFT.  The product is 0; the negative control of
+   tests/test_gpu_cert.py builds the library at 8 and must then see wrong picks and decisions, which shows that the
+   self-tests (sr_device_selftest_gibbs / _decide) can see an understated bound. */
+#ifndef SR_CERT_SHIFT
+#define SR_CERT_SHIFT 0
+#endif
+#define SR_CERT_SCALE (1.0 / (double)(1ull << SR_CERT_SHIFT))
 #ifndef SR_SP_LCK
 #define SR_SP_LCK 1
 #endif
@@ -853,6 +861,29 @@ __device__ __forceinline__ double2 t4sp(const double *T4, int c, uint32_t nib)
 __device__ __forceinline__ double t4s(const double *T4, int c, uint32_t nib) { return T4[2 * (c * 16 + (int)nib)]; }
 __device__ __forceinline__ double t4p(const double *T4, uint32_t nib) { return T4[2 * (64 + (int)nib) + 1]; }
 
+/* The Gibbs step tables' entries (rA = 2^-vA, rB = 2^-vB: the ratio of consecutive walk weights after a zero / a
+ * one).  t4_row: nibble l's row, sc[c] = sum of the first c prefix products (c = 0..4), returns the product of all
+ * four; t8_entry: byte e, {sum of its 8 prefix products, their product}.  Built per sweep by the sweep kernel and by
+ * the certification self-test (sr_device_selftest_gibbs) alike. */
+__device__ __forceinline__ double t4_row(int l, double rA, double rB, double (&sc)[5])
+{
+  double pr = 1.0, sm = 1.0;
+  sc[0] = 0.0;
+  sc[1] = sm;
+  pr = pr * ((l & 1) ? rB : rA); sm = sm + pr; sc[2] = sm;
+  pr = pr * ((l & 2) ? rB : rA); sm = sm + pr; sc[3] = sm;
+  pr = pr * ((l & 4) ? rB : rA); sm = sm + pr; sc[4] = sm;
+  pr = pr * ((l & 8) ? rB : rA);
+  return pr;
+}
+__device__ __forceinline__ double2 t8_entry(int e, double rA, double rB)
+{
+  double pr = 1.0, sm = 0.0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { sm = sm + pr; pr = pr * (((e >> k) & 1) ? rB : rA); }
+  return make_double2(sm, pr);
+}
+
 /* 2^q (q <= ~0) to ~1.6e-7 relative: exact f64 split q = n + f, f in [0,1), v_exp_f32(f) */
 __device__ __forceinline__ double exp2_split(double q)
 {
@@ -1043,8 +1074,8 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, const uint16_t *pre
   int res = -1, POp = 0;
   if (S > 0.0 && S < 0x1p1000 && !uf) {
     const double inv = 1.0 / S;
-    const double REL = (double)(N + 33) * 0x1p-50;
-    const double ABS = (double)(N + 1) * 0x1p-39 + 0x1p-46 + ((B8 && SR_CK32) ? 0x1p-21 : 0.0);
+    const double REL = (double)(N + 33) * 0x1p-50 * SR_CERT_SCALE;
+    const double ABS = ((double)(N + 1) * 0x1p-39 + 0x1p-46 + ((B8 && SR_CK32) ? 0x1p-21 : 0.0)) * SR_CERT_SCALE;
     int j = klo;   /* first window word whose checkpoint reaches u (checkpoints ascend) */
     double Sp0, yj;   /* the partial sum before word j, y at its start */
     if (B8 && SR_CKG > 1) {
@@ -1245,8 +1276,8 @@ __device__ __forceinline__ int walk_pick_s(const uint32_t (&wk)[NWM], const doub
   int res = -1;
   {
     const double inv = 1.0 / S;
-    const double REL = (double)(N + 33) * 0x1p-50;   /* + the byte tables' own rounding (<= 16 ulp per entry) */
-    const double ABS = (double)(N + 1) * 0x1p-39;
+    const double REL = (double)(N + 33) * 0x1p-50 * SR_CERT_SCALE;   /* + the byte tables' own rounding (<= 16 ulp per entry) */
+    const double ABS = (double)(N + 1) * 0x1p-39 * SR_CERT_SCALE;
     /* the words before the window hold S = 0 (< u S), so counting k < khi finds the word */
     const double uS = u * S;
     int j = 0;
@@ -1589,8 +1620,8 @@ __device__ __forceinline__ int draw_pair9(const uint32_t (&wk)[5], int h, const 
   uf = uf || pair_swap_i32(uf ? 1 : 0) != 0;
   if (St > 0.0 && St < 0x1p1000 && !uf) {
     const double inv = 1.0 / St;
-    const double REL = (double)(N + 41) * 0x1p-50;
-    const double ABS = (double)(N + 1) * 0x1p-39;
+    const double REL = (double)(N + 41) * 0x1p-50 * SR_CERT_SCALE;
+    const double ABS = (double)(N + 1) * 0x1p-39 * SR_CERT_SCALE;
     const double uS = u * St;
     int jl = 0;
 #pragma unroll
@@ -2234,6 +2265,50 @@ __device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const i
  * 1 + t0_m) / Beta(1 + f0_m, 1 + t1_m), every Gibbs draw, logl term and proposal delta with its taxon's own
  * coefficients -- the exact paths throughout (per-taxon step ratios leave nothing to share or certify by
  * integer sums).  One taxon or more per thread, one workgroup per chain, LDS or HBM columns. */
+/* ---- phase C's certified Metropolis decision (mcmc.c:492 / 569 / 637: delta >= 0 || delta > log(uniform_pos)).
+ * With X = sum dt, Y = sum |dt| (exact integers), S = X0 (cc - d) + X1 (dd - c) is the exact sum of the exact
+ * per-taxon terms and B = Y0 (|cc|+|d|) + Y1 (|dd|+|c|) bounds their magnitudes; the reference's rounded terms
+ * and sequential sum stay within (K + 7) 2^-53 B of S, K = #nonzero terms <= Knz = Y0 + Y1, so Eb = (Knz + 16)
+ * 2^-52 B decides delta >= 0 and delta > log u whenever the true value is farther than Eb.  log u is first taken
+ * in f32 (error << 2^-16 (1 + |log u|)), exactly only when that is too close.  The lane-parallel part: returns
+ * cls 0 rejected, 1 accepted, 2 needs the exact delta or the exact log (pr: the pair kernels' packed Y). */
+__device__ __forceinline__ int pc_classify(int X0, int X1, int Y0, int Y1, const CD &K, double aC, double aD, bool pr,
+                                           uint32_t uw, double &Sp, double &Ebp, int &Knz)
+{
+  Sp = ((double)X0 * K.cc - (double)X0 * K.d) + ((double)X1 * K.dd - (double)X1 * K.c);
+  /* PR: o[2] holds Y0 + Y1 (one packed field), o[3] = 0 -- bounded by the larger coefficient */
+  const double B = pr ? (double)(Y0 + Y1) * fmax(aC, aD) : (double)Y0 * aC + (double)Y1 * aD;
+  Knz = Y0 + Y1;   /* >= the number of nonzero terms: each has |dt0| + |dt1| >= 1 */
+  Ebp = ((double)Knz + 16.0) * 0x1p-52 * B * SR_CERT_SCALE;
+  if (Knz == 0 || Sp > Ebp) return 1;
+  if (Sp < -Ebp) {
+    const float uf = (float)((double)uw / 4294967296.0);
+    const double lua = (double)__builtin_amdgcn_logf(uf) * 0.69314718055994531;
+    const double dl = 0x1p-16 * (1.0 + __builtin_fabs(lua));
+    return (Sp - Ebp > lua + dl) ? 1 : ((Sp + Ebp < lua - dl) ? 0 : 2);
+  }
+  return 2;
+}
+
+/* The serial part for a proposal classified 1 or 2 (S, Eb, kz = Knz of pc_classify): true when decided (accept;
+ * udrawn: the uniform_pos was consumed), false when the exact sequential delta must decide.  dl: the delta the
+ * accepted move adds to loglik when known exactly (have_exact). */
+__device__ __forceinline__ bool pc_resolve(double S, double Eb, int c0, int kz, double u, const sr_mtab &tb, bool &accept,
+                                           bool &udrawn, bool &have_exact, double &dl)
+{
+  accept = false; have_exact = false; dl = S;
+  if (kz == 0) { accept = true; udrawn = false; have_exact = true; dl = 0.0; return true; }
+  if (c0 == 1 && S > Eb) { accept = true; udrawn = false; return true; }
+  if (c0 == 1) { accept = true; udrawn = true; return true; }
+  if (S < -Eb) {   /* near a threshold: the exact log first */
+    const double lu = sr_log_m(u, &tb);
+    udrawn = true;
+    if (S - Eb > lu) { accept = true; return true; }
+    if (S + Eb < lu) return true;
+  }
+  return false;
+}
+
 template <int TB, int NWM, bool GM, bool PR = false, bool SP = false, bool MCD = false, bool LK = false>
 __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 {
@@ -2509,14 +2584,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       }
       /* PR: one shared copy of the tables, built by waves 0-4 (T8 quarters, T4), then a barrier */
       if ((PR ? wave == 4 : (!SHT || wave == NWV - 1)) && lane < 16) {   /* per-wave (PR, SHT: shared) tables for 4 walk entries with bits = lane */
-        double pr = 1.0, sm = 1.0;
         double sc[5];
-        sc[0] = 0.0;
-        sc[1] = sm;
-        pr = pr * ((lane & 1) ? rB : rA); sm = sm + pr; sc[2] = sm;
-        pr = pr * ((lane & 2) ? rB : rA); sm = sm + pr; sc[3] = sm;
-        pr = pr * ((lane & 4) ? rB : rA); sm = sm + pr; sc[4] = sm;
-        pr = pr * ((lane & 8) ? rB : rA);
+        const double pr = t4_row(lane, rA, rB, sc);
 #pragma unroll
         for (int c = 0; c < 5; ++c) { T4w[2 * (c * 16 + lane)] = sc[c]; T4w[2 * (c * 16 + lane) + 1] = pr; }
       }
@@ -2525,10 +2594,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 #pragma unroll
         for (int q = 0; q < (SH8 ? 1 : 4); ++q) {
           const int e = lane + 64 * (SH8 ? wave : q);
-          double pr = 1.0, sm = 0.0;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) { sm = sm + pr; pr = pr * (((e >> k) & 1) ? rB : rA); }
-          if (!SH8 || wave < 4) *reinterpret_cast<double2 *>(T8w + 2 * e) = make_double2(sm, pr);
+          const double2 te = t8_entry(e, rA, rB);
+          if (!SH8 || wave < 4) *reinterpret_cast<double2 *>(T8w + 2 * e) = te;
         }
         if (lane == 0 && (!SH8 || wave == (PR ? 4 : 0))) *reinterpret_cast<double2 *>(T8w + 2 * 256) = make_double2(0.0, 1.0);
       }
@@ -3199,13 +3266,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           STAMP_E(5);
           FST(5);
 
-          /* ---- lane-parallel certified decisions (lane p decides proposal p).  With
-             X = sum dt, Y = sum |dt| (exact integers), S = X0 (cc - d) + X1 (dd - c) is the exact
-             sum of the exact per-taxon terms and B = Y0 (|cc|+|d|) + Y1 (|dd|+|c|) bounds their
-             magnitudes; the reference's rounded terms and sequential sum stay within
-             (K + 7) 2^-53 B of S, K = #nonzero terms <= Knz = Y0 + Y1, so Eb = (Knz + 16) 2^-52 B decides
-             delta >= 0 and delta > log u whenever the true value is farther than Eb.  log u is
-             first taken in f32 (error << 2^-16 (1 + |log u|)), exactly only when that is too close.
+          /* ---- lane-parallel certified decisions (lane p decides proposal p; pc_classify / pc_resolve).
              cls: 0 rejected, 1 accepted, 2 needs the exact delta or the exact log. */
           const double aC = __builtin_fabs(K.cc) + __builtin_fabs(K.d), aD = __builtin_fabs(K.dd) + __builtin_fabs(K.c);
           double Sp = 0.0, Ebp = 0.0;
@@ -3225,26 +3286,16 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                   const int *yp = xb + 16 + ((bpar * 2 + (half ^ 1)) * 16 + p) * 4;
                   X0 += xld(yp); X1 += xld(yp + 1); Y0 += xld(yp + 2); Y1 += xld(yp + 3);
                 }
-                Sp = ((double)X0 * K.cc - (double)X0 * K.d) + ((double)X1 * K.dd - (double)X1 * K.c);
-                /* PR: o[2] holds Y0 + Y1 (one packed field), o[3] = 0 -- bounded by the larger coefficient */
-                const double B = PR ? (double)(Y0 + Y1) * fmax(aC, aD) : (double)Y0 * aC + (double)Y1 * aD;
-                Knz = Y0 + Y1;   /* >= the number of nonzero terms: each has |dt0| + |dt1| >= 1 */
-                Ebp = ((double)Knz + 16.0) * 0x1p-52 * B;
                 uwp = (uint32_t)vuw;
+                cls = pc_classify(X0, X1, Y0, Y1, K, aC, aD, PR, uwp, Sp, Ebp, Knz);
 #ifdef SR_FORCE_EXACT   /* test build: every decision by the exact sequential delta */
-                if (Knz == 0) cls = 1; else cls = 2;
+                cls = (Knz == 0) ? 1 : 2;
                 Ebp = __builtin_inf();
 #else
                 if (MCD) {   /* manycd: per-taxon coefficients, the exact sequential delta decides */
                   cls = (Knz == 0) ? 1 : 2;
                   Ebp = __builtin_inf();
-                } else if (Knz == 0 || Sp > Ebp) cls = 1;
-                else if (Sp < -Ebp) {
-                  const float uf = (float)((double)uwp / 4294967296.0);
-                  const double lua = (double)__builtin_amdgcn_logf(uf) * 0.69314718055994531;
-                  const double dl = 0x1p-16 * (1.0 + __builtin_fabs(lua));
-                  cls = (Sp - Ebp > lua + dl) ? 1 : ((Sp + Ebp < lua - dl) ? 0 : 2);
-                } else cls = 2;
+                }
 #endif
               }
             }
@@ -3263,20 +3314,9 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             const double S = readlane_f64(Sp, p), Eb = readlane_f64(Ebp, p);
             const int c0 = __builtin_amdgcn_readlane(cls, p), kz = __builtin_amdgcn_readlane(Knz, p);
             const double u = (double)(uint32_t)__builtin_amdgcn_readlane((int)uwp, p) / 4294967296.0;
-            bool accept = false, decided = true, have_exact = false;
-            double dl = S;
-            if (kz == 0) { accept = true; udrawn = false; have_exact = true; dl = 0.0; }
-            else if (c0 == 1 && S > Eb) { accept = true; udrawn = false; }
-            else if (c0 == 1) { accept = true; udrawn = true; }
-            else {   /* near a threshold: the exact log first */
-              decided = false;
-              if (S < -Eb) {
-                const double lu = sr_log_m(u, &tb);
-                udrawn = true;
-                if (S - Eb > lu) { accept = true; decided = true; }
-                else if (S + Eb < lu) { accept = false; decided = true; }
-              }
-            }
+            bool accept, have_exact;
+            double dl;
+            const bool decided = pc_resolve(S, Eb, c0, kz, u, tb, accept, udrawn, have_exact, dl);
             if (!decided || (accept && want_logl && !have_exact)) {   /* the exact sequential delta */
               if constexpr (SP)
                 dl = sr_exact_delta<PR, GM, SP>(kind, q, K, sab, P, pre, M, N, KTC, olo, ohi, hl, nh, hcnt, nhall, hbx,
@@ -4343,5 +4383,186 @@ extern "C" __attribute__((visibility("default"))) int sr_device_selftest_math(in
   HIPCHK(hipMemcpy(out_log, dl, n * 8, hipMemcpyDeviceToHost));
   (void)hipFree(din); (void)hipFree(de); (void)hipFree(dl);
   return 0;
+}
+
+/* ================================================================ certification self-tests (test hooks)
+ * The bit-exactness of the sampler rests on two analytic error bounds that chain-level parity cannot probe
+ * (a uniform u lands in the band where an understated bound would give a wrong answer about once in 1e13 draws):
+ * the Gibbs picks' REL / ABS (draw_fast_s, draw_fast) and phase C's Eb (pc_classify / pc_resolve).  These hooks run
+ * the product's own device functions on caller-chosen inputs -- u placed on and around the reference's exact CDF
+ * boundaries, count sums whose reference delta sits at 0 or at log u -- and return what the function decided and
+ * whether it fell back to the exact path (tests/test_gpu_cert.py checks every case against the oracle). */
+
+/* One wave per block, one case per lane; block b's lanes share (c, d) = cd[2b], cd[2b + 1].  MODE 0 / 1:
+ * draw_fast_s<9> / <17> (register walks, the LDS-column kernels up to N = 287 / 543), 2: draw_fast<false> (LDS
+ * columns beyond), 3: draw_fast<true> (HBM columns: byte tables, grouped checkpoints, SR_QSPAN trims).  Case m: the
+ * column's position-ordered bits P[w * M + m] (M = cases), its prefix table pre[w * M + m], walk direction rev[m]
+ * (1: walk entry w = position N - 1 - w, the b-draw), current limit o[m] and walk end L[m] (entries 0..L), u[m].
+ * out[5 m ..]: the pick and the count deltas dt0, df0, dt1, df1 at it; fb[m]: exact-walk fallbacks taken. */
+template <int MODE>
+__global__ void __launch_bounds__(64) sr_gibbs_selftest_kernel(const uint32_t *P, const uint16_t *pre, int N, int M,
+                                                               const double *cd, const int *oo, const int *LL,
+                                                               const int *rv, const double *uu, int *out,
+                                                               unsigned long long *fb, double *cks)
+{
+  __shared__ double tabs[512];
+  __shared__ double T4w[T4STRIDE];
+  __shared__ double T8w[2 * 257];
+  const int lane = threadIdx.x, m = blockIdx.x * 64 + lane;
+  for (int i = lane; i < 256; i += 64) {
+    ((uint64_t *)tabs)[i] = c_exp_tab[i];
+    tabs[256 + i] = c_log_tab[i];
+  }
+  __syncthreads();
+  sr_mtab tb;
+  tb.exp_tab = (const uint64_t *)tabs; tb.log_tab = tabs + 256;
+  CD K;   /* as the sweep kernel's phase A */
+  K.c = cd[2 * blockIdx.x]; K.d = cd[2 * blockIdx.x + 1];
+  K.cc = sr_log_m(1. - sr_exp_m(K.c, &tb), &tb);
+  K.dd = sr_log_m(1. - sr_exp_m(K.d, &tb), &tb);
+  K.ec = sr_exp_m(SR_LOGEPSILON, &tb);
+  const double vA = (K.d - K.cc) * 1.4426950408889634;
+  const double vB = (K.dd - K.c) * 1.4426950408889634;
+  const double rA = sr_exp_m(K.cc - K.d, &tb), rB = sr_exp_m(K.c - K.dd, &tb);
+  if (lane < 16) {
+    double sc[5];
+    const double pr = t4_row(lane, rA, rB, sc);
+#pragma unroll
+    for (int c = 0; c < 5; ++c) { T4w[2 * (c * 16 + lane)] = sc[c]; T4w[2 * (c * 16 + lane) + 1] = pr; }
+  }
+  for (int q = 0; q < 4; ++q) *reinterpret_cast<double2 *>(T8w + 2 * (lane + 64 * q)) = t8_entry(lane + 64 * q, rA, rB);
+  if (lane == 0) *reinterpret_cast<double2 *>(T8w + 2 * 256) = make_double2(0.0, 1.0);
+  __syncthreads();
+  const int NW = (N + 31) >> 5;
+  const uint32_t *Pm = P + m;
+  const uint16_t *prem = pre + m;
+  const int o = oo[m], L = LL[m];
+  const bool rev = rv[m] != 0;
+  const double u = uu[m];
+  const int POo = rev ? (int)prem[NW * M] - col_pre(prem, Pm, M, N - o) : col_pre(prem, Pm, M, o);
+  int d0 = 0, e0 = 0, d1 = 0, e1 = 0, res;
+  if constexpr (MODE <= 1) {
+    constexpr int NWM = MODE == 0 ? 9 : 17;
+    uint32_t wk[NWM];
+    load_fwd<NWM>(Pm, M, NW, wk);
+    if (rev) {
+      uint32_t rw[NWM];
+      make_rev<NWM>(Pm, M, N, NW, wk, rw);
+#pragma unroll
+      for (int k = 0; k < NWM; ++k) wk[k] = rw[k];
+    }
+    res = draw_fast_s<NWM>(wk, Pm, M, N, rev, o, L, POo, u, K, tb, vA, vB, T4w, T8w, (uint64_t *)(fb + m), d0, e0, d1, e1);
+  } else {
+    res = draw_fast<MODE == 3>(Pm, prem, M, N, NW, rev, o, L, POo, u, K, tb, vA, vB, rA, rB, T4w, T8w, cks + m, M,
+                               (uint64_t *)(fb + m), d0, e0, d1, e1);
+  }
+  int *r = out + 5 * m;
+  r[0] = res; r[1] = d0; r[2] = e0; r[3] = d1; r[4] = e1;
+}
+
+/* Phase C's decision per case: sums[4 m ..] = X0, X1, Y0, Y1 of one proposal (the exact integer sums of dt0, dt1
+ * and of |dt0| + |dt1| over the taxa: Y0 = Y1 = Y as the one-workgroup kernels store them), cd[2 m ..] = c, d, uw[m]
+ * the proposal's uniform_pos word.  out[m]: 0 rejected (u drawn), 1 accepted without drawing u (delta >= 0), 2
+ * accepted with u drawn, 3 the exact sequential delta must decide (the sampler's fallback). */
+__global__ void __launch_bounds__(64) sr_decide_selftest_kernel(const int *sums, const double *cd, const uint32_t *uw,
+                                                                int n, int *out)
+{
+  __shared__ double tabs[512];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    ((uint64_t *)tabs)[i] = c_exp_tab[i];
+    tabs[256 + i] = c_log_tab[i];
+  }
+  __syncthreads();
+  sr_mtab tb;
+  tb.exp_tab = (const uint64_t *)tabs; tb.log_tab = tabs + 256;
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= n) return;
+  CD K;
+  K.c = cd[2 * m]; K.d = cd[2 * m + 1];
+  K.cc = sr_log_m(1. - sr_exp_m(K.c, &tb), &tb);
+  K.dd = sr_log_m(1. - sr_exp_m(K.d, &tb), &tb);
+  K.ec = 0.0;
+  const double aC = __builtin_fabs(K.cc) + __builtin_fabs(K.d), aD = __builtin_fabs(K.dd) + __builtin_fabs(K.c);
+  double Sp, Ebp;
+  int Knz;
+  const int cls = pc_classify(sums[4 * m], sums[4 * m + 1], sums[4 * m + 2], sums[4 * m + 3], K, aC, aD, false, uw[m], Sp,
+                              Ebp, Knz);
+  int res = 0;
+  if (cls != 0) {
+    bool accept, udrawn = false, have_exact;
+    double dl;
+    const double u = (double)uw[m] / 4294967296.0;
+    if (!pc_resolve(Sp, Ebp, cls, Knz, u, tb, accept, udrawn, have_exact, dl)) res = 3;
+    else res = accept ? (udrawn ? 2 : 1) : 0;
+  }
+  out[m] = res;
+}
+
+/* Host entry points of the self-tests (negative codes: -1 bad arguments, -2 device error).  ncases must be a
+ * multiple of 64; P is [NW][ncases] u32, pre [NW + 1][ncases] u16, cd [ncases / 64][2]. */
+extern "C" __attribute__((visibility("default"))) int sr_device_selftest_gibbs(int device, int mode, int N, int ncases,
+                                                                              const uint32_t *P, const uint16_t *pre,
+                                                                              const double *cd, const int *o, const int *L,
+                                                                              const int *rev, const double *u, int *out,
+                                                                              unsigned long long *fb)
+{
+  const int NW = (N + 31) >> 5;
+  if (ncases <= 0 || ncases % 64 || N < 1 || N > 4095 || mode < 0 || mode > 3 || (mode == 0 && NW > 9) ||
+      (mode == 1 && NW > 17))
+    return -1;
+  for (int m = 0; m < ncases; ++m)
+    if (o[m] < 0 || o[m] > L[m] || L[m] > N) return -1;
+  HIPCHK(hipSetDevice(device));
+  const size_t C = (size_t)ncases;
+  void *b[11] = {};
+  const size_t sz[11] = {NW * C * 4, (NW + 1) * C * 2, C / 64 * 2 * 8, C * 4, C * 4, C * 4, C * 8, C * 5 * 4, C * 8,
+                         (NW + 2) * C * 8, 0};
+  int rc = 0;
+  for (int k = 0; k < 10 && !rc; ++k) rc = hipMalloc(&b[k], sz[k]) != hipSuccess;
+  const void *src[7] = {P, pre, cd, o, L, rev, u};
+  for (int k = 0; k < 7 && !rc; ++k) rc = hipMemcpy(b[k], src[k], sz[k], hipMemcpyHostToDevice) != hipSuccess;
+  if (!rc) rc = hipMemset(b[8], 0, sz[8]) != hipSuccess;
+  if (!rc) {
+    const dim3 g(ncases / 64), t(64);
+    const uint32_t *dP = (const uint32_t *)b[0];
+    const uint16_t *dpre = (const uint16_t *)b[1];
+    const double *dcd = (const double *)b[2], *du = (const double *)b[6];
+    const int *dO = (const int *)b[3], *dL = (const int *)b[4], *dR = (const int *)b[5];
+    int *dout = (int *)b[7];
+    unsigned long long *dfb = (unsigned long long *)b[8];
+    double *dck = (double *)b[9];
+    if (mode == 0) hipLaunchKernelGGL(sr_gibbs_selftest_kernel<0>, g, t, 0, 0, dP, dpre, N, ncases, dcd, dO, dL, dR, du, dout, dfb, dck);
+    else if (mode == 1) hipLaunchKernelGGL(sr_gibbs_selftest_kernel<1>, g, t, 0, 0, dP, dpre, N, ncases, dcd, dO, dL, dR, du, dout, dfb, dck);
+    else if (mode == 2) hipLaunchKernelGGL(sr_gibbs_selftest_kernel<2>, g, t, 0, 0, dP, dpre, N, ncases, dcd, dO, dL, dR, du, dout, dfb, dck);
+    else hipLaunchKernelGGL(sr_gibbs_selftest_kernel<3>, g, t, 0, 0, dP, dpre, N, ncases, dcd, dO, dL, dR, du, dout, dfb, dck);
+    rc = hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess;
+  }
+  if (!rc) rc = hipMemcpy(out, b[7], sz[7], hipMemcpyDeviceToHost) != hipSuccess;
+  if (!rc) rc = hipMemcpy(fb, b[8], sz[8], hipMemcpyDeviceToHost) != hipSuccess;
+  for (int k = 0; k < 10; ++k) (void)hipFree(b[k]);
+  return rc ? -2 : 0;
+}
+
+extern "C" __attribute__((visibility("default"))) int sr_device_selftest_decide(int device, int ncases, const int *sums,
+                                                                               const double *cd, const uint32_t *uw,
+                                                                               int *out)
+{
+  if (ncases <= 0) return -1;
+  HIPCHK(hipSetDevice(device));
+  const size_t C = (size_t)ncases;
+  void *b[4] = {};
+  const size_t sz[4] = {C * 16, C * 16, C * 4, C * 4};
+  int rc = 0;
+  for (int k = 0; k < 4 && !rc; ++k) rc = hipMalloc(&b[k], sz[k]) != hipSuccess;
+  const void *src[3] = {sums, cd, uw};
+  for (int k = 0; k < 3 && !rc; ++k) rc = hipMemcpy(b[k], src[k], sz[k], hipMemcpyHostToDevice) != hipSuccess;
+  if (!rc) {
+    hipLaunchKernelGGL(sr_decide_selftest_kernel, dim3((ncases + 63) / 64), dim3(64), 0, 0, (const int *)b[0],
+                       (const double *)b[1], (const uint32_t *)b[2], ncases, (int *)b[3]);
+    rc = hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess;
+  }
+  if (!rc) rc = hipMemcpy(out, b[3], sz[3], hipMemcpyDeviceToHost) != hipSuccess;
+  for (int k = 0; k < 4; ++k) (void)hipFree(b[k]);
+  return rc ? -2 : 0;
 }
 #endif   /* !SR_JIT */

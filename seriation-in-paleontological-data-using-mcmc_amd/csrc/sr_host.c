@@ -497,9 +497,12 @@ static int session_new(const sr_dataset *ds, const sr_chain_spec *specs, int32_t
      records, int16 a, b, pi records), M <= SR_MMAX taxa (several per thread beyond the block; the records hold
      positions only).  The LDS layout must also fit 160 KB (srk_create), else HBM columns. */
   if (ds->N > 4095 || ds->M > SR_MMAX) return SR_EUNSUPPORTED;
-  /* the environment names another GSL generator (mcmc.c:591-592): not MT19937's stream, refused */
-  const int rt = rng_type_check(0);
-  if (rt) return rt;
+  /* the environment names another GSL generator (mcmc.c:591-592): a session that samples MT19937's stream is
+     refused; an opt-in Philox session (SR_F_RNG_PHILOX) samples no GSL stream and ignores the variable */
+  if (!(o.flags & SR_F_RNG_PHILOX)) {
+    const int rt = rng_type_check(0);
+    if (rt) return rt;
+  }
   sr_session *s = (sr_session *)calloc(1, sizeof(*s));
   if (!s) return SR_ENOMEM;
   s->ds.N = ds->N; s->ds.M = ds->M; s->ds.nh = ds->nh;
@@ -705,10 +708,12 @@ static int download(sr_session *s, sr_state_host *st)
 }
 
 /* ---- checkpoint / resume (the reference restarts every run; optional here) ----
- * File: "SRCK" | u32 version | i32 N, M, nh, nchains | u64 FNV-1a of the dataset (X, hard) | [v5, v6: i32 nrec]
+ * File: "SRCK" | u32 version | i32 N, M, nh, nchains | u64 FNV-1a of the dataset (X, hard) | [v5-v8: i32 nrec]
+ * | [v7, v8: i32 record capacity of the checkpointed session]
  * | sr_chain_spec[nchains] | the device state as sr_state_host arrays (P, rpi, hp, ab, cnt, cdl, mt, rng, acc;
  * manycd: cdv) | [v5, v6: the session's buffered records: ab_pi [nchains][nrec][2M+N] i16, cdl [nchains][nrec][3]
- * f64, manycd: cdv [nchains][nrec][2M] f64], little-endian.  Restoring uploads the same words, so the continued
+ * f64, manycd: cdv [nchains][nrec][2M] f64], little-endian.  A restore keeps at least the checkpointed session's
+ * record capacity, so the saves that session could still make fit without the caller re-supplying calls_per_launch.  Restoring uploads the same words, so the continued
  * chains are the ones an uninterrupted session produces, and summaries over the records (compute_exp_data,
  * mcmc.c:53-67) span the whole sampling phase across the interruption (tests/test_gpu_edge.py). */
 static uint64_t dataset_hash(const sr_dataset *ds)
@@ -724,6 +729,8 @@ typedef struct { size_t bytes; void *p; } ck_part;
 #define SR_CK_VERSION_MANYCD 4   /* version 3 + the per-taxon c, d of every chain (manycd sessions) */
 #define SR_CK_VERSION_REC 5      /* version 3 + the buffered records (written since round 5) */
 #define SR_CK_VERSION_REC_MANYCD 6   /* version 4 + the buffered records */
+#define SR_CK_VERSION_CAP 7      /* version 5 + the record capacity (written since round 6) */
+#define SR_CK_VERSION_CAP_MANYCD 8   /* version 6 + the record capacity */
 #define SR_CK_PARTS 10
 
 static int ck_parts(sr_state_host *st, ck_part *pt)
@@ -738,19 +745,20 @@ static int ck_parts(sr_state_host *st, ck_part *pt)
   return st->manycd ? 10 : 9;
 }
 
-typedef struct { int32_t nrec; int16_t *ab; double *cdl, *cdv; } ck_records;
+typedef struct { int32_t nrec, cap; int16_t *ab; double *cdl, *cdv; } ck_records;
 
 static int ck_write(const char *path, const sr_dataset *ds, const sr_chain_spec *specs, int32_t n, sr_state_host *st,
                     const ck_records *rec)
 {
   FILE *f = fopen(path, "wb");
   if (!f) return SR_EIO;
-  const uint32_t ver = st->manycd ? SR_CK_VERSION_REC_MANYCD : SR_CK_VERSION_REC;
+  const uint32_t ver = st->manycd ? SR_CK_VERSION_CAP_MANYCD : SR_CK_VERSION_CAP;
   const int32_t dims[4] = {ds->N, ds->M, ds->nh, n};
   const uint64_t h = dataset_hash(ds);
-  const int32_t nrec = rec ? rec->nrec : 0;
+  const int32_t nrec = rec ? rec->nrec : 0, cap = rec ? rec->cap : 0;
   int ok = fwrite("SRCK", 1, 4, f) == 4 && fwrite(&ver, 4, 1, f) == 1 && fwrite(dims, 4, 4, f) == 4 &&
-           fwrite(&h, 8, 1, f) == 1 && fwrite(&nrec, 4, 1, f) == 1 && fwrite(specs, sizeof(sr_chain_spec), n, f) == (size_t)n;
+           fwrite(&h, 8, 1, f) == 1 && fwrite(&nrec, 4, 1, f) == 1 && fwrite(&cap, 4, 1, f) == 1 &&
+           fwrite(specs, sizeof(sr_chain_spec), n, f) == (size_t)n;
   ck_part pt[SR_CK_PARTS];
   const int np = ck_parts(st, pt);
   for (int k = 0; k < np && ok; k++) ok = fwrite(pt[k].p, 1, pt[k].bytes, f) == pt[k].bytes;
@@ -769,7 +777,7 @@ SR_API int sr_session_checkpoint(sr_session *s, const char *path)
   sr_state_host st;
   int rc = download(s, &st);
   if (rc) return rc;
-  ck_records r = {s->nrec, NULL, NULL, NULL};
+  ck_records r = {s->nrec, s->rec_cap, NULL, NULL, NULL};
   if (r.nrec > 0) {   /* the buffered records travel with the state (v5 / v6) */
     const size_t rows = (size_t)s->nchains * r.nrec, W = 2 * (size_t)s->ds.M + s->ds.N;
     r.ab = (int16_t *)malloc(rows * W * 2);
@@ -842,19 +850,20 @@ SR_API int sr_session_restore(const sr_dataset *ds, const char *path, const sr_r
   if (!f) return SR_EIO;
   char magic[4];
   uint32_t ver = 0;
-  int32_t dims[4], nrec = 0;
+  int32_t dims[4], nrec = 0, cap = 0;
   uint64_t h = 0;
   int rc = SR_OK;
   sr_chain_spec *specs = NULL;
   int16_t *rab = NULL;
   double *rcd = NULL, *rcv = NULL;
   if (fread(magic, 1, 4, f) != 4 || memcmp(magic, "SRCK", 4) != 0 || fread(&ver, 4, 1, f) != 1 ||
-      (ver != SR_CK_VERSION && ver != SR_CK_VERSION_MANYCD && ver != SR_CK_VERSION_REC && ver != SR_CK_VERSION_REC_MANYCD) ||
+      ver < SR_CK_VERSION || ver > SR_CK_VERSION_CAP_MANYCD ||
       fread(dims, 4, 4, f) != 4 || fread(&h, 8, 1, f) != 1 || dims[3] <= 0)
     rc = SR_EPARSE;
-  const int with_rec = ver == SR_CK_VERSION_REC || ver == SR_CK_VERSION_REC_MANYCD;
-  const int mcd = ver == SR_CK_VERSION_MANYCD || ver == SR_CK_VERSION_REC_MANYCD;
+  const int with_rec = ver >= SR_CK_VERSION_REC, with_cap = ver >= SR_CK_VERSION_CAP;
+  const int mcd = ver == SR_CK_VERSION_MANYCD || ver == SR_CK_VERSION_REC_MANYCD || ver == SR_CK_VERSION_CAP_MANYCD;
   if (rc == SR_OK && with_rec && (fread(&nrec, 4, 1, f) != 1 || nrec < 0)) rc = SR_EPARSE;
+  if (rc == SR_OK && with_cap && (fread(&cap, 4, 1, f) != 1 || cap < nrec)) rc = SR_EPARSE;
   if (rc) { fclose(f); return rc; }
   if (dims[0] != ds->N || dims[1] != ds->M || dims[2] != ds->nh || h != dataset_hash(ds))
     rc = SR_EINVAL;   /* the checkpoint belongs to another dataset */
@@ -867,8 +876,10 @@ SR_API int sr_session_restore(const sr_dataset *ds, const char *path, const sr_r
     if (opts) o = *opts; else sr_default_opts(&o);
     if (opts && (o.manycd != 0) != mcd) rc = SR_EINVAL;
     o.manycd = mcd;
-    /* the record buffer holds the checkpoint's records and the caller's further calls */
-    if (auto_calls_per_launch(&o) < nrec) o.calls_per_launch = nrec;
+    /* the record buffer holds the checkpoint's records and the caller's further calls: at least the checkpointed
+       session's capacity (v7 / v8), the caller's calls_per_launch, and the records themselves */
+    const int want = cap > nrec ? cap : nrec;
+    if (auto_calls_per_launch(&o) < want) o.calls_per_launch = want;
     ck_reader r = {f, ds, with_rec};
     if (rc == SR_OK) rc = session_new(ds, specs, dims[3], &o, ck_restore, &r, out);
   }

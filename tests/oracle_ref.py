@@ -46,6 +46,18 @@ def load(path):
                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      P(ctypes.c_int32), P(ctypes.c_double), P(ctypes.c_int32), P(ctypes.c_double),
                                      P(ctypes.c_double), P(ctypes.c_double), P(ctypes.c_longlong), P(ctypes.c_ulonglong)]
+    L.oracle_auxa_pick.restype = ctypes.c_int
+    L.oracle_auxa_pick.argtypes = [P(ctypes.c_int32), ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                                   ctypes.c_double, P(ctypes.c_double)]
+    L.oracle_auxa_boundary.restype = ctypes.c_double
+    L.oracle_auxa_boundary.argtypes = [P(ctypes.c_int32), ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                                       ctypes.c_int]
+    L.oracle_delta_terms.restype = ctypes.c_double
+    L.oracle_delta_terms.argtypes = [P(ctypes.c_int32), P(ctypes.c_int32), ctypes.c_long, ctypes.c_double, ctypes.c_double]
+    L.oracle_mh_outcome.restype = ctypes.c_int
+    L.oracle_mh_outcome.argtypes = [ctypes.c_double, ctypes.c_double]
+    L.oracle_phase_seconds.restype = None
+    L.oracle_phase_seconds.argtypes = [P(ctypes.c_double)]
     L.oracle_rng_stream.restype = None
     L.oracle_rng_stream.argtypes = [ctypes.c_ulong, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_long,
                                     P(ctypes.c_double), P(ctypes.c_ulonglong)]
@@ -80,7 +92,8 @@ def parse(text, maxs=2000):
 
 
 def run_chain(text, seed, tb, ts, sweeps=10, check=0, maxs=2000, want_init=False, rng="mt", manycd=0):
-    """Returns dict(rc, init (a,b,pi), init_cdl, rec_int [ts, 2M+N], rec_dbl [ts, 3], exp, acc, words) and, for
+    """Returns dict(rc, init (a,b,pi), init_cdl, rec_int [ts, 2M+N], rec_dbl [ts, 3], exp, acc, words, burnin_s,
+    sample_s (wall seconds of the tb burn-in and the ts saved calls, timed inside the oracle)) and, for
     manycd=1 (per-taxon c, d: mcmc.c:777-786, 807-816), rec_cdv [ts, 2M] (every taxon's c then d per sample).
     rng="philox": the sampling phase on the Philox stream (the product's SR_F_RNG_PHILOX)."""
     if isinstance(text, str):
@@ -102,8 +115,11 @@ def run_chain(text, seed, tb, ts, sweeps=10, check=0, maxs=2000, want_init=False
                                   _p(init, ctypes.c_int32), _p(initd, ctypes.c_double),
                                   _p(ri, ctypes.c_int32), _p(rd, ctypes.c_double), _p(cv, ctypes.c_double),
                                   _p(ex, ctypes.c_double), _p(acc, ctypes.c_longlong), ctypes.byref(words))
+    ph = np.zeros(2)
+    lib().oracle_phase_seconds(_p(ph, ctypes.c_double))
     out = dict(rc=rc, N=N, M=M, init=init, init_cdl=initd, rec_int=ri[:ts * W].reshape(ts, W),
-               rec_dbl=rd[:ts * 3].reshape(ts, 3), exp=ex, acc=acc, words=words.value)
+               rec_dbl=rd[:ts * 3].reshape(ts, 3), exp=ex, acc=acc, words=words.value,
+               burnin_s=float(ph[0]), sample_s=float(ph[1]))
     if manycd:
         out["rec_cdv"] = cv[:ts * 2 * M].reshape(ts, 2 * M)
     return out
@@ -122,3 +138,30 @@ def exp_log(x):
     l = np.zeros_like(x)
     lib().oracle_exp_log(_p(x, ctypes.c_double), len(x), _p(e, ctypes.c_double), _p(l, ctypes.c_double))
     return e, l
+
+
+def auxa_pick(x, o, c, d, u, want_p=False):
+    """mcmc_auxa + logtop + randompick over walk-order bits x (length L = the walk end) from limit o with the
+    uniform u given: the pick (and the probabilities randompick subtracts)."""
+    x = np.ascontiguousarray(x, np.int32)
+    p = np.zeros(len(x) + 1) if want_p else None
+    r = lib().oracle_auxa_pick(_p(x, ctypes.c_int32), len(x), int(o), float(c), float(d), float(u), _p(p, ctypes.c_double))
+    return (r, p) if want_p else r
+
+
+def auxa_boundary(x, o, c, d, i):
+    """The smallest u in [0, 1] whose pick exceeds entry i (2.0: none)."""
+    x = np.ascontiguousarray(x, np.int32)
+    return lib().oracle_auxa_boundary(_p(x, ctypes.c_int32), len(x), int(o), float(c), float(d), int(i))
+
+
+def delta_terms(dt0, dt1, c, d):
+    """A proposal's delta summed as the reference does (per-taxon terms in taxon order)."""
+    dt0 = np.ascontiguousarray(dt0, np.int32)
+    dt1 = np.ascontiguousarray(dt1, np.int32)
+    return lib().oracle_delta_terms(_p(dt0, ctypes.c_int32), _p(dt1, ctypes.c_int32), len(dt0), float(c), float(d))
+
+
+def mh_outcome(delta, u):
+    """1 accepted without drawing u (delta >= 0), 2 accepted with u drawn, 0 rejected (mcmc.c:492)."""
+    return lib().oracle_mh_outcome(float(delta), float(u))

@@ -13,7 +13,9 @@ def shapes():
     sys.path.insert(0, HERE)
     import test_gpu_edge
     import test_gpu_jit
+    import test_gpu_fuzz
     out = {(N, M, nh, tb) for _, N, M, nh, tb in test_gpu_edge.CASES}
+    out |= set(test_gpu_fuzz.lds_shapes())
     out |= {(spec[0], spec[1], spec[2], 0) for _, spec, _ in test_gpu_jit.CASES if spec is not None}
     out |= {(256, 300, 5, 0), (400, 150, 5, 0),   # test_gpu_edge.test_steep_walks
             (70, 90, 3, 0), (70, 90, 9, 0),      # test_gpu_jit shards, test_gpu_multi

@@ -131,18 +131,27 @@ def test_restore_validates_chain_state(tmp_path):
         return rc
 
     assert restore(good) in (0, L.SR_EDEVICE)
-    raw5 = good.read_bytes()
-    assert raw5[:4] == b"SRCK" and np.frombuffer(raw5, "<u4", 1, 4)[0] == 5   # version 5: records follow the state
-    assert np.frombuffer(raw5, "<i4", 1, 32)[0] == 0                          # (none in an initial checkpoint)
-    # a version-3 file (before round 5: no record count, no records) still restores
+    raw7 = good.read_bytes()
+    # version 7: the record count and the session's record capacity, then (after the state) the records
+    assert raw7[:4] == b"SRCK" and np.frombuffer(raw7, "<u4", 1, 4)[0] == 7
+    assert np.frombuffer(raw7, "<i4", 2, 32).tolist() == [0, 0]                # (none in an initial checkpoint)
+    # a version-5 file (round 5: record count, no capacity) and a version-3 file (before round 5: no record count,
+    # no records) still restore
+    v5 = tmp_path / "v5.srck"
+    v5.write_bytes(raw7[:4] + np.array([5], "<u4").tobytes() + raw7[8:36] + raw7[40:])
+    assert restore(v5) in (0, L.SR_EDEVICE)
     v3 = tmp_path / "v3.srck"
-    v3.write_bytes(raw5[:4] + np.array([3], "<u4").tobytes() + raw5[8:32] + raw5[36:])
+    v3.write_bytes(raw7[:4] + np.array([3], "<u4").tobytes() + raw7[8:32] + raw7[40:])
     assert restore(v3) in (0, L.SR_EDEVICE)
+    badcap = bytearray(raw7)   # a capacity below the record count is refused
+    badcap[32:40] = np.array([5, 4], "<i4").tobytes()
+    (tmp_path / "badcap.srck").write_bytes(bytes(badcap))
+    assert restore(tmp_path / "badcap.srck") == -2
     trunc = tmp_path / "trunc.srck"
-    trunc.write_bytes(raw5[:-8])
+    trunc.write_bytes(raw7[:-8])
     assert restore(trunc) == -2
     N, M, nh, NW = ds.N, ds.M, ds.nh, (ds.N + 31) // 32
-    off = 36 + C * ctypes.sizeof(L.sr_chain_spec)
+    off = 40 + C * ctypes.sizeof(L.sr_chain_spec)
     sizes = [("P", C * NW * M * 4), ("rpi", C * N * 4), ("hp", C * 64 * 4), ("ab", C * 2 * M * 4),
              ("cnt", C * 4 * M * 4), ("cdl", C * 4 * 8), ("mt", C * 8 * 624 * 4), ("rng", C * 2 * 8), ("acc", C * 10 * 8)]
     base = {}
@@ -232,7 +241,7 @@ def test_checkpoint_many_hard_sites(tmp_path):
         L.lib().sr_session_destroy(h)
     assert rc in (0, L.SR_EDEVICE)
     NW = (N + 31) // 32
-    off = 36 + C * ctypes.sizeof(L.sr_chain_spec) + C * NW * M * 4 + C * N * 4
+    off = 40 + C * ctypes.sizeof(L.sr_chain_spec) + C * NW * M * 4 + C * N * 4
     raw = bytearray(good.read_bytes())
     assert len(raw) == off + C * 128 * 4 + C * 2 * M * 4 + C * 4 * M * 4 + C * 4 * 8 + C * 8 * 624 * 4 + C * 2 * 8 + C * 10 * 8
     hp = np.frombuffer(bytes(raw), "<i4", C * 128, off).reshape(C, 128)

@@ -231,7 +231,8 @@ def test_gsl_rng_type_oracle_and_fake_device(tmp_path, rtype, code):
 
 def test_gsl_rng_type_library_refuses(monkeypatch):
     """the library entry points apply the same check: sr_rng_env_setup's codes, and sr_session_create refuses
-    another generator before any device call (SR_EUNSUPPORTED / SR_EINVAL), whatever the device."""
+    another generator before any device call (SR_EUNSUPPORTED / SR_EINVAL) for every session that samples
+    MT19937's stream, whatever the device; Philox sessions (SR_F_RNG_PHILOX) are not refused."""
     import ctypes
     import seriation_amd as sa
     lib = L.lib()
@@ -248,6 +249,13 @@ def test_gsl_rng_type_library_refuses(monkeypatch):
             o = sa.core.make_opts()
             assert lib.sr_session_create(ctypes.byref(ds.c), sa.core.make_specs([1]), 1, ctypes.byref(o),
                                          ctypes.byref(h)) == want
+            # an opt-in Philox session samples no GSL stream: the variable does not refuse it (here it then
+            # fails for want of a device, or runs on one)
+            o = sa.core.make_opts(rng="philox")
+            rc = lib.sr_session_create(ctypes.byref(ds.c), sa.core.make_specs([1]), 1, ctypes.byref(o), ctypes.byref(h))
+            assert rc in (L.SR_OK, L.SR_EDEVICE), rc
+            if rc == L.SR_OK:
+                lib.sr_session_destroy(h)
 
 
 @pytest.mark.gpu

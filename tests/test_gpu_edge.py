@@ -268,9 +268,10 @@ def test_checkpoint_resume_continues_exactly(tmp_path):
 
 @pytest.mark.parametrize("manycd", [0, 1])
 def test_checkpoint_carries_records(tmp_path, manycd):
-    """Checkpoints keep the buffered records (version 5 / 6): 500 saved calls + checkpoint + restore + 500 saved
-    calls give the same 1000 records and the same exp_data rows (compute_exp_data over the whole sampling phase,
-    mcmc.c:53-67) bit for bit as 1000 calls straight -- manycd sessions with their per-taxon c, d too."""
+    """Checkpoints keep the buffered records and the record capacity (version 7 / 8): 500 saved calls + checkpoint
+    + restore + 500 saved calls give the same 1000 records and the same exp_data rows (compute_exp_data over the
+    whole sampling phase, mcmc.c:53-67) bit for bit as 1000 calls straight -- manycd sessions with their per-taxon
+    c, d too.  The restore passes default options: the checkpointed session's capacity (1000) comes back with it."""
     import os
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "datasets", "g10s10.txt")
     ds = sa.Dataset.load(path)
@@ -282,15 +283,16 @@ def test_checkpoint_carries_records(tmp_path, manycd):
         sum_full = s.summaries()
         cv_full = s.fetch_cd_vectors() if manycd else None
     ck = str(tmp_path / "rec.srck")
-    with sa.Session(ds, seeds, calls_per_launch=H, manycd=manycd) as s:
+    with sa.Session(ds, seeds, calls_per_launch=T, manycd=manycd) as s:
         s.run(H, save=True)
         s.checkpoint(ck)
     with open(ck, "rb") as fh:
-        head = fh.read(36)
-    assert np.frombuffer(head, "<u4", 1, 4)[0] == (6 if manycd else 5) and np.frombuffer(head, "<i4", 1, 32)[0] == H
-    r = sa.Session.restore(ds, ck, calls_per_launch=T, manycd=manycd)
+        head = fh.read(40)
+    assert np.frombuffer(head, "<u4", 1, 4)[0] == (8 if manycd else 7)
+    assert np.frombuffer(head, "<i4", 2, 32).tolist() == [H, T]
+    r = sa.Session.restore(ds, ck, manycd=manycd)
     try:
-        assert L.lib().sr_session_records(r.h) == H
+        assert L.lib().sr_session_records(r.h) == H and r.record_capacity == T
         r.run(T - H, save=True)
         ab2, cdl2 = r.fetch_records()
         sum2 = r.summaries()

@@ -60,7 +60,7 @@ def test_manycd_several_taxa_per_thread():
 
 
 def test_manycd_session_records_and_checkpoint(tmp_path):
-    """Session API: fetch_cd_vectors equals the oracle's per-taxon records; a checkpoint (version 6: the per-taxon
+    """Session API: fetch_cd_vectors equals the oracle's per-taxon records; a checkpoint (version 8: the per-taxon
     c, d and the buffered records) restores into a session that holds the first 3 records and continues exactly;
     restoring it as manycd = 0 is refused."""
     text = _text("g10s10.txt")

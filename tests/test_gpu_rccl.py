@@ -85,3 +85,25 @@ def test_bench_two_ranks_on_one_gpu_equals_single_process():
         assert len(p["rejected_checked"]) == 2 and not set(p["rejected_checked"]) & set(p["selected_checked"])
         assert p["chains"] == p["selected_checked"] + p["rejected_checked"]
     assert two["parity"]["rejected_checked"][-1] < 24   # rank 0's shard
+
+
+def test_bench_total_chains_ragged_three_ranks_equals_single_process():
+    """The metric's own form (BASELINE.json: 100 chains at 1/2/4/8 GPUs; script.py:55-62 runs a fixed 100): with
+    --total-chains 100 the chains are sharded contiguously and raggedly (dist.shard: 33/33/34 over three ranks,
+    13/13/13/13/12/12/12/12 over eight).  Three gloo ranks on the one GPU must give the single-process 100-chain
+    line bit for bit -- selection, gathered records, E[c], E[d], CORRMN -- and both lines say strong scaling."""
+    common = ["--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--calls-per-step", "20", "--total-chains", "100"]
+    single = _bench_line([sys.executable, "bench.py", "--gpus", "1"] + common)
+    three = _bench_line([sys.executable, "bench.py", "--gpus", "3", "--device-of-rank", "0,0,0", "--dist-backend",
+                         "gloo"] + common)
+    assert single["config"]["chains"] == three["config"]["chains"] == 100
+    assert single["config"]["chains_per_rank"] == [100] and three["config"]["chains_per_rank"] == [33, 33, 34]
+    assert single["scaling"] == three["scaling"] == "strong" and three["n_gpus"] == 3
+    a, b = single["selection"], three["selection"]
+    assert a["chains_selected"] == b["chains_selected"] and len(a["chains_selected"]) >= 1
+    assert a["records_sha256"] == b["records_sha256"]
+    for k in ("exp_c", "exp_d", "corr_mn"):
+        assert a[k] == b[k], k
+    assert single["parity"]["match"] and three["parity"]["match"]
+    assert three["parity"]["rejected_checked"][-1] < 33   # rank 0's shard
+    assert "config2" not in single and "config5" not in single   # --no-cpu-baseline: no extra legs

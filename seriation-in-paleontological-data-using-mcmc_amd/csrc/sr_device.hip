@@ -3760,6 +3760,13 @@ static int plan_kernel(int N, int M, int nh, int block_threads, int gm_force, in
   /* columns in LDS when the whole layout fits, else the HBM-column variant */
   int gm = 0;
   Lay L = sr_layout(N, M, NW, TB, false, pr != 0, nh);
+  if (L.total > 160 * 1024 && block_threads <= 0 && !mcd && !pr && gm_force != 1 && TB == 1024 && M <= 1024) {
+    /* mid-size shapes (513-1024 taxa, N up to ~320): the 1024-thread LDS layout does not fit, a 512-thread one (two
+       taxa per thread) does -- LDS columns there beat HBM columns at 1024 threads by 11-30 % (256 x 600, 200 x 800,
+       128 x 1000: profiles/r06c_ab_planner.json, same box, parity legs green) */
+    const Lay L2 = sr_layout(N, M, NW, 512, false, false, nh);
+    if (L2.total <= 160 * 1024 && sr_pick_kernel(512, N, M, false, false, nh, false, false)) { TB = 512; L = L2; }
+  }
   if (L.total > 160 * 1024) { gm = 1; L = sr_layout(N, M, NW, TB, true, false, nh); }
   if (gm_force >= 0 && gm_force != gm) {   /* explicit variant request (tests) */
     gm = gm_force;

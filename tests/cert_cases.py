@@ -44,8 +44,9 @@ def _margin(N):
 
 
 def u_ladder(ub, N):
-    """u values around a boundary ub: the boundary itself and +-1, 2, 4, 16, 256 ulps, then +-f * ABS for f from
-    2 down to 2^-11 in quarter-octave steps (the band an understated bound, e.g. ABS / 2^8, fails in)."""
+    """u values around a boundary ub: the boundary itself and +-1, 2, 4, 16, 256 ulps, +-f * ABS for f from 2 down
+    to 2^-11 in quarter-octave steps (the band an understated bound, e.g. ABS / 2^8, fails in), and from 2^1.5 up to
+    2^10.5 in half-octave steps (where the fast path certifies)."""
     out = {ub}
     for k in (1, 2, 4, 16, 256):
         out.add(_step(ub, k))
@@ -54,6 +55,10 @@ def u_ladder(ub, N):
     A = _margin(N)
     for q in range(0, 49):
         f = 2.0 ** (1 - q / 4.0)
+        out.add(ub + f * A)
+        out.add(ub - f * A)
+    for q in range(3, 22):   # and out to 2^10 ABS: the fast path certifies there (its picks are checked too)
+        f = 2.0 ** (q / 2.0)
         out.add(ub + f * A)
         out.add(ub - f * A)
     return sorted(u for u in out if 0.0 <= u < 1.0)

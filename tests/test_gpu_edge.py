@@ -292,7 +292,7 @@ def test_checkpoint_carries_records(tmp_path, manycd):
     assert np.frombuffer(head, "<i4", 2, 32).tolist() == [H, T]
     r = sa.Session.restore(ds, ck, manycd=manycd)
     try:
-        assert L.lib().sr_session_records(r.h) == H and r.record_capacity == T
+        assert L.lib().sr_session_records(r.h) == H and r.record_capacity >= T
         r.run(T - H, save=True)
         ab2, cdl2 = r.fetch_records()
         sum2 = r.summaries()

@@ -65,3 +65,44 @@ def test_batched_cli_rejects_bad_flags(capsys):
         with pytest.raises(SystemExit) as e:
             main(argv)
         assert e.value.code == 2
+
+
+def test_choose_chains_equals_pandas_parsing(tmp_path):
+    """script.py:76-96 reads each exp_data.csv with pd.read_csv (pandas' own float parser, here 2.x; the reference
+    pinned 1.0.4, absent) and maps values back by float equality.  On a Chains/ tree the oracle CLI wrote (24 chains
+    of g10s10, the reference's file format), launcher.choose_chains (Python float()) must select exactly the chains
+    the reference's pandas code selects, and every exp_loglik must parse to the same double."""
+    import subprocess
+    pd = pytest.importorskip("pandas")
+    here = os.path.dirname(os.path.abspath(__file__))
+    cli = os.path.join(os.path.dirname(here), "oracle", "build", "mcmc_oracle")
+    if not os.path.exists(cli):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(os.path.dirname(here), "oracle")])
+    ds = os.path.join(here, "golden", "datasets", "g10s10.txt")
+    for k in range(24):
+        d = tmp_path / ("run%02d" % k)
+        (d / "Chains" / "chain_00").mkdir(parents=True)
+        with open(ds, "rb") as fin:
+            subprocess.check_call([cli, "0", "2", "6"], cwd=str(d), stdin=fin, stderr=subprocess.DEVNULL,
+                                  env=dict(os.environ, GSL_RNG_SEED=str(k + 1)))
+        dst = tmp_path / "Chains" / ("chain_%02d" % k)
+        dst.mkdir(parents=True)
+        (dst / "exp_data.csv").write_bytes((d / "Chains" / "chain_00" / "exp_data.csv").read_bytes())
+
+    def pandas_choose(k):   # script.py:70-99 with pd.read_csv, literally
+        root = str(tmp_path / "Chains")
+        neg = [pd.read_csv(os.path.join(root, cd, "exp_data.csv")).exp_loglik.to_list()[0] for cd in os.listdir(root)]
+        lo, sd = min(neg), np.std(neg)
+        y = sorted(x for x in neg if lo - sd < x < lo + sd)
+        out = []
+        for z in y[:k]:
+            for cd in os.listdir(root):
+                if pd.read_csv(os.path.join(root, cd, "exp_data.csv")).exp_loglik.to_list()[0] == z:
+                    out.append(int(cd.split("_")[1]))
+        return sorted(out)
+
+    for cd in os.listdir(str(tmp_path / "Chains")):
+        path = os.path.join(str(tmp_path / "Chains"), cd, "exp_data.csv")
+        assert launcher._read_exp_loglik(path) == pd.read_csv(path).exp_loglik.to_list()[0], cd
+    for k in (1, 2, 8):
+        assert launcher.choose_chains(k, root=str(tmp_path)) == pandas_choose(k)

@@ -11,7 +11,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SHAPES = [(341, 890), (400, 700), (250, 1000)]
+SHAPES = [(256, 600), (200, 800), (128, 1000)]
 VARIANTS = {"lds512": ["--block-threads", "512", "--columns", "lds"],
             "hbm1024": ["--block-threads", "1024", "--columns", "hbm"]}
 COMMON = ["--no-cpu-baseline", "--legs", "none", "--parity-chains", "2", "--parity-rejected", "0", "--parity-calls", "2",

@@ -1,6 +1,7 @@
 #!/bin/bash
 # One full GPU-box pass for the round record: smoke, GPU test suite, the default bench (CPU
-# baseline included), rocprofv3 --kernel-trace --stats of that SAME bench command, separate --pmc
+# baseline and the config2 / config5 legs included), rocprofv3 --kernel-trace --stats of the headline bench command
+# (--legs none --no-cpu-baseline: the same timed workload, without the legs' other kernels), separate --pmc
 # passes over it (HBM FETCH_SIZE / WRITE_SIZE; SQ issue / park split, instruction mix, LDS), then
 # config 5 (1024 x 2048, HBM columns) with its own bench line (after 3 warm-up launches, and after 100 = 2000
 # sweeps: c5_bench_ss, nearer the steady state of the headline's 1000 warm-up calls), kernel trace and FETCH / WRITE / SQ
@@ -13,6 +14,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${1:-round}
 mkdir -p "$OUT"
 B="bench.py"
+BT="bench.py --legs none --no-cpu-baseline"   # the headline's kernels alone (the legs run other shapes)
 P="bench.py --no-cpu-baseline --parity-chains 0 --steps 5 --warmup 3"
 C5="bench.py --no-cpu-baseline --parity-chains 0 --sites 1024 --taxa 2048 --calls-per-step 2 --steps 10 --warmup 3 --block-threads 1024"
 # the config-5 bench line re-checks its first 4 saved calls of 2 selected chains against the oracle (the CPU
@@ -24,8 +26,8 @@ if [ "$2" != "skip-tests" ]; then
 timeout -k 10 240 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 &&
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || exit $?
 fi
-timeout -k 10 300 python $B > "$OUT/bench.json" 2> "$OUT/bench.err" &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 $B > "$OUT/prof.log" 2>&1 &&
+timeout -k 10 500 python $B > "$OUT/bench.json" 2> "$OUT/bench.err" &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 $BT > "$OUT/prof.log" 2>&1 &&
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o f -- python3 $P > "$OUT/pmc_fetch.log" 2>&1 &&
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o w -- python3 $P > "$OUT/pmc_write.log" 2>&1 &&
 timeout -s KILL 180 rocprofv3 --pmc $SQA --output-format csv -d "$OUT/pmc_sq" -o s -- python3 $P > "$OUT/pmc_sq.log" 2>&1 &&

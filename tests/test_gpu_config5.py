@@ -108,3 +108,36 @@ def test_config5_100_chains_split_grid(config5):
         assert rc == 0
         assert np.array_equal(ab[i].astype(np.int32), ri), "chain %d: integers differ from the oracle" % i
         assert np.array_equal(cdl[i].view(np.uint64), rdb.view(np.uint64)), "chain %d: c/d/loglik differ" % i
+
+
+def test_config5_converged_regime_equals_oracle_digests(config5):
+    """Config 5 in the regime its rates are quoted at: 4 chains (seeds 1-4) under the reference CLI's protocol,
+    1000 burn-in + 1000 saved calls (mcmc.c:140-185; 20 000 sweeps per chain), on the product's default config-5
+    kernel (split chains, cooperative launch), against the committed oracle digests (tests/golden/config5.json,
+    made by tests/golden/make_golden_c5.py: ~28 min of oracle time in the build container).  Every saved call's
+    a||b||pi digest, c / d / loglik bits and the exp_data row must match -- the long-walk window trims (SR_QSPAN),
+    the grouped f64 Gibbs checkpoints and the LDS checkpoints run at depth here, where the short parity tests
+    above (101 calls) do not reach.  mcmc.c:918-996, 1127-1682."""
+    import hashlib
+    import json
+    import os
+    from golden.make_golden import record_digest
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "config5.json")) as fh:
+        g = json.load(fh)
+    assert g["dataset_sha256"] == hashlib.sha256(config5).hexdigest()
+    ds = sa.Dataset.parse(config5, maxs=0)
+    seeds = [ch["seed"] for ch in g["chains"]]
+    with sa.Session(ds, seeds, calls_per_launch=g["saved_calls"]) as s:
+        assert s.kernel == "split"
+        for _ in range(g["burnin_calls"] // 50):
+            s.run(50, save=False)
+        for _ in range(g["saved_calls"] // 50):
+            s.run(50, save=True)
+        ab, cdl = s.fetch_records()
+        rows = s.summaries()
+    for k, ch in enumerate(g["chains"]):
+        dig = [record_digest(r.astype(np.int32)) for r in ab[k]]
+        bad = [i for i in range(len(dig)) if dig[i] != ch["sha256"][i]]
+        assert not bad, "seed %d: integer state differs from saved call %d on" % (ch["seed"], bad[0])
+        assert [[float(v).hex() for v in r] for r in cdl[k]] == ch["cdl_hex"], ch["seed"]
+        assert [float(v).hex() for v in rows[k, 1:4]] == ch["exp_hex"], ch["seed"]

@@ -142,3 +142,29 @@ def test_summaries_match_exp_data_bits():
         row = sd.summaries_from_records([7], o["rec_dbl"][None])[0]
         assert row[0] == 7
         assert [float(v).hex() for v in row[1:]] == [float(v).hex() for v in o["exp"]], seed
+
+
+def test_gloo_world8_ragged_100_chains():
+    """The metric's own N = 8 form on the CPU: 100 chains over 8 gloo ranks in ragged contiguous shards (12 or 13
+    chains each, bench.py --gpus 8 --total-chains 100), both collectives and the statistics equal to one process
+    holding all 100 chains (script.py:55-99)."""
+    world, n_total = 8, 100
+    assert sorted({len(sd.shard(n_total, world, r)) for r in range(world)}) == [12, 13]
+    ctx = mp.get_context("spawn")
+    mgr = ctx.Manager()
+    out = mgr.dict()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+        assert p.exitcode == 0
+    rows, sel, sab, scd, stats = _single_process(n_total)
+    assert 0 < len(sel) <= K
+    for r in range(world):
+        b, s_, ab_b, cd_b, st, dev_same = out[r]
+        assert dev_same
+        assert b == rows.tobytes() and s_ == sel
+        assert ab_b == sab.tobytes() and cd_b == scd.tobytes()
+        assert st == stats

@@ -354,8 +354,8 @@ def main():
                     "several ranks on one GPU, which RCCL does not allow)")
     ap.add_argument("--no-save", action="store_true", help="sample without saving records (SURVEY.md 8(d) "
                     "asks for both; the default saves one record per call, as the reference's sampling phase)")
-    ap.add_argument("--legs", default="auto", help="extra workloads in the same line at N = 1: comma-separated from "
-                    "config2, config5; none; auto = both unless --no-cpu-baseline or N > 1")
+    ap.add_argument("--legs", default="auto", help="extra workloads in the same line at N = 1 (ignored at N > 1): "
+                    "comma-separated from config2, config5; none; auto = both unless --no-cpu-baseline or N > 1")
     args = ap.parse_args()
     legs = set()
     if args.legs == "auto":
@@ -407,7 +407,7 @@ def main():
         cpu = cpu_baseline(args.dataset, warm_calls, args.cpu_calls, workers)
         cpu_o0 = cpu_baseline(args.dataset, warm_calls, max(1, args.cpu_calls // 4), workers, "O0")
         cpu_o0["kind"] = "port (reference-like -O0 build)"
-    if rank == 0 and "config2" in legs:
+    if rank == 0 and world == 1 and "config2" in legs:
         import tempfile
         tmp = tempfile.mkdtemp(prefix="sr_bench_c2_")
         if not args.no_cpu_baseline:

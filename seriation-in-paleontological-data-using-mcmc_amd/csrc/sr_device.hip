@@ -324,6 +324,15 @@ __device__ __forceinline__ void gsync()
 #define FST(ph) do { } while (0)
 #define STAMP_STORE(dst) do { } while (0)
 #endif
+/* SR_STAMP_BAR (with SR_STAMPS, diagnostic): the cycles each wave spends inside the sweep loop's workgroup barriers,
+   accumulated in stamp slot 15 (tools/stamp_profile.py: "barrier wait") -- the part of SQ_WAIT_ANY that is barrier
+   wait rather than s_waitcnt on LDS / memory */
+#if defined(SR_STAMPS) && defined(SR_STAMP_BAR)
+#define SR_SYNC() do { const unsigned long long tb_ = __builtin_amdgcn_s_memtime(); __syncthreads(); \
+  st_acc[15] += __builtin_amdgcn_s_memtime() - tb_; } while (0)
+#else
+#define SR_SYNC() __syncthreads()
+#endif
 #ifdef SR_STAMP_GIBBS   /* phase B split: slots 1 prefix+pass0, 2 pass1, 3 pass2, 4 tail */
 #define GSTAMP(ph) do { unsigned long long t_ = __builtin_amdgcn_s_memtime(); gst[ph] += t_ - *gst_t; *gst_t = t_; } while (0)
 #define GSTAMP_ARGS , unsigned long long *gst, unsigned long long *gst_t
@@ -2501,7 +2510,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       }
       STAMP(0);
       FST(11);
-      __syncthreads();
+      SR_SYNC();
       FST(11);
       {
         int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
@@ -2527,12 +2536,12 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               const double y = d_samplebeta<false>(R, cv[k * M + m], (double)(k ? scnt[M + m] : scnt[3 * M + m]),
                                                    (double)(k ? scnt[2 * M + m] : scnt[m]), k ? SR_MIND : SR_MINC,
                                                    k ? SR_MAXD : SR_MAXC, tid, TB, tb);
-              __syncthreads();   /* every thread has read cv[k M + m] */
+              SR_SYNC();   /* every thread has read cv[k M + m] */
               if (tid == 0) cv[k * M + m] = y;
             }
-          __syncthreads();
+          SR_SYNC();
           for (int m = tid; m < 2 * M; m += TB) cx[m] = sr_log_m(1. - sr_exp_m(cv[m], &tb), &tb);
-          __syncthreads();
+          SR_SYNC();
           c = cv[0];
           d = cv[M];
           if (tid == 0) { misc[MS_ACC + 0] += M - 1; misc[MS_ACC + 1] += M - 1; }   /* samplec returns M (mcmc.c:785) */
@@ -2599,7 +2608,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         }
         if (lane == 0 && (!SH8 || wave == (PR ? 4 : 0))) *reinterpret_cast<double2 *>(T8w + 2 * 256) = make_double2(0.0, 1.0);
       }
-      if constexpr (SH8) __syncthreads(); else wsync();
+      if constexpr (SH8) SR_SYNC(); else wsync();
 
 #ifdef SR_STAMP_GIBBS
       STAMP(5);
@@ -2615,7 +2624,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         const int nround = (2 * M + SR_RNG_SLACK <= rcap) ? 1 : (M + TB - 1) / TB;
         for (int rd = 0; rd < nround; ++rd) {
         const int mlo = (nround == 1) ? 0 : rd * TB, mhi = (nround == 1) ? M : min(M, mlo + TB);
-        if (rd > 0) __syncthreads();   /* every thread is done with the previous round's words */
+        if (rd > 0) SR_SYNC();   /* every thread is done with the previous round's words */
         FST(1);
         rng_ensure(R, min(2 * (mhi - mlo) + SR_RNG_SLACK, rcap), tid, TB);
         FST(8);
@@ -2726,7 +2735,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       STAMP(1);
       if (GM && want_logl) {   /* mcmc_logl with the terms in HBM: each wave reads them 64 at a time
                                   (coalesced, 4 chunks in flight) and adds them in m order through readlane */
-        if constexpr (SP) xsync(); else __syncthreads();
+        if constexpr (SP) xsync(); else SR_SYNC();
         double s = 0.0;
         for (int c0 = 0; c0 < M; c0 += 256) {
           double v[4];
@@ -2745,7 +2754,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
         }
         loglik = s;
       } else if (want_logl) {   /* mcmc_logl (mcmc.c:639-645), sequential over m, lane 0 of every wave */
-        __syncthreads();
+        SR_SYNC();
         if (PR ? tid == 0 : lane == 0) {
           double s = 0.0;
           int m = 0;
@@ -2757,7 +2766,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           if (PR) *reinterpret_cast<double *>(&misc[MS_LOGL]) = s; else *xs = s;
         }
         if constexpr (PR) {   /* one sum (thread 0), read by all behind a barrier */
-          __syncthreads();
+          SR_SYNC();
           loglik = *reinterpret_cast<const double *>(&misc[MS_LOGL]);
         } else {
           wsync();
@@ -2784,7 +2793,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                                  (a half not starting at a multiple of TB): their limits and counts, read by the
                                  owner threads below, are ordered by a barrier */
           const bool multi = 2 * M + SR_RNG_SLACK > (SR_RING - 1) * SR_MT_N - (SR_MT_N - 1);
-          if (multi && (olo % TB) != 0 && (olo / TB + 1) * TB < ohi) __syncthreads();
+          if (multi && (olo % TB) != 0 && (olo / TB + 1) * TB < ohi) SR_SYNC();
         }
         /* the lane-parallel proposal tables (ptab) hold "a proposal of each kind starting at word o"
            for the 128 words from stream position (tblk, toff) (the sweep's cooperative fill, or a wave's
@@ -3250,7 +3259,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             STAMP_K(PK_PI3);
           }
           FST(4);
-          __syncthreads();
+          SR_SYNC();
           if constexpr (SP) {   /* this half's sums of the batch's proposals (lane p of wave 0), exchanged */
             if (wave == 0 && lane >= p0 && lane < pend && lane < 16 && !((vpk >> 26) & 1)) {
               int X0 = 0, X1 = 0, Y0 = 0, Y1 = 0;
@@ -3539,9 +3548,9 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           FST(10);
           /* the hard tables only when a hard site moved (the columns' hard-site bits never change) */
           if (hmoved) {   /* (block-uniform: every wave holds the same hard positions) */
-            if constexpr (SHT) __syncthreads(); else wsync();   /* SHT: every wave is past its reads of the shared tables */
+            if constexpr (SHT) SR_SYNC(); else wsync();   /* SHT: every wave is past its reads of the shared tables */
             build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane, !SHT || wave == 0);
-            if constexpr (SHT) __syncthreads();                 /* ... and the next batch reads the new ones */
+            if constexpr (SHT) SR_SYNC();                 /* ... and the next batch reads the new ones */
             if (SR_DOUBLE == 8 && !SHT) { wsync(); build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane); }
             tvalid = false;
             if (SR_COOP_TABLES > 1 && p0 < 16) {
@@ -3555,7 +3564,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               const int savail = min((int)((R.gen - tblk) * SR_MT_N - toff), 128);
               for (int k = tid; k < 3 * 128; k += TB)
                 ptab_fill(ptab, ring, sbase, savail, k & 127, k >> 7, N, nh, hcnt, nhall, mdN, mdN1, md2, mdH, mdH1);
-              __syncthreads();
+              SR_SYNC();
               tvalid = true;
             }
           }
@@ -3566,7 +3575,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       }
       STAMP(7);
       FST(0);
-      __syncthreads();
+      SR_SYNC();
       FST(11);
     } /* sweeps */
 

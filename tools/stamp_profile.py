@@ -62,6 +62,11 @@ if not os.environ.get("SR_FINE") and not os.environ.get("SR_GIBBS_STATS"):
     print("  phase-C batches/sweep %.3f; proposals drawn into batches/sweep %.2f (16 needed); proposal-table refills/sweep "
           "%.3f; scalar-path proposals/sweep %.3f" % (bs[1], bs[2], bs[3], bs[0]))
 print("  accepted per sweep (profiled launch, chain mean): pi1 %.3f pi2 %.3f swap %.3f pi3 %.3f" % tuple(acc[3:7]))
+if os.environ.get("SR_BAR") and nw <= 8:   # SR_STAMPS + SR_STAMP_BAR builds: cycles inside the sweep loop's barriers
+    bar = out[:, 9:9 + nw, 7].astype(np.float64) / 2.0 / sweeps
+    tot = per[:, :, :8].sum(2)
+    print("  barrier wait (cycles/sweep): wave0 %.0f, mean wave %.0f = %.1f %% of the mean wave's sweep" % (
+        bar[:, 0].mean(), bar.mean(), 100.0 * bar.mean() / tot.mean()))
 if os.environ.get("SR_GIBBS_STATS"):
     h = out[:, 0, :].astype(np.float64).sum(0)
     nd = max(h[4], 1)

@@ -180,3 +180,26 @@ def test_init_chain_hard_sites_near_n(N, nh):
         assert cdl.view(np.uint64).tolist() == o["init_cdl"].view(np.uint64).tolist()
         assert sorted(pi.tolist()) == list(range(N))
         assert (np.diff(pi[hard]) > 0).all()
+
+
+def test_parallel_chain_init_equals_serial(tmp_path, monkeypatch):
+    """session_new initialises the chains on several host threads (init_chains: each chain its own RNG and state
+    slice); the state must be the serial loop's byte for byte.  sr_host_initial_checkpoint writes that state
+    (mcmc.c:339-437, 592-708 restated) without a device: 1 thread against 7, 37 chains of g5s5 and of a synthetic
+    700 x 300 matrix."""
+    import ctypes
+    import os
+    import seriation_amd as sa
+    from seriation_amd import _lib as L
+    here = os.path.dirname(os.path.abspath(__file__))
+    import gen_synthetic
+    X, hard = gen_synthetic.make(700, 300, 5)
+    for ds in (sa.Dataset.load(os.path.join(here, "golden", "datasets", "g5s5.txt")), sa.Dataset(X, hard)):
+        specs = sa.core.make_specs(list(range(11, 48)))
+        out = []
+        for nt in ("1", "7"):
+            monkeypatch.setenv("SR_INIT_THREADS", nt)
+            p = tmp_path / ("init%s.srck" % nt)
+            assert L.lib().sr_host_initial_checkpoint(ctypes.byref(ds.c), specs, 37, os.fsencode(str(p))) == 0
+            out.append(p.read_bytes())
+        assert out[0] == out[1]

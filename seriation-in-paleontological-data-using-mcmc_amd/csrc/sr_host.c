@@ -473,7 +473,8 @@ static int init_chain(const sr_dataset *ds, uint64_t seed, sr_state_host *st, in
 /* The chains' initialisation (mcmc_readmodel's state, initab, randomize, count01, logl and the position-ordered bit
    columns: O(N M) per chain, ~20 ms at 1024 x 2048) on several host threads: chains are independent (own RNG, own
    slice of st), so the state is the serial loop's bit for bit.  Threads: the CPUs this process may run on (its
-   affinity mask), at most 32 and one per chain; SR_INIT_THREADS overrides; serial when the initab notes go to
+   affinity mask, and OMP_NUM_THREADS when set), at most 32 and one per chain; SR_INIT_THREADS overrides; serial
+   when the initab notes go to
    stderr (their order is the reference's) or for one chain. */
 typedef struct {
   const sr_dataset *ds;
@@ -505,6 +506,8 @@ static int init_chains(const sr_dataset *ds, const sr_chain_spec *specs, int n, 
   int nt = 1;
   cpu_set_t cs;
   if (sched_getaffinity(0, sizeof cs, &cs) == 0) nt = CPU_COUNT(&cs);
+  const char *omp = getenv("OMP_NUM_THREADS");   /* a launcher's thread budget (the GPU box's CPU share) */
+  if (omp && atoi(omp) > 0 && atoi(omp) < nt) nt = atoi(omp);
   const char *e = getenv("SR_INIT_THREADS");
   if (e && atoi(e) > 0) nt = atoi(e);
   if (nt > 32) nt = 32;

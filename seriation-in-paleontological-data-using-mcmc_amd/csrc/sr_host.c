@@ -474,8 +474,7 @@ static int init_chain(const sr_dataset *ds, uint64_t seed, sr_state_host *st, in
    columns: O(N M) per chain, ~20 ms at 1024 x 2048) on several host threads: chains are independent (own RNG, own
    slice of st), so the state is the serial loop's bit for bit.  Threads: the CPUs this process may run on (its
    affinity mask, and OMP_NUM_THREADS when set), at most 32 and one per chain; SR_INIT_THREADS overrides; serial
-   when the initab notes go to
-   stderr (their order is the reference's) or for one chain. */
+   when the initab notes go to stderr (their order is the reference's) or for one chain. */
 typedef struct {
   const sr_dataset *ds;
   const sr_chain_spec *specs;

@@ -208,7 +208,9 @@ int32_t sr_session_specialized(const sr_session *s);
  * SR_F_GENERIC_KERNEL) would run, without a GPU: compiled from the source snapshot the library was built
  * from (build/spec/) with hipcc into the cache ($SR_JIT_CACHE, else build/jit/ next to the library), so
  * that session creation finds it.  1 ready, 0 the session runs no specialised kernel, SR_EIO the code
- * object could not be produced (stderr says why), SR_EUNSUPPORTED / SR_EINVAL as sr_session_create. */
+ * object could not be produced (stderr says why), SR_EUNSUPPORTED / SR_EINVAL as sr_session_create.
+ * (Session creation compiles a missing shape itself unless SR_JIT=cache: then only embedded or cached objects
+ * are used and any other shape runs the generic kernel -- no compiler is spawned at run time.) */
 int sr_specialize(const sr_dataset *ds, const sr_run_opts *opts);
 /* Checkpoint / resume (the reference has none): the full chain state (columns, pi,
    limits, counts, c/d/loglik, MT19937 ring and cursor, acceptance counters) and the session's buffered

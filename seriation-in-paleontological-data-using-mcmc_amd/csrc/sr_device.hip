@@ -29,6 +29,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 #include <type_traits>
 #define SR_TABLES_NO_ARRAYS
 #include "sr_tables.h"
@@ -3836,7 +3837,16 @@ static int srk_spec_resolve(int N, int M, int nh, const srk_kplan &kp, srk_spec_
   src->img = sr_spec_embedded(&src->s, &src->bytes);
   src->path[0] = 0;
   if (src->img) return 0;
-  const int rc = sr_spec_object(&src->s, src->path, sizeof src->path, 1);
+  /* SR_JIT=cache: a deployment that never spawns the compiler from a session -- embedded or cached (sr_specialize
+     ahead of time) objects only, else the generic kernel */
+  const char *jm = getenv("SR_JIT");
+  int rc;
+  if (jm && !strcmp(jm, "cache")) {
+    rc = sr_spec_path(&src->s, src->path, sizeof src->path);
+    if (!rc && access(src->path, R_OK) != 0) rc = SR_SPEC_ENOJIT;
+  } else {
+    rc = sr_spec_object(&src->s, src->path, sizeof src->path, 1);
+  }
   if (rc) sr_spec_note(rc, rc == SR_SPEC_ECC ? src->path : nullptr);
   return rc;
 #endif

@@ -55,6 +55,7 @@ typedef struct { int TB, NWM, N, M, NH, force; } sr_spec_shape;
 #define SR_SPEC_EPROF (-5)
 #define SR_SPEC_ELOAD (-6)
 #define SR_SPEC_ECACHE (-7)
+#define SR_SPEC_ENOJIT (-8)   /* not embedded, not cached, and run-time compiles are off (SR_JIT=cache) */
 /* the cache path of the shape's code object (0), or a reason code */
 int sr_spec_path(const sr_spec_shape *s, char *path, size_t len);
 /* the path of the shape's code object, compiled into the cache first if it is missing (0), or a reason;

@@ -180,6 +180,8 @@ const char *sr_spec_reason(int code)
     case SR_SPEC_EPROF: return "a profiler tool library is preloaded and the code object is not cached";
     case SR_SPEC_ELOAD: return "the code object did not load or does not match this library";
     case SR_SPEC_ECACHE: return "the cache directory cannot be created or written ($SR_JIT_CACHE / build/jit)";
+    case SR_SPEC_ENOJIT: return "not embedded, not in the cache, and SR_JIT=cache forbids compiling at run time "
+                                "(sr_specialize fills the cache ahead)";
     default: return "unknown";
   }
 }

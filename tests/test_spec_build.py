@@ -189,3 +189,29 @@ def test_embedded_objects_are_in_the_library():
     assert BENCH_KERNEL in blob
     assert sa.lib().sr_spec_is_embedded(250, 500, 12, 0) == 0
     assert sa.lib().sr_spec_is_embedded(256, 512, 12, 1024) == 0
+
+
+SESSION_CHILD = textwrap.dedent("""
+    import sys
+    sys.path.insert(0, %r)
+    import seriation_amd as sa
+    ds = sa.Dataset.load(sys.argv[1], maxs=0)
+    try:
+        sa.Session(ds, [1])
+        print("created")
+    except sa.SrError as e:
+        print("refused %%d" %% e.code)
+""" % PKG)
+
+
+def test_cache_only_mode_never_spawns_the_compiler(tmp_path):
+    """SR_JIT=cache: a session whose shape is neither embedded nor cached gets the generic kernel and one line saying
+    why -- no compiler is spawned, nothing is written to the cache (the session's own shape resolution runs before
+    any HIP call, so this holds without a GPU too); sr_specialize still fills the cache ahead of time."""
+    env = dict(os.environ, SR_JIT="cache", SR_JIT_CACHE=str(tmp_path))
+    r = subprocess.run([sys.executable, "-c", SESSION_CHILD, SUBJECT], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "SR_JIT=cache forbids compiling at run time" in r.stderr
+    assert "compiling the sweep kernel" not in r.stderr
+    assert not [f for f in os.listdir(tmp_path) if f.endswith(".co")]

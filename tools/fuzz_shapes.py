@@ -1,6 +1,6 @@
 """Parity fuzz over random shapes (GPU): random N, M, hard sites, block size, column placement and c/d mode, each run against
 the CPU oracle (2 burn-in + 3 saved calls, 2 seeds).  Prints one line per shape and exits 1 on the first mismatch.
-    python tools/fuzz_shapes.py [count] [seed] [--lds]"""
+    python tools/fuzz_shapes.py [count] [seed] [--lds | --mid]"""
 import os
 import sys
 
@@ -16,16 +16,17 @@ from test_gpu_edge import make_text    # noqa: E402
 
 def main():
     lds = "--lds" in sys.argv   # LDS-column shapes (register and LDS walks; with SR_JIT unset, specialised kernels)
-    argv = [a for a in sys.argv[1:] if a != "--lds"]
+    mid = "--mid" in sys.argv   # the planner's mid-size shapes (N 64-320, M 513-1024: 512-thread LDS columns, round 6)
+    argv = [a for a in sys.argv[1:] if a not in ("--lds", "--mid")]
     count = int(argv[0]) if argv else 12
     rng = np.random.default_rng(int(argv[1]) if len(argv) > 1 else 2026)
     for t in range(count):
-        N = int(rng.integers(8, 544 if lds else 1500))
-        M = int(rng.integers(2, 1025 if lds else 2600))
+        N = int(rng.integers(64, 321)) if mid else int(rng.integers(8, 544 if lds else 1500))
+        M = int(rng.integers(513, 1025)) if mid else int(rng.integers(2, 1025 if lds else 2600))
         nh = int(min(N - 2, rng.choice([0, 3, 12, 40, 70])))
-        tb = int(rng.choice([0, 256, 512, 1024]))
-        cols = "auto" if lds else str(rng.choice(["auto", "hbm"]))
-        mcd = int(rng.random() < 0.2)   # manycd: per-taxon c, d (1024 threads)
+        tb = 0 if mid else int(rng.choice([0, 256, 512, 1024]))
+        cols = "auto" if (lds or mid) else str(rng.choice(["auto", "hbm"]))
+        mcd = 0 if mid else int(rng.random() < 0.2)   # manycd: per-taxon c, d (1024 threads)
         if mcd:
             tb = int(rng.choice([0, 1024]))
         if tb and M > tb and cols == "auto" and rng.random() < 0.5:

@@ -93,4 +93,12 @@ def run_all(lib):
 
 if __name__ == "__main__":
     import seriation_amd as sa
-    print(json.dumps(run_all(sa.lib())))
+    if len(sys.argv) > 1:   # more seeds (a soak beyond the test suite's fixed cases): cert_run.py SEED ...
+        out = {}
+        for sd in sys.argv[1:]:
+            k = int(sd)
+            out[sd] = {"gibbs": [gibbs_summary(sa.lib(), *g, seed=k) for g in GIBBS_SHAPES],
+                       "decide": decide_summary(sa.lib(), seed=k + 100)}
+        print(json.dumps(out))
+    else:
+        print(json.dumps(run_all(sa.lib())))

@@ -118,6 +118,9 @@ static inline int om_rng_env_setup(unsigned long *seed)
         if ((k + 1) % 4 == 0) fputc('\n', stderr);
       }
       fputc('\n', stderr);
+      /* Departure (parity unpinned): GSL 2.6 follows the list with GSL_ERROR_VOID("unknown generator"), whose
+         default handler prints its own "gsl: env.c:<line>: ERROR: unknown generator" line and abort()s; the
+         oracle and the product both return exit status 1 here (no GSL to take the handler's exact text from) */
       return 2;
     }
     if (strcmp(p, "mt19937") != 0) {

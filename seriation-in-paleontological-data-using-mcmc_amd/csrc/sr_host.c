@@ -770,9 +770,10 @@ static int download(sr_session *s, sr_state_host *st)
  * File: "SRCK" | u32 version | i32 N, M, nh, nchains | u64 FNV-1a of the dataset (X, hard) | [v5-v8: i32 nrec]
  * | [v7, v8: i32 record capacity of the checkpointed session]
  * | sr_chain_spec[nchains] | the device state as sr_state_host arrays (P, rpi, hp, ab, cnt, cdl, mt, rng, acc;
- * manycd: cdv) | [v5, v6: the session's buffered records: ab_pi [nchains][nrec][2M+N] i16, cdl [nchains][nrec][3]
+ * manycd: cdv) | [v5-v8: the session's buffered records: ab_pi [nchains][nrec][2M+N] i16, cdl [nchains][nrec][3]
  * f64, manycd: cdv [nchains][nrec][2M] f64], little-endian.  A restore keeps at least the checkpointed session's
- * record capacity, so the saves that session could still make fit without the caller re-supplying calls_per_launch.  Restoring uploads the same words, so the continued
+ * record capacity, so the saves that session could still make fit without the caller re-supplying
+ * calls_per_launch.  Restoring uploads the same words, so the continued
  * chains are the ones an uninterrupted session produces, and summaries over the records (compute_exp_data,
  * mcmc.c:53-67) span the whole sampling phase across the interruption (tests/test_gpu_edge.py). */
 static uint64_t dataset_hash(const sr_dataset *ds)

@@ -528,7 +528,10 @@ def main():
                         "re-read every sweep; HBM bandwidth far from peak)")
     limiter["source"] = traffic_src
     out = {
-        "metric": "chain-iterations/sec (100 chains, 256x512 matrix) at 1/2/4/8 MI355X",
+        # BASELINE.json's metric names the headline workload; any other shape or chain count says what it ran
+        "metric": ("chain-iterations/sec (100 chains, 256x512 matrix) at 1/2/4/8 MI355X"
+                   if (ds.N, ds.M, total) == (256, 512, 100) else
+                   "chain-iterations/sec (%d chains, %dx%d matrix) at %d MI355X" % (total, ds.N, ds.M, world)),
         "value": value,
         "unit": "chain-iterations/s",
         "n_gpus": world,

@@ -45,7 +45,7 @@ extern char **environ;
 static const char *const spec_files[] = {"sr_device.hip", "sr_math.h", "sr_rng.h", "sr_tables.h", "sr_internal.h",
                                          "seriation.h"};
 #define SPEC_NFILES (sizeof spec_files / sizeof spec_files[0])
-#define SPEC_FLAGS "--genco -O3 -std=c++17 -ffp-contract=off -fno-fast-math"
+#define SPEC_FLAGS "--genco -O3 -std=c++17 -ffp-contract=off -fno-fast-math -mllvm -disable-machine-licm"   /* as the Makefile's HIPFLAGS */
 
 static uint64_t fnv(uint64_t h, const void *p, size_t n)
 {

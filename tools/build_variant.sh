@@ -16,7 +16,7 @@ cp "$SRCF" "$D/spec/sr_device.hip"
 H=$(build/srhash "$D/spec")
 gcc -O2 -std=gnu11 -pthread -fPIC -ffp-contract=off -fno-fast-math -Wall -I../include -Icsrc \
   -DSR_SPEC_HASH=0x${H}ull -DSR_ARCH='"gfx950"' -DSR_SPEC_EXTRA="\"$2\"" -c -o "$D/sr_spec.o" csrc/sr_spec.c
-/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function \
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -mllvm -disable-machine-licm -Wall -Wno-unused-function \
   -I../include -Icsrc $2 -c -o "$D/sr_device.o" -x hip "$SRCF"
 /opt/rocm/bin/hipcc -shared -fPIC -o "$D/libseriation.so" build/sr_host.o "$D/sr_device.o" build/sr_post.o "$D/sr_spec.o" -ldl -lm -pthread
 echo "$D/libseriation.so"

@@ -2326,10 +2326,11 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   static_assert(!MCD || (!PR && !SP && NWM == 0), "manycd: generic one-workgroup kernels only");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NWV = TB / 64;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  /* wave: scalar in the HBM-column kernels (readfirstlane), so their per-wave LDS pointers live in SGPRs */
+  const int tid = threadIdx.x, lane = tid & 63, wave = GM ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
   /* PR (pair kernels): lanes 2t, 2t+1 own taxon t (tx) together, hf = which half of the pair;
      otherwise one thread per taxon */
-  const int hf = PR ? (tid & 1) : 0, tx = PR ? (tid >> 1) : tid;
+  const int tx = PR ? (tid >> 1) : tid;   /* (hf: per sweep, below) */
   constexpr int TXS = PR ? TB / 2 : TB;   /* taxon stride */
   /* SP: two workgroups per chain (sr_sp_half); both hold the whole block-uniform state (RNG ring,
      rpi, hard tables, c, d, loglik) and take every decision identically, each from sums exchanged
@@ -2360,7 +2361,6 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   const int CKS = LCK ? TB : SP ? 2 * TB : sr_ckstride(M, TB);   /* SP: slots [half TB + tid] (LCK: [tid] in LDS) */
   using CKT = typename std::conditional<GM && SR_CK32, float, double>::type;   /* Gibbs checkpoints: f32 in HBM scratch, f64 in LDS */
   CKT *ckb = (GM && !LCK) ? (CKT *)A.gck + (size_t)chain * (SP ? sr_sp_ck(N, TB) : sr_gm_ck(N, M, TB)) : (CKT *)(void *)(smem + L.ck);
-  const int ckslot = (SP && !LCK) ? half * TB + tid : tid;   /* this thread's Gibbs checkpoint slots */
   int *ccnt = (int *)(smem + L.ccnt);
   int32_t *sab = GM ? A.ab + (size_t)chain * 2 * M : (int32_t *)(smem + L.sab);     /* a[M], b[M] */
   int32_t *scnt = GM ? A.cnt + (size_t)chain * 4 * M : (int32_t *)(smem + L.scnt);  /* t0[M], f0[M], t1[M], f1[M] */
@@ -2472,6 +2472,18 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
 
   for (int call = 0; call < A.calls; ++call) {
     for (int sw = 0; sw < A.spc; ++sw) {
+      /* HBM-column kernels: the per-lane indices re-derived from an opaque copy of the thread index each sweep, so
+         the addresses and lane masks built from them are computed where they are used instead of being hoisted out
+         of the sweep loop and spilled (config 5's split kernel: 53 -> 24 VGPR spills, one spilled dword reloaded
+         inside the loop; the LDS-column kernels run slower with it) */
+      int tid_sw = tid;
+      if constexpr (GM) __asm__ volatile("" : "+v"(tid_sw));
+      {
+      const int tid = tid_sw, lane = tid & 63;
+      const int hf = PR ? (tid & 1) : 0, tx = PR ? (tid >> 1) : tid;
+      const int mt = olo + tx;
+      const int ckslot = (SP && !LCK) ? half * TB + tid : tid;   /* this thread's Gibbs checkpoint slots */
+      (void)hf; (void)mt; (void)ckslot;
       const bool want_logl = (sw == A.spc - 1);
       /* this sweep's lane-parallel proposal tables, filled cooperatively (one entry per thread) before the
          phase-A barrier, at the stream position phase C most likely starts from: the c, d draws' fast path
@@ -3578,6 +3590,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
       FST(0);
       SR_SYNC();
       FST(11);
+      }
     } /* sweeps */
 
     /* ---------------- saved sample (mcmc_save_chain, mcmc.c:69-92) */

@@ -112,6 +112,13 @@ struct KArgs {
 #ifndef SR_SP_LCK
 #define SR_SP_LCK 1
 #endif
+/* split kernels whose LDS layout has room (LK): the own half's column prefix table in LDS (stride = the half's
+   taxa) and the Gibbs checkpoints in HBM scratch, instead of the checkpoints in LDS and the prefixes in HBM: the
+   prefixes are read several times per proposal and taxon, the checkpoints once per walk, and the L2 holds the
+   columns of 25 half-chains per XCD (config 5: 4.208 -> 4.151 ms per launch, profiles/r06u_ab_c5_lpre.json) */
+#ifndef SR_SP_LPRE
+#define SR_SP_LPRE 1
+#endif
 /* HBM-column kernels: one block-shared copy of the hard-site and 4-step tables (16 waves at 1024 threads held 64 N
    bytes of per-wave hard tables: at N ~ 1250 the layout passed 160 KB; shared, N reaches 4095 at 1024 threads) */
 #ifndef SR_GM_SHARED
@@ -241,7 +248,7 @@ __host__ __device__ static constexpr inline Lay sr_layout(int N, int M, int NW, 
   L.ht = o;    o = sr_al16(o + (sht ? 1 : (size_t)NWV) * (2 * N + 2) * 2);   /* per wave (gm: shared): hcnt[N+1], nhall[N] (int16) */
   const size_t rw = (pr || sr_regwalk(N, M, TB, gm, nh)) ? 1 : 0;   /* register walks (pair kernels too): byte tables instead of LDS checkpoints */
   L.ck = o;    o = sr_al16(o + g * (1 - rw) * ((N >> 5) + 1) * sr_ckstride(M, TB) * sizeof(double) +
-                           (lck ? (size_t)sr_lck_slots(N) * TB * sizeof(double) : 0));
+                           ((lck && !SR_SP_LPRE) ? (size_t)sr_lck_slots(N) * TB * sizeof(double) : 0));
   L.ccnt = o;  o = sr_al16(o + (size_t)2 * KT * 4);
   L.sab = o;   o = sr_al16(o + g * 2 * M * 4);
   L.scnt = o;  o = sr_al16(o + g * 4 * M * 4);
@@ -249,7 +256,9 @@ __host__ __device__ static constexpr inline Lay sr_layout(int N, int M, int NW, 
   L.hbw = o;   o = sr_al16(o + (size_t)NWV * NW * 4);                 /* per wave: hard bitmap */
   L.t4 = o;    o = sr_al16(o + NT * 160 * 8);                         /* per wave: 4-entry step tables (T4STRIDE) */
   L.t8 = o;    o = sr_al16(o + (rw ? NT : (gm ? 1 : 0)) * T8STRIDE * 8);   /* per wave (gm: one shared copy): 8-entry step tables */
-  L.pre = o;   o = sr_al16(o + g * (NW + 1) * M * 2);                 /* column prefix ones per word boundary */
+  /* column prefix ones per word boundary (SR_SP_LPRE split kernels: the own half's, (((M + 1) / 2 + 63) & ~63) taxa =
+     sr_sp_half) */
+  L.pre = o;   o = sr_al16(o + (g * M + ((lck && SR_SP_LPRE) ? (size_t)((((M + 1) / 2) + 63) & ~63) : 0)) * (NW + 1) * 2);
   L.part = o;  o = sr_al16(o + (size_t)2 * 16 * NWV * 8 * 4);         /* [2][proposal][wave] count sums */
   L.tot = o;   o = sr_al16(o + (size_t)2 * NWV * 4 * 4);               /* [2][wave] t0, f0, t1, f1 */
   L.xs = o;    o = sr_al16(o + (size_t)NWV * sizeof(double));          /* per-wave broadcast slot */
@@ -817,20 +826,20 @@ __device__ __noinline__ int draw_exact(const uint32_t *Pm, int M, int N, bool re
 
 /* ones of column m at positions [0, x) from the per-word prefix table (pre: column m's entries,
  * stride M; row k = ones in [0, 32k)) and one partial word */
-__device__ __forceinline__ int col_pre(const uint16_t *prem, const uint32_t *Pm, int M, int x)
+__device__ __forceinline__ int col_pre(const uint16_t *prem, const uint32_t *Pm, int M, int x, int PS = 0)
 {
   const int w = x >> 5, bits = x & 31;
   const uint32_t word = bits ? Pm[w * M] : 0u;
-  return (int)prem[w * M] + __popc(word & ((1u << bits) - 1u));
+  return (int)prem[w * (PS ? PS : M)] + __popc(word & ((1u << bits) - 1u));   /* PS: the table's own stride */
 }
 
 /* the same without a branch: the word read always (row 0 when x is a multiple of 32, masked to nothing),
    so a proposal's taxon terms carry no exec-mask branches and the slots' reads can be in flight together */
-__device__ __forceinline__ int col_pre_bf(const uint16_t *prem, const uint32_t *Pm, int M, int x)
+__device__ __forceinline__ int col_pre_bf(const uint16_t *prem, const uint32_t *Pm, int M, int x, int PS = 0)
 {
   const int w = x >> 5, bits = x & 31;
   const uint32_t word = Pm[(bits ? w : 0) * M];
-  return (int)prem[w * M] + __popc(word & ((1u << bits) - 1u));
+  return (int)prem[w * (PS ? PS : M)] + __popc(word & ((1u << bits) - 1u));
 }
 
 /* 32 walk bits [32k, 32k+32): fwd = positions, rev = positions N-1-w (bit i = walk 32k+i) */
@@ -932,7 +941,7 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, const uint16_t *pre
                                          int POo, double u, const CD &K, const sr_mtab &tb, double vA, double vB, double rA, double rB,
                                          const double *T4, const double *T8,
                                          typename std::conditional<B8 && SR_CK32, float, double>::type *ck,
-                                         int ckstride, uint64_t *fbk, int &dt0, int &df0,
+                                         int ckstride, int PS, uint64_t *fbk, int &dt0, int &df0,
                                          int &dt1, int &df1 GSTAMP_ARGS)
 {
   /* POo: ones among walk entries [0, o), from the caller's column prefix table */
@@ -1160,10 +1169,10 @@ __device__ __forceinline__ int draw_fast(const uint32_t *Pm, const uint16_t *pre
       yj = (j == khi) ? S : (double)ck[j * ckstride];   /* (Sj: y follows from it below) */
     }
     int Oj;   /* ones among walk entries [0, 32 j) */
-    if (!rev) Oj = (int)prem[j * M];
+    if (!rev) Oj = (int)prem[j * (PS ? PS : M)];
     else {    /* positions [N - 32 j, N) */
       const int x = N - 32 * j;
-      Oj = (int)prem[NW * M] - col_pre(prem, Pm, M, x);
+      Oj = (int)prem[NW * (PS ? PS : M)] - col_pre(prem, Pm, M, x, PS);
     }
     const int w0 = 32 * j;
     const uint32_t ww = walk_word(Pm, M, N, NW, rev, j);
@@ -1782,8 +1791,9 @@ __device__ __forceinline__ void ones_split(const uint32_t *Pm, int M, int lo, in
 }
 
 /* recompute column m's prefix table (rows 0..NW) */
-__device__ __forceinline__ void col_pre_build(uint16_t *prem, const uint32_t *Pm, int M, int NW)
+__device__ __forceinline__ void col_pre_build(uint16_t *prem, const uint32_t *Pm, int M, int NW, int PS = 0)
 {
+  const int S = PS ? PS : M;
   int s = 0;
   for (int k0 = 0; k0 < NW; k0 += 8) {   /* 8 independent loads per round */
     uint32_t wv[8];
@@ -1791,11 +1801,11 @@ __device__ __forceinline__ void col_pre_build(uint16_t *prem, const uint32_t *Pm
     for (int t = 0; t < 8; ++t) wv[t] = Pm[min(k0 + t, NW - 1) * M];
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
-      if (k0 + t < NW) prem[(k0 + t) * M] = (uint16_t)s;
+      if (k0 + t < NW) prem[(k0 + t) * S] = (uint16_t)s;
       s += (k0 + t < NW) ? __popc(wv[t]) : 0;
     }
   }
-  prem[NW * M] = (uint16_t)s;
+  prem[NW * S] = (uint16_t)s;
 }
 
 __device__ __forceinline__ int ininterval(int i, int a, int b, int inc1, int inc2)   /* mcmc.c:1097-1124 */
@@ -2095,7 +2105,7 @@ __device__ __forceinline__ HM hard_bits_col(const uint32_t *Pm, int M, int hl, i
 template <typename HM>
 __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, const uint32_t *Pm, const uint16_t *prem,
                                          int M, HM hbm, const int16_t *hcnt, const int16_t *nhall, int &dt0, int &dt1,
-                                         const uint32_t *hbx, int N_)
+                                         const uint32_t *hbx, int N_, int PS = 0)
 {
   const int i = q.i, j = q.j;
   dt0 = 0; dt1 = 0;
@@ -2126,7 +2136,7 @@ __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, 
 #if SR_BF_TERMS
     {   /* branch-free: every lane reads the three prefixes, lanes with ain == bin keep zeros */
       const int sp = ain ? a : b;
-      const int c0 = col_pre_bf(prem, Pm, M, i), c1 = col_pre_bf(prem, Pm, M, sp), c2 = col_pre_bf(prem, Pm, M, j + 1);
+      const int c0 = col_pre_bf(prem, Pm, M, i, PS), c1 = col_pre_bf(prem, Pm, M, sp, PS), c2 = col_pre_bf(prem, Pm, M, j + 1, PS);
       const int O1 = c1 - c0, O2 = c2 - c1;
       const int Z1 = (sp - i) - O1, Z2 = (j + 1 - sp) - O2;
       const bool on = ain != bin;
@@ -2136,7 +2146,7 @@ __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, 
 #else
     if (ain != bin) {
       const int sp = ain ? a : b;
-      const int c0 = col_pre(prem, Pm, M, i), c1 = col_pre(prem, Pm, M, sp), c2 = col_pre(prem, Pm, M, j + 1);
+      const int c0 = col_pre(prem, Pm, M, i, PS), c1 = col_pre(prem, Pm, M, sp, PS), c2 = col_pre(prem, Pm, M, j + 1, PS);
       const int O1 = c1 - c0, O2 = c2 - c1;
       const int Z1 = (sp - i) - O1, Z2 = (j + 1 - sp) - O2;
       if (ain) { dt1 = O1 - O2; dt0 = Z2 - Z1; }
@@ -2185,24 +2195,24 @@ __device__ __forceinline__ void taxon_dt(int kind, const Prop &q, int a, int b, 
     const int sizeW = max(0, whi - wlo + 1);
     int onesI = 0, sizeI = 0;
 #if SR_BF_TERMS
-    const int onesW = (whi >= wlo) ? col_pre_bf(prem, Pm, M, max(whi + 1, 0)) - col_pre_bf(prem, Pm, M, wlo) : 0;
+    const int onesW = (whi >= wlo) ? col_pre_bf(prem, Pm, M, max(whi + 1, 0), PS) - col_pre_bf(prem, Pm, M, wlo, PS) : 0;
     {   /* branch-free: nhall indices and the positions read clamped into range, an empty rank range adds 0 */
       const bool on = s_lo < s_hi;
       const int pl = min(max((int)nhall[min(max(ri + q.Kn - s_hi, 0), N_ - 1)], 0), N_ - 1);
       const int ph = min(max((int)nhall[min(max(ri + q.Kn - s_lo - 1, 0), N_ - 1)], 0), N_ - 1);
       int hc;
       const int ho = hard_ones(pl, ph, hc);
-      const int oI = col_pre_bf(prem, Pm, M, ph + 1) - col_pre_bf(prem, Pm, M, pl) - ho;
+      const int oI = col_pre_bf(prem, Pm, M, ph + 1, PS) - col_pre_bf(prem, Pm, M, pl, PS) - ho;
       onesI = on ? oI : 0;
       sizeI = on ? s_hi - s_lo : 0;
     }
 #else
-    const int onesW = (whi >= wlo) ? col_pre(prem, Pm, M, whi + 1) - col_pre(prem, Pm, M, wlo) : 0;
+    const int onesW = (whi >= wlo) ? col_pre(prem, Pm, M, whi + 1, PS) - col_pre(prem, Pm, M, wlo, PS) : 0;
     if (s_lo < s_hi) {
       const int pl = nhall[ri + q.Kn - s_hi], ph = nhall[ri + q.Kn - s_lo - 1];
       int hc;
       const int ho = hard_ones(pl, ph, hc);
-      onesI = col_pre(prem, Pm, M, ph + 1) - col_pre(prem, Pm, M, pl) - ho;
+      onesI = col_pre(prem, Pm, M, ph + 1, PS) - col_pre(prem, Pm, M, pl, PS) - ho;
       sizeI = s_hi - s_lo;
     }
 #endif
@@ -2234,7 +2244,7 @@ __device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const i
                                               int hl, int nh, const int16_t *hcnt, const int16_t *nhall, const uint32_t *hbx,
                                               double *cb, int *cc, double *xs,
                                               int lane, int wave, int TB, XSync &&xsync, const double *kv = nullptr,
-                                              const double *kx = nullptr)
+                                              const double *kx = nullptr, int PS = 0)
 {
   constexpr int CH = PR ? 32 : 64;
   const bool ev = PR ? (lane & 1) == 0 : true;
@@ -2243,7 +2253,7 @@ __device__ __forceinline__ double sr_exact_delta(int kind, Prop q, CD K, const i
     int dt0 = 0, dt1 = 0;
     if (m < M && ev)
       taxon_dt(kind, q, sab[m], sab[M + m], P + m, pre + m, M, kind == PK_PI3 ? hard_bits_col<uint64_t>(P + m, M, hl, nh) : 0ull,
-               hcnt, nhall, dt0, dt1, hbx, N);
+               hcnt, nhall, dt0, dt1, hbx, N, PS);
     CD Km = K;
     if (kv && m < M) { Km.c = kv[m]; Km.d = kv[M + m]; Km.cc = kx[m]; Km.dd = kx[M + m]; }
     const double tv = (m < M && ev) ? qval(dt0, -dt0, dt1, -dt1, Km) : 0.0;
@@ -2343,9 +2353,11 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   const int olo = SP ? half * sr_sp_half(M) : 0, ohi = SP ? min(M, olo + sr_sp_half(M)) : M;   /* own taxa */
   const int mt = olo + tx;   /* own taxon, one-taxon-per-thread kernels */
   const int KTC = (M + sr_chunk(PR) - 1) / sr_chunk(PR);   /* exact-delta chunks */
-  constexpr bool LCK = SP && LK;   /* Gibbs checkpoints in LDS (split kernels whose layout fits them, SR_SP_LCK) */
+  constexpr bool LCK = SP && LK && !SR_SP_LPRE;   /* Gibbs checkpoints in LDS (split kernels whose layout fits them, SR_SP_LCK) */
+  constexpr bool LPRE = SP && LK && SR_SP_LPRE;   /* ... or the own half's column prefixes in LDS instead (SR_SP_LPRE) */
+  const int PS = LPRE ? sr_sp_half(M) : M;          /* the prefix table's stride */
   constexpr bool SHT = GM && SR_GM_SHARED;   /* block-shared hard-site / 4-step tables */
-  const Lay L = sr_layout(N, M, NW, TB, GM, PR, nh, LCK);
+  const Lay L = sr_layout(N, M, NW, TB, GM, PR, nh, SP && LK);
   double *tabs = (double *)(smem + L.tab);
   /* GM: the per-taxon arrays are the chain's HBM state itself (P, a/b, counts: updated in
      place) or its HBM scratch; otherwise LDS copies loaded here and stored at the end */
@@ -2355,7 +2367,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   uint32_t *P = GM ? A.P + (size_t)chain * NW * M : (uint32_t *)(smem + L.P);
   int32_t *rpiA = (int32_t *)(smem + L.rpi0);
   int32_t *rpiB = (int32_t *)(smem + L.rpi1);
-  uint16_t *pre = GM ? A.gpre + (size_t)chain * sr_gm_pre(M, NW) : (uint16_t *)(smem + L.pre);   /* column prefix ones */
+  uint16_t *pre = LPRE ? (uint16_t *)(smem + L.pre) - olo   /* (own taxa [olo, ohi) only) */
+                 : GM ? A.gpre + (size_t)chain * sr_gm_pre(M, NW) : (uint16_t *)(smem + L.pre);   /* column prefix ones */
   int16_t *hcnt = (int16_t *)(smem + L.ht) + (SHT ? 0 : wave) * (2 * N + 2);    /* this wave's (SHT: the block's) hard-site tables */
   int16_t *nhall = hcnt + N + 1;
   const int CKS = LCK ? TB : SP ? 2 * TB : sr_ckstride(M, TB);   /* SP: slots [half TB + tid] (LCK: [tid] in LDS) */
@@ -2458,7 +2471,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
   __syncthreads();
 
   build_hard_tables(hp, nh, N, NW, hbw, hcnt, nhall, lane, !SHT || wave == 0);   /* (SHT: read after the phase-A barrier) */
-  for (int m = olo + tid; m < ohi; m += TB) col_pre_build(pre + m, P + m, M, NW);   /* own columns */
+  for (int m = olo + tid; m < ohi; m += TB) col_pre_build(pre + m, P + m, M, NW, PS);   /* own columns */
   {
     const int hl0 = (lane < nh) ? hp[lane] : 0;   /* loaded with every lane active */
     if ((SP || M <= TXS) && mt < ohi) hbc = hard_bits_col<HM>(P + mt, M, hl0, nh);
@@ -2652,8 +2665,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
           int na = a0, nb = b0;
           if constexpr (PR) {   /* pair kernels: each lane of the pair walks half of the words */
             const uint16_t *prem = pre + m;
-            const int POa = col_pre(prem, Pm, M, a0);
-            const int POb = (int)prem[NW * M] - col_pre(prem, Pm, M, b0);
+            const int POa = col_pre(prem, Pm, M, a0, PS);
+            const int POb = (int)prem[NW * PS] - col_pre(prem, Pm, M, b0, PS);
             uint32_t wk[5];
             int d0, e0, d1, e1;
 #pragma unroll
@@ -2670,8 +2683,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             t0 += d0; f0 += e0; t1 += d1; f1 += e1;
           } else if constexpr (MCD) {   /* manycd: the taxon's own coefficients, the exact reference walk */
             const uint16_t *prem = pre + m;
-            const int POa = col_pre(prem, Pm, M, a0);
-            const int POb = (int)prem[NW * M] - col_pre(prem, Pm, M, b0);
+            const int POa = col_pre(prem, Pm, M, a0, PS);
+            const int POb = (int)prem[NW * PS] - col_pre(prem, Pm, M, b0, PS);
             CD Km = K;
             Km.c = cv[m]; Km.d = cv[M + m]; Km.cc = cx[m]; Km.dd = cx[M + m];
             for (int pass = 0; pass < 2; ++pass) {
@@ -2689,8 +2702,8 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             /* ones before each trip's start entry from the column prefix table: forward, positions
                [0, a0); reversed, walk entries [0, N - b0) = positions [b0, N) */
             const uint16_t *prem = pre + m;
-            const int POa = col_pre(prem, Pm, M, a0);
-            const int POb = (int)prem[NW * M] - col_pre(prem, Pm, M, b0);
+            const int POa = col_pre(prem, Pm, M, a0, PS);
+            const int POb = (int)prem[NW * PS] - col_pre(prem, Pm, M, b0, PS);
             for (int pass = 0; pass < 2; ++pass) {
               int d0, e0, d1, e1;
               const bool rev = pass != 0;
@@ -2714,13 +2727,13 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             }
           } else {
           const uint16_t *prem = pre + m;   /* ones before each trip's start entry, as above */
-          const int POa = col_pre(prem, Pm, M, a0);
-          const int POb = (int)prem[NW * M] - col_pre(prem, Pm, M, b0);
+          const int POa = col_pre(prem, Pm, M, a0, PS);
+          const int POb = (int)prem[NW * PS] - col_pre(prem, Pm, M, b0, PS);
           for (int pass = 0; pass < 2; ++pass) {
             int d0, e0, d1, e1;
             const bool rev = pass != 0;
             const int res = draw_fast<GM>(Pm, prem, M, N, NW, rev, rev ? N - b0 : a0, rev ? N - na : b0, rev ? POb : POa,
-                                      rev ? ub : ua, K, tb, vA, vB, rA, rB, T4w, T8w, ckb + ckslot, CKS, &misc[MS_FBK], d0, e0,
+                                      rev ? ub : ua, K, tb, vA, vB, rA, rB, T4w, T8w, ckb + ckslot, CKS, PS, &misc[MS_FBK], d0, e0,
                                       d1, e1 GSTAMP_PASS);
             GSTAMP_K4();
             t0 += d0; f0 += e0; t1 += d1; f1 += e1;
@@ -3075,7 +3088,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 q.Kn = hf ? qb.Kn : qa.Kn; q.r0 = hf ? qb.r0 : qa.r0;
                 int d0 = 0, d1 = 0;
                 if ((hf ? vb : va) && tx < M)
-                  taxon_dt(prop_kind(pa), q, a1, b1, P + tx, pre + tx, M, hb1, hcnt, nhall, d0, d1, hbx, N);
+                  taxon_dt(prop_kind(pa), q, a1, b1, P + tx, pre + tx, M, hb1, hcnt, nhall, d0, d1, hbx, N, PS);
                 int Xa0, Xa1, Ya, Xb0, Xb1, Yb;
                 if (prop_kind(pa) == PK_PI1) {   /* dt in {-1, 0, 1}, dt0 dt1 = 0: ballot counts per parity */
                   const uint64_t p0m = __ballot(d0 > 0), n0m = __ballot(d0 < 0);
@@ -3115,7 +3128,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               for (int sI = 1; sI < 16; ++sI) {
                 const Prop q = load_prop(sI);
                 int dt0 = 0, dt1 = 0;
-                taxon_dt(prop_kind(sI), q, a1, b1, P + mtc, pre + mtc, M, hb1, hcnt, nhall, dt0, dt1, hbx, N);
+                taxon_dt(prop_kind(sI), q, a1, b1, P + mtc, pre + mtc, M, hb1, hcnt, nhall, dt0, dt1, hbx, N, PS);
                 const bool use = mt < ohi && !vetoed(sI);
                 d0s[sI] = use ? dt0 : 0; d1s[sI] = use ? dt1 : 0;
               }
@@ -3126,7 +3139,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               if (sI >= p0 && sI < pend && !vetoed(sI)) {
                 const Prop q = load_prop(sI);
                 int dt0 = 0, dt1 = 0;
-                if (own) taxon_dt(prop_kind(sI), q, a1, b1, P + mt, pre + mt, M, hb1, hcnt, nhall, dt0, dt1, hbx, N);
+                if (own) taxon_dt(prop_kind(sI), q, a1, b1, P + mt, pre + mt, M, hb1, hcnt, nhall, dt0, dt1, hbx, N, PS);
                 d0s[sI] = dt0; d1s[sI] = dt1;
               }
             }
@@ -3137,7 +3150,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 if (sI >= p0 && sI < pend && !vetoed(sI)) {
                   const Prop q = load_prop(sI);
                   int dt0 = 0, dt1 = 0;
-                  if (mt < ohi) taxon_dt(prop_kind(sI), q, a1 + z, b1, P + mt, pre + mt, M, hb1, hcnt, nhall, dt0, dt1, hbx, N);
+                  if (mt < ohi) taxon_dt(prop_kind(sI), q, a1 + z, b1, P + mt, pre + mt, M, hb1, hcnt, nhall, dt0, dt1, hbx, N, PS);
                   d0s[sI] |= dt0 & z; d1s[sI] |= dt1 & z;
                 }
               }
@@ -3253,7 +3266,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 if (sI >= p0 && sI < pend && !vetoed(sI)) {
                   const Prop q = load_prop(sI);
                   int dt0 = 0, dt1 = 0;
-                  if (mv) taxon_dt(prop_kind(sI), q, a, b, P + m, pre + m, M, hb, hcnt, nhall, dt0, dt1, hbx, N);
+                  if (mv) taxon_dt(prop_kind(sI), q, a, b, P + m, pre + m, M, hb, hcnt, nhall, dt0, dt1, hbx, N, PS);
                   x0s[sI] += dt0; x1s[sI] += dt1; ys[sI] += abs(dt0) + abs(dt1);
                 }
               }
@@ -3343,7 +3356,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
               if constexpr (SP)
                 dl = sr_exact_delta<PR, GM, SP>(kind, q, K, sab, P, pre, M, N, KTC, olo, ohi, hl, nh, hcnt, nhall, hbx,
                                                 cbuf + xpar * KTC * sr_chunk(PR), xb + 272 + xpar * KTC, xs, lane, wave,
-                                                TB, xsync);
+                                                TB, xsync, nullptr, nullptr, PS);
               else   /* (no exchange: the one-workgroup kernels never see the split machinery) */
                 dl = sr_exact_delta<PR, GM, SP>(kind, q, K, sab, P, pre, M, N, KTC, 0, M, hl, nh, hcnt, nhall, hbx,
                                                 cbuf + xpar * KTC * sr_chunk(PR), ccnt + xpar * KTC, xs, lane, wave, TB,
@@ -3388,7 +3401,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             const int a = sab[m], b = sab[M + m];
             int dt0, dt1;
             taxon_dt(kind, q, a, b, Pm, prem, M, kind == PK_PI3 ? hard_bits_col<HM>(Pm, M, hl, nh) : (HM)0, hcnt, nhall, dt0, dt1,
-                     hbx, N);
+                     hbx, N, PS);
             /* every read of the taxon's state before its first write (the compiler cannot tell the LDS / HBM
                arrays apart, so a read after a write waits for it: one round trip instead of one per access) */
             const int k0 = scnt[m], k1 = scnt[M + m], k2 = scnt[2 * M + m], k3 = scnt[3 * M + m];
@@ -3406,7 +3419,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                 wv[t] = (w >= 0 && w < NW && w <= wh + 1) ? Pm[w * M] : 0u;
               }
               vb = (Pm[(i >> 5) * M] >> (i & 31)) & 1u;
-              sbase = prem[wl * M];
+              sbase = prem[wl * PS];
             }
             scnt[m] = k0 + dt0; scnt[M + m] = k1 - dt0; scnt[2 * M + m] = k2 + dt1; scnt[3 * M + m] = k3 - dt1;
             int na_ = a, nb_ = b;   /* HBM columns: the new limits, stored below when they change */
@@ -3431,7 +3444,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
                   uint32_t nw = (old & ~m1) | (sh & m1);
                   if ((j >> 5) == w) nw = (nw & ~(1u << (j & 31))) | (vb << (j & 31));
                   Pm[w * M] = nw;
-                  if (w < wh) { sacc += __popc(nw); prem[(w + 1) * M] = (uint16_t)sacc; }   /* prefix entries (lo/32, hi/32] */
+                  if (w < wh) { sacc += __popc(nw); prem[(w + 1) * PS] = (uint16_t)sacc; }   /* prefix entries (lo/32, hi/32] */
                 }
               }
             } else {
@@ -3503,14 +3516,14 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             }
             {   /* the move permutes positions [lo, hi] only: prefix entries (lo/32, hi/32] change */
               const int rlo = wl + 1, rhi = wh;
-              int sacc = prem[(rlo - 1) * M];
+              int sacc = prem[(rlo - 1) * PS];
               for (int r0 = rlo; r0 <= rhi; r0 += 8) {
                 uint32_t wv[8];
 #pragma unroll
                 for (int t = 0; t < 8; ++t) wv[t] = (r0 + t <= rhi) ? Pm[(r0 + t - 1) * M] : 0u;
 #pragma unroll
                 for (int t = 0; t < 8; ++t)
-                  if (r0 + t <= rhi) { sacc += __popc(wv[t]); prem[(r0 + t) * M] = (uint16_t)sacc; }
+                  if (r0 + t <= rhi) { sacc += __popc(wv[t]); prem[(r0 + t) * PS] = (uint16_t)sacc; }
               }
             }
             }
@@ -4035,7 +4048,7 @@ extern "C" int srk_create(const sr_state_host *st, int device, int block_threads
     CKT *gck = nullptr;
     /* (split kernels with their checkpoints in LDS: no HBM scratch) */
     rc |= dev_alloc_copy(d, &gck, (const CKT *)nullptr,
-                         C * (d->sp ? (d->lck ? 0 : sr_sp_ck(st->N, TB)) : sr_gm_ck(st->N, st->M, TB)));
+                         C * (d->sp ? ((d->lck && !SR_SP_LPRE) ? 0 : sr_sp_ck(st->N, TB)) : sr_gm_ck(st->N, st->M, TB)));
     A.gck = gck;
     rc |= dev_alloc_copy(d, &A.glbuf, (const double *)nullptr, C * st->M);
     rc |= dev_alloc_copy(d, &A.gcbuf, (const double *)nullptr, C * sr_gm_cbuf(st->M));
@@ -4492,7 +4505,7 @@ __global__ void __launch_bounds__(64) sr_gibbs_selftest_kernel(const uint32_t *P
     }
     res = draw_fast_s<NWM>(wk, Pm, M, N, rev, o, L, POo, u, K, tb, vA, vB, T4w, T8w, (uint64_t *)(fb + m), d0, e0, d1, e1);
   } else {
-    res = draw_fast<MODE == 3>(Pm, prem, M, N, NW, rev, o, L, POo, u, K, tb, vA, vB, rA, rB, T4w, T8w, cks + m, M,
+    res = draw_fast<MODE == 3>(Pm, prem, M, N, NW, rev, o, L, POo, u, K, tb, vA, vB, rA, rB, T4w, T8w, cks + m, M, 0,
                                (uint64_t *)(fb + m), d0, e0, d1, e1);
   }
   int *r = out + 5 * m;

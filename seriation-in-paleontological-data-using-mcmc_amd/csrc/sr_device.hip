@@ -129,6 +129,11 @@ struct KArgs {
 #ifndef SR_COOP_TABLES
 #define SR_COOP_TABLES 1
 #endif
+/* the register form of an accepted pi1 in the HBM-column kernels too (off: in round 5 its registers spilled 37 more
+   VGPRs there, r05l) */
+#ifndef SR_GM_APPLY_REG
+#define SR_GM_APPLY_REG 0
+#endif
 /* the proposal sums of a batch of at least this many proposals by one transposed reduction per wave
    (wave_sum32_t; 0 = one reduction per slot) */
 #ifndef SR_TSUMS
@@ -3408,7 +3413,7 @@ __global__ __launch_bounds__(TB) void sr_sweep_kernel(KArgs A)
             const int lo = min(i, j), hi = max(i, j), wl = lo >> 5, wh = hi >> 5;
             /* pi1 over at most 8 words (always at N <= 256): the words [wl - 1, wh + 1], the moved bit and the
                prefix below word wl read now; the shifted words and their prefix entries computed in registers */
-            const bool reg1 = SR_APPLY_REG && !GM && kind == PK_PI1 && wh - wl < 8;   /* (GM: registers, r05l) */
+            const bool reg1 = SR_APPLY_REG && (!GM || SR_GM_APPLY_REG) && kind == PK_PI1 && wh - wl < 8;   /* (GM: SR_GM_APPLY_REG) */
             uint32_t wv[10];
             uint32_t vb = 0u;
             int sbase = 0;

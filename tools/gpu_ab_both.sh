@@ -18,6 +18,7 @@ for rep in $(seq 1 $REPS); do
   timeout -k 10 200 python bench.py $C3 > "$OUT/c3_product_$rep.json" 2> "$OUT/c3_product_$rep.err" && show "$OUT/c3_product_$rep.json" "c3 product $rep" &&
   SERIATION_LIB=$VL timeout -k 10 200 python bench.py $C3 > "$OUT/c3_${v}_$rep.json" 2> "$OUT/c3_${v}_$rep.err" && show "$OUT/c3_${v}_$rep.json" "c3 $v $rep" || exit 1
 done
+[ -n "$NO_TESTS" ] && exit 0
 SERIATION_LIB=$VL timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
   tests/test_gpu_config5.py tests/test_gpu_fuzz.py > "$OUT/pytest_$v.log" 2>&1; rc=$?
 tail -3 "$OUT/pytest_$v.log"
